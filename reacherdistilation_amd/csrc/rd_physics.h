@@ -1,0 +1,167 @@
+// Reacher-v2 (gym 0.10.5 on MuJoCo 1.50) dynamics for gfx950: device-side, f32,
+// one environment per lane.  Restates what the reference's env.step()/env.reset()
+// execute inside mujoco-py (reference mlp_train.py:112,135,138,196,200 ->
+// gym ReacherEnv.step -> do_simulation(a, frame_skip=2) -> 2 x mj_step(RK4)).
+//
+// Model (pinned against src/distilation/tests/data/dataset.json):
+//   M(q1)   = [[A0+I2+2HC cos q1 + 1, I2 + HC cos q1], [., I2 + 1]]   (armature 1)
+//   bias    = HC sin q1 * [-(2 v0 v1 + v1^2), v0^2]                    (RNE)
+//   tau     = 200 clip(a,-1,1) - v - bias                               (gear, damping 1)
+//   joint-1 limit +-3: one soft constraint, solref (.02,1), solimp (.9,.95,.001),
+//   R = (1-d)/d * invweight0 -- solved exactly (scalar).
+//   RK4 (h = .01), kinematics left at the last stage (stale fingertip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rd {
+
+// ------------------------------------------------------------------ constants
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kMl = 1000.0 * kPi * 0.01 * 0.01 * 0.11;
+constexpr double kIc = kMl * (3 * 0.01 * 0.01 + 0.11 * 0.11) / 12.0;
+constexpr double kMf = 1000.0 * 4.0 / 3.0 * kPi * 0.01 * 0.01 * 0.01;
+constexpr double kIf = 0.4 * kMf * 0.01 * 0.01;
+constexpr double kA0 = kIc + kMl * 0.05 * 0.05 + (kMl + kMf) * 0.1 * 0.1;
+constexpr double kI2 = kIc + kMl * 0.05 * 0.05 + kIf + kMf * 0.11 * 0.11;
+constexpr double kHC = 0.1 * (kMl * 0.05 + kMf * 0.11);
+constexpr double kM110 = kA0 + kI2 + 2 * kHC + 1.0;
+constexpr double kM120 = kI2 + kHC;
+constexpr double kM220 = kI2 + 1.0;
+constexpr double kInvW0 = kM110 / (kM110 * kM220 - kM120 * kM120);
+constexpr double kBref = 2.0 / (0.95 * 0.02);
+constexpr double kKref = 1.0 / (0.95 * 0.95 * 0.02 * 0.02);
+
+constexpr int kEpisodeSteps = 50;   // gym TimeLimit (reference config.py:17 EPISODE_STEPS)
+constexpr int kObsDim = 11;         // reference config.py:19 OBSPACE_SHAPE
+constexpr int kActDim = 2;          // reference config.py:20 ACSPACE_SHAPE
+constexpr int kStateDim = 8;        // q0 q1 v0 v1 tx ty dx dy (SoA rows)
+
+struct State {
+    float q0, q1, v0, v1, tx, ty, dx, dy;   // (dx,dy) = fingertip - target at the held kinematics
+};
+
+__device__ __forceinline__ void sincos_acc(float x, float* s, float* c) { sincosf(x, s, c); }
+
+// One MuJoCo forward pass -> constrained qacc of the two arm dofs.
+__device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, float c1,
+                                     float& a0, float& a1) {
+    const float A0 = (float)kA0, I2 = (float)kI2, HC = (float)kHC;
+    float s, c;
+    sincos_acc(q1, &s, &c);
+    const float m11 = A0 + I2 + 2.0f * HC * c + 1.0f;
+    const float m12 = I2 + HC * c;
+    const float m22 = I2 + 1.0f;
+    const float b0 = -HC * s * (2.0f * v0 * v1 + v1 * v1);
+    const float b1 = HC * s * v0 * v0;
+    const float t0 = 200.0f * c0 - v0 - b0;
+    const float t1 = 200.0f * c1 - v1 - b1;
+    const float rdet = 1.0f / (m11 * m22 - m12 * m12);
+    const float i11 = m22 * rdet, i12 = -m12 * rdet, i22 = m11 * rdet;
+    a0 = i11 * t0 + i12 * t1;
+    a1 = i12 * t0 + i22 * t1;
+    const float lower = q1 + 3.0f, upper = 3.0f - q1;
+    if (lower < 0.0f || upper < 0.0f) {               // rare: joint-1 limit active
+        const bool lo = lower < 0.0f;
+        const float dist = lo ? lower : upper;
+        const float J = lo ? 1.0f : -1.0f;
+        const float x = fminf(fabsf(dist) * 1000.0f, 1.0f);
+        const float y = x <= 0.5f ? 2.0f * x * x : 1.0f - 2.0f * (1.0f - x) * (1.0f - x);
+        const float d = 0.9f + y * 0.05f;
+        const float aref = -(float)kBref * (J * v1) - (float)kKref * d * dist;
+        const float R = (1.0f - d) / d * (float)kInvW0;
+        const float f = fmaxf(0.0f, (aref - J * a1) / (i22 + R));
+        a0 += i12 * J * f;
+        a1 += i22 * J * f;
+    }
+}
+
+// env.step on one env: returns the reward (computed from the held stale fingertip,
+// float32 ctrl cost of the UNCLIPPED action), advances the state by 2 RK4 substeps.
+__device__ __forceinline__ float env_step(State& st, float a0, float a1) {
+    const float h = 0.01f;
+    const float r = -sqrtf(st.dx * st.dx + st.dy * st.dy) - (a0 * a0 + a1 * a1);
+    const float c0 = fminf(fmaxf(a0, -1.0f), 1.0f);   // ctrlrange +-1 (ctrllimited)
+    const float c1 = fminf(fmaxf(a1, -1.0f), 1.0f);
+    float q0 = st.q0, q1 = st.q1, v0 = st.v0, v1 = st.v1;
+    float kq0 = q0, kq1 = q1;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+        float k1a, k1b, k2a, k2b, k3a, k3b, k4a, k4b;
+        qacc(q1, v0, v1, c0, c1, k1a, k1b);
+        const float v0b = v0 + h * (0.5f * k1a), v1b = v1 + h * (0.5f * k1b);
+        qacc(q1 + h * (0.5f * v1), v0b, v1b, c0, c1, k2a, k2b);
+        const float v0c = v0 + h * (0.5f * k2a), v1c = v1 + h * (0.5f * k2b);
+        qacc(q1 + h * (0.5f * v1b), v0c, v1c, c0, c1, k3a, k3b);
+        const float v0d = v0 + h * k3a, v1d = v1 + h * k3b;
+        kq0 = q0 + h * v0c;
+        kq1 = q1 + h * v1c;
+        qacc(kq1, v0d, v1d, c0, c1, k4a, k4b);
+        const float b1 = 1.0f / 6.0f, b2 = 1.0f / 3.0f;
+        q0 += h * (v0 * b1 + v0b * b2 + v0c * b2 + v0d * b1);
+        q1 += h * (v1 * b1 + v1b * b2 + v1c * b2 + v1d * b1);
+        v0 += h * (k1a * b1 + k2a * b2 + k3a * b2 + k4a * b1);
+        v1 += h * (k1b * b1 + k2b * b2 + k3b * b2 + k4b * b1);
+    }
+    float s0, c0k, s01, c01;
+    sincos_acc(kq0, &s0, &c0k);
+    sincos_acc(kq0 + kq1, &s01, &c01);
+    st.q0 = q0; st.q1 = q1; st.v0 = v0; st.v1 = v1;
+    st.dx = 0.1f * c0k + 0.11f * c01 - st.tx;
+    st.dy = 0.1f * s0 + 0.11f * s01 - st.ty;
+    return r;
+}
+
+// reset_model + set_state + sim.forward(): kinematics fresh at the reset position.
+__device__ __forceinline__ void env_reset(State& st, const float* d /*q0 q1 v0 v1 tx ty*/) {
+    st.q0 = d[0]; st.q1 = d[1]; st.v0 = d[2]; st.v1 = d[3]; st.tx = d[4]; st.ty = d[5];
+    float s0, c0, s01, c01;
+    sincos_acc(st.q0, &s0, &c0);
+    sincos_acc(st.q0 + st.q1, &s01, &c01);
+    st.dx = 0.1f * c0 + 0.11f * c01 - st.tx;
+    st.dy = 0.1f * s0 + 0.11f * s01 - st.ty;
+}
+
+// gym ReacherEnv._get_obs: [cos q, sin q, target, qvel, fingertip - target (x,y,0)]
+__device__ __forceinline__ void observe(const State& st, float* ob) {
+    float s0, c0, s1, c1;
+    sincos_acc(st.q0, &s0, &c0);
+    sincos_acc(st.q1, &s1, &c1);
+    ob[0] = c0; ob[1] = c1; ob[2] = s0; ob[3] = s1;
+    ob[4] = st.tx; ob[5] = st.ty; ob[6] = st.v0; ob[7] = st.v1;
+    ob[8] = st.dx; ob[9] = st.dy; ob[10] = 0.0f;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+// Synthetic reset stream: key = seed, counter = (env_id lo, env_id hi, episode, block).
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                       uint32_t k0, uint32_t k1, uint32_t out[4]) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// draws (q0,q1,v0,v1,tx,ty) with ReacherEnv.reset_model's ranges
+__device__ __forceinline__ void philox_draw(uint64_t seed, uint64_t env_id, uint32_t episode, float d[6]) {
+    uint32_t o[4], p[4];
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    philox((uint32_t)env_id, (uint32_t)(env_id >> 32), episode, 0u, k0, k1, o);
+    philox((uint32_t)env_id, (uint32_t)(env_id >> 32), episode, 1u, k0, k1, p);
+    d[0] = __fmaf_rn(0.2f, u01(o[0]), -0.1f);
+    d[1] = __fmaf_rn(0.2f, u01(o[1]), -0.1f);
+    d[2] = __fmaf_rn(0.01f, u01(o[2]), -0.005f);
+    d[3] = __fmaf_rn(0.01f, u01(o[3]), -0.005f);
+    d[4] = __fmaf_rn(0.4f, u01(p[0]), -0.2f);
+    d[5] = __fmaf_rn(0.4f, u01(p[1]), -0.2f);
+}
+
+}  // namespace rd
