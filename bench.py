@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: batched Reacher-v2 rollout + distillation step on MI355X.
+
+One "step" = one lockstep env-step of every env on every rank, fused with its teacher
+query, student forward/backward, distillation loss and one TF1 Adam step (+ one RCCL
+all-reduce of the 5060-float student gradient when N > 1) -- the reference's hot-loop
+iteration (mlp_train.py:143-204) batched.  Unit: env-steps/s summed over all ranks.
+
+  python bench.py [--gpus N --steps K --warmup W --workload c4|c2|c3|c5 --envs-per-gpu E]
+  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Default workload: BASELINE config 4's 262,144 envs on EVERY GPU
+(weak scaling: per-GPU work fixed as N grows), teacher-driven, MSE, fp32 -- the metric is
+quoted at 1/2/4/8 MI355X, which is config 4.  Rank 0 prints one JSON line, with a
+`roofline` object for the dominant kernel (rollout_kernel, timed with HIP events on its
+stream inside the timed region) and a `cpu_baseline` (the C f32 restatement, OpenMP, on a
+bounded sample; rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Reacher env-steps/sec (rollout+distill step) at 1/2/4/8 MI355X; student MSE"
+# algorithmic work per env-step of the fused step: FLOPs of the
+# GEMM-shaped parts (teacher fwd 9,856 + student fwd 9,856 + student bwd 18,304)
+FLOP_PER_ENV_STEP = 2 * (11 * 64 + 64 * 64 + 64 * 2) * 2 + 2 * (64 * 2 * 2 + 64 * 64 * 2 + 11 * 64)
+# HBM bytes per env-step of rollout_kernel: read state 32 B, write q, v, dx, dy 24 B
+BYTES_PER_ENV_STEP = 56
+PEAK_F32_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (dense)
+PEAK_HBM_GBS = 8000.0
+
+WORKLOADS = {
+    "c2": dict(envs=4096, loss="mse", act_with="teacher",
+               desc="BASELINE config 2: 4,096 envs/GPU, 2x64 tanh MlpPolicy student, MSE, fp32"),
+    "c3": dict(envs=65536, loss="kl", act_with="teacher",
+               desc="BASELINE config 3: 65,536 envs/GPU, Gaussian KL(s||t) distillation, fp32"),
+    "c4": dict(envs=262144, loss="mse", act_with="teacher",
+               desc="BASELINE config 4: 262,144 envs per GPU, RCCL student-grad all-reduce, MSE, fp32"),
+    "c5": dict(envs=131072, loss="mse", act_with="student",
+               desc="BASELINE config 5 shard: DAgger (student acts, teacher relabels), 131,072 envs/GPU, MSE"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--envs-per-gpu", type=int, default=0)
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline(workload, seconds, threads):
+    """Time the oracle's C f32 rollout+distill step (OpenMP) on a bounded sample."""
+    import numpy as np
+
+    from oracle import ref_c
+    from reacherdistilation_amd.policy import student_init, synthetic_teacher
+    n = 4096
+    t, s = synthetic_teacher(1), student_init(2)
+    state = ref_c.philox_reset(n, 0, 0, 0)
+    threads = threads or min(16, os.cpu_count() or 1)
+    P = ref_c.param_count()
+    m = np.zeros(P, np.float32); v = np.zeros(P, np.float32)
+    sp = s.flat.copy()
+    steps = 0
+    b1p, b2p = 0.9, 0.999
+    t0 = time.perf_counter()
+    while True:
+        g, _ = ref_c.distill_step(state, steps, (t.flat, t.ob_mean, t.ob_std), (sp, s.ob_mean, s.ob_std),
+                                  loss=workload["loss"], act_student=workload["act_with"] == "student",
+                                  nthreads=threads)
+        ref_c.adam_tf1(sp, m, v, g, b1p, b2p)
+        b1p *= 0.9; b2p *= 0.999
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=n * steps / el, unit="env-steps/s", cores=threads, kind="port",
+                sample=f"{n} envs x {steps} steps ({el:.1f} s), same step (env + teacher + student fwd/bwd "
+                       f"+ {workload['loss']} + TF1 Adam), C f32 restatement oracle/reacher_ref.c, "
+                       f"OpenMP {threads} threads")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    wl = WORKLOADS[args.workload]
+    n = args.envs_per_gpu or wl["envs"]
+    cfg = DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr)
+    tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world)
+
+    def one_step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        tr.launch(tr.STAGE_ROLLOUT)
+        if ev is not None:
+            ev[1].record()
+        if world == 1:
+            tr.launch(tr.STAGE_REDUCE_APPLY)
+        else:
+            tr.launch(tr.STAGE_REDUCE)
+            tr.allreduce_grad()
+            tr.launch(tr.STAGE_APPLY)
+
+    for _ in range(args.warmup):
+        one_step()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # student action-MSE vs teacher over the last steps (all ranks)
+    met = tr.metrics(min(10, tr.counter()))
+    mt = torch.tensor(met.sum(0), dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(mt)
+    mse = float(mt[2] / (2 * mt[3]))
+
+    if rank == 0:
+        ms = elapsed * 1e3 / args.steps
+        value = n * world * args.steps / elapsed
+        launch_s = kern_ms * 1e-3
+        achieved = FLOP_PER_ENV_STEP * n / launch_s / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}.json")
+        if os.path.exists(pmc):
+            with open(pmc) as fh:
+                traffic = json.load(fh).get("hbm_bytes_per_launch")
+        out = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: Philox(seed 0) Reacher-v2 resets, seeded synthetic teacher (normc, fixture logstd) "
+                    "and student (2x64 MlpPolicy)",
+            "config": {"workload": args.workload, "description": wl["desc"], "envs_per_gpu": n,
+                       "envs_total": n * world, "student": "MlpPolicy 2x64 tanh (5060 params)",
+                       "teacher": "MlpPolicy 2x64 tanh", "loss": wl["loss"], "act_with": wl["act_with"],
+                       "optimizer": f"TF1 Adam lr {args.lr}, 1 step per env-step",
+                       "parallelism": f"dp{world}"},
+            "student_mse": mse,
+            "roofline": {"kernel": "rollout_kernel", "bound": "mfma", "achieved": achieved,
+                         "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS,
+                         "traffic": traffic, "flop_per_env_step": FLOP_PER_ENV_STEP,
+                         "launch_us": kern_ms * 1e3,
+                         "hbm_gbs_algorithmic": BYTES_PER_ENV_STEP * n / launch_s / 1e9},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

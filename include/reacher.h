@@ -44,6 +44,8 @@ typedef struct rd_env rd_env;
 int rd_create(rd_env** out, int64_t n_envs, int64_t env_base, uint64_t seed, int device,
               void* hip_stream);
 int rd_destroy(rd_env* env);
+/* Subsequent launches go to `hip_stream` (e.g. a graph-capture stream). */
+int rd_set_stream(rd_env* env, void* hip_stream);
 
 /* env.reset() for all N envs (episode counter += 1 after the first reset). */
 int rd_reset(rd_env* env, float* obs);

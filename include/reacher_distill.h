@@ -1,0 +1,103 @@
+/* reacher_distill.h -- C ABI of the fused rollout + distillation step (libreacher.so).
+ *
+ * One rdd_step() is one iteration of the reference's hot loop, batched over N envs in
+ * lockstep on one GPU (reference mlp_train.py:143-204, phase 2; the batched on-policy
+ * form of backup/student_rollout.py:618-740 train_student):
+ *   teacher query      sess.run(teacher.pi.pd.flat | ob)        mlp_train.py:165-167
+ *   student forward    student graph on the observation          mlp_train.py:38-66,173-186
+ *   distillation loss  kl_loss(s_pdflat, t_pdflat) (loss.py:3-13) or action-MSE
+ *   optimiser          AdamOptimizer(lr,.9,.999,1e-8).minimize    mlp_train.py:73-80,148-161
+ *   env.step           with the teacher mean (teacher-driven) or the student mean
+ *                      (DAgger, mlp_train.py:196)                  + auto-reset at 50 steps
+ * The policy is baselines' MlpPolicy(hid_size=64, num_hid_layers=2) for both teacher
+ * (reference teacher.py:14-16) and student; flat parameter layout (P = 5060 floats):
+ *   W1[11][64] | b1[64] | W2[64][64] | b2[64] | W3[64][2] | b3[2] | logstd[2]
+ * plus a fixed observation filter (mean[11], std[11]) per network:
+ *   obz = clip((ob - mean) / std, -5, 5).
+ *
+ * Conventions as in reacher.h: device pointers, asynchronous on the handle's stream, no
+ * host sync except rdd_read_metrics / rdd_get_counter; 0 = OK, RD_EINVAL, -(hipError_t).
+ *
+ * Multi-GPU (one process per GPU, envs sharded contiguously): per step call
+ * rdd_rollout(), all-reduce(SUM) rdd_grad_buffer() across ranks (RCCL), then rdd_apply().
+ * Single GPU: rdd_step() == rdd_rollout() + rdd_apply() fused into two kernels.
+ */
+#ifndef REACHER_DISTILL_H
+#define REACHER_DISTILL_H
+#include <stdint.h>
+
+#include "reacher.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RDD_LOSS_MSE 0      /* mean((mu_s - mu_t)^2) over [N_global, 2] (BASELINE configs 2, 5) */
+#define RDD_LOSS_KL 1       /* sum over envs of KL(s||t), reference loss.py:3-13 (config 3)    */
+#define RDD_ACT_TEACHER 0   /* env stepped with the teacher mean (configs 2-4)               */
+#define RDD_ACT_STUDENT 1   /* env stepped with the student mean: DAgger (config 5)          */
+
+typedef struct {
+    int64_t n_envs;          /* envs on this rank                                   */
+    int64_t n_envs_global;   /* envs over all ranks (MSE normalisation)             */
+    int64_t env_base;        /* global id of this rank's env 0 (Philox stream key)   */
+    uint64_t seed;           /* Philox reset seed                                   */
+    int32_t loss;            /* RDD_LOSS_*                                          */
+    int32_t act_with;        /* RDD_ACT_*                                           */
+    float lr, beta1, beta2, eps;   /* Adam (reference: 1e-4, .9, .999, 1e-8)         */
+    int32_t grid;            /* rollout workgroups; 0 = auto (<= one per CU)          */
+    int32_t metrics_len;     /* ring length of the per-step metrics history; 0 = 4096 */
+} rdd_config;
+
+typedef struct rdd_trainer rdd_trainer;
+
+int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_stream);
+int rdd_destroy(rdd_trainer* tr);
+int rdd_param_count(void);
+/* Subsequent launches go to `hip_stream` (e.g. a graph-capture stream). */
+int rdd_set_stream(rdd_trainer* tr, void* hip_stream);
+
+/* Copy network parameters in (device pointers; params [P], ob_mean/ob_std [11]). */
+int rdd_set_teacher(rdd_trainer* tr, const float* params, const float* ob_mean, const float* ob_std);
+int rdd_set_student(rdd_trainer* tr, const float* params, const float* ob_mean, const float* ob_std);
+int rdd_get_student(rdd_trainer* tr, float* params);
+
+/* Envs <- Philox episode-0 resets, step counter <- 0, Adam moments/powers <- initial. */
+int rdd_reset(rdd_trainer* tr);
+
+/* The step: rollout (env + teacher + student fwd/bwd + loss, per-workgroup gradient
+ * partials) and reduction into rdd_grad_buffer(); rdd_apply(): TF1 Adam + counter++. */
+int rdd_rollout(rdd_trainer* tr);
+int rdd_apply(rdd_trainer* tr);
+int rdd_step(rdd_trainer* tr);
+/* The same work as individual launches (for per-kernel timing with events in between):
+ * RDD_STAGE_ROLLOUT = the fused rollout kernel only; RDD_STAGE_REDUCE = partials -> grad;
+ * RDD_STAGE_APPLY = Adam + counter; RDD_STAGE_REDUCE_APPLY = both in one launch.
+ * rdd_step == ROLLOUT then REDUCE_APPLY. */
+#define RDD_STAGE_ROLLOUT 1
+#define RDD_STAGE_REDUCE 2
+#define RDD_STAGE_APPLY 3
+#define RDD_STAGE_REDUCE_APPLY 4
+int rdd_launch_stage(rdd_trainer* tr, int stage);
+float* rdd_grad_buffer(rdd_trainer* tr);   /* device [P], valid after rdd_rollout */
+/* Use a caller-owned device buffer [P] as the gradient buffer (e.g. a torch tensor that
+ * the host all-reduces in place with RCCL); NULL restores the trainer's own buffer. */
+int rdd_bind_grad_buffer(rdd_trainer* tr, float* grad);
+
+/* Policy query without stepping (teacher.pi.pd.flat / student pdflat):
+ * obs [n][11] -> t_pdflat, s_pdflat [n][4] (either output may be NULL). */
+int rdd_forward(rdd_trainer* tr, const float* obs, int64_t n, float* t_pdflat, float* s_pdflat);
+
+/* Env state hooks (state [8][n_envs] SoA, see reacher.h). */
+int rdd_get_env_state(rdd_trainer* tr, float* state);
+int rdd_set_env_state(rdd_trainer* tr, const float* state);
+
+/* Host-synchronising readers.  Metrics per completed step s (ring of metrics_len):
+ * {sum reward, loss, sum (mu_s - mu_t)^2, envs}; out [count][4] for the last `count` steps. */
+int rdd_get_counter(rdd_trainer* tr, int64_t* steps);
+int rdd_read_metrics(rdd_trainer* tr, int64_t count, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,115 @@
+"""ORACLE (test infrastructure only) -- numpy restatement of the policy side of the hot path.
+
+  teacher query  baselines ppo1 MlpPolicy(hid_size=64, num_hid_layers=2) pol branch
+                 (reference teacher.py:14-16; queried at mlp_train.py:123-125,165-167):
+                 obz = clip((ob - mean) / std, -5, 5); h1 = tanh(obz W1 + b1);
+                 h2 = tanh(h1 W2 + b2); mean = h2 W3 + b3; pdflat = [mean, logstd]
+  student        the same 2x64 MlpPolicy structure (BASELINE configs 2-5; reference
+                 backup/student_rollout.py:79-87 StudentAgent), logstd trainable
+  loss           kl_loss (reference loss.py:3-13): sum over envs and action dims of
+                 KL(s||t) = lt - ls + (es^2 + (ms - mt)^2) / (2 et^2) - 1/2, or the BASELINE
+                 action-MSE mean((ms - mt)^2) over [N, 2]
+  optimiser      tf.train.AdamOptimizer(1e-4, .9, .999, 1e-8) (reference mlp_train.py:73-80),
+                 TF1 ApplyAdam functor: m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2);
+                 var -= m * lr*sqrt(1 - b2^t)/(1 - b1^t) / (sqrt(v) + eps), with
+                 beta1_power/beta2_power float32 variables multiplied once per step.
+
+Parity status: UNPINNED beyond the formulas -- TensorFlow/baselines are not installed and
+the reference has no test for this math.  Gradients are checked against
+finite differences in tests/test_policy_oracle.py.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+OBD, HID, ACD = 11, 64, 2
+# flat parameter layout (shared with the HIP kernel and the C oracle)
+P_W1 = 0
+P_B1 = P_W1 + OBD * HID
+P_W2 = P_B1 + HID
+P_B2 = P_W2 + HID * HID
+P_W3 = P_B2 + HID
+P_B3 = P_W3 + HID * ACD
+P_LS = P_B3 + ACD
+P_TOT = P_LS + ACD  # 5060
+
+
+def unpack(p):
+    return dict(W1=p[P_W1:P_B1].reshape(OBD, HID), b1=p[P_B1:P_W2], W2=p[P_W2:P_B2].reshape(HID, HID),
+                b2=p[P_B2:P_W3], W3=p[P_W3:P_B3].reshape(HID, ACD), b3=p[P_B3:P_LS], ls=p[P_LS:P_TOT])
+
+
+def pack(W1, b1, W2, b2, W3, b3, ls):
+    return np.concatenate([np.ravel(x) for x in (W1, b1, W2, b2, W3, b3, ls)])
+
+
+def forward(p, obmu, obsd, ob):
+    """ob [N,11] -> dict(z, h1, h2, mean [N,2], logstd [2])."""
+    q = unpack(p)
+    z = np.clip((ob - obmu) / obsd, -5.0, 5.0)
+    h1 = np.tanh(z @ q["W1"] + q["b1"])
+    h2 = np.tanh(h1 @ q["W2"] + q["b2"])
+    mean = h2 @ q["W3"] + q["b3"]
+    return dict(z=z, h1=h1, h2=h2, mean=mean, logstd=q["ls"])
+
+
+def loss_and_dmean(fs, ft, loss, n_global):
+    """Returns (loss, dL/dmean_s [N,2], dL/dlogstd_s [2], sum sq action error)."""
+    diff = fs["mean"] - ft["mean"]
+    sq = float((diff ** 2).sum())
+    if loss == "mse":
+        return sq / (2.0 * n_global), diff / n_global, np.zeros(ACD), sq
+    lt, ls = ft["logstd"], fs["logstd"]
+    vt, vs = np.exp(2 * lt), np.exp(2 * ls)
+    kl = (lt - ls + (vs + diff ** 2) / (2 * vt) - 0.5).sum()
+    dls = (vs / vt - 1.0) * diff.shape[0]
+    return float(kl), diff / vt, dls, sq
+
+
+def backward(p, fs, dmean, dls):
+    q = unpack(p)
+    g = dict(W3=fs["h2"].T @ dmean, b3=dmean.sum(0), ls=np.asarray(dls, np.float64))
+    dz2 = (dmean @ q["W3"].T) * (1 - fs["h2"] ** 2)
+    g["W2"] = fs["h1"].T @ dz2
+    g["b2"] = dz2.sum(0)
+    dz1 = (dz2 @ q["W2"].T) * (1 - fs["h1"] ** 2)
+    g["W1"] = fs["z"].T @ dz1
+    g["b1"] = dz1.sum(0)
+    return pack(g["W1"], g["b1"], g["W2"], g["b2"], g["W3"], g["b3"], g["ls"])
+
+
+def loss_fn(sp, smu, ssd, tp, tmu, tsd, ob, loss, n_global):
+    fs, ft = forward(sp, smu, ssd, ob), forward(tp, tmu, tsd, ob)
+    return loss_and_dmean(fs, ft, loss, n_global)[0]
+
+
+class AdamTF1:
+    """tf.train.AdamOptimizer as the reference builds it (mlp_train.py:73-80)."""
+
+    def __init__(self, n, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8, dtype=np.float32):
+        self.lr, self.b1, self.b2, self.eps = dtype(lr), dtype(b1), dtype(b2), dtype(eps)
+        self.m = np.zeros(n, dtype)
+        self.v = np.zeros(n, dtype)
+        self.b1p, self.b2p = dtype(b1), dtype(b2)   # beta powers start at beta (t = 1)
+        self.dtype = dtype
+        self.t = 0
+
+    def step(self, var, g):
+        d = self.dtype
+        g = g.astype(d)
+        one = d(1)
+        alpha = self.lr * np.sqrt(one - self.b2p) / (one - self.b1p)
+        self.m += (g - self.m) * (one - self.b1)
+        self.v += (g * g - self.v) * (one - self.b2)
+        var -= (self.m * alpha) / (np.sqrt(self.v) + self.eps)
+        self.b1p = d(self.b1p * self.b1)
+        self.b2p = d(self.b2p * self.b2)
+        self.t += 1
+        return var
+
+
+def normc(rng, shape, std):
+    """baselines.common.tf_util.normc_initializer."""
+    out = rng.standard_normal(shape).astype(np.float32)
+    out *= std / np.sqrt(np.square(out).sum(axis=0, keepdims=True))
+    return out

@@ -175,15 +175,16 @@ static void mlp_bwd(const float* p, const fwd_t* f, const float* dmean, const fl
         for (int j = 0; j < HID; ++j) g[P_W1 + k * HID + j] += f->z[k] * dz1[j];
 }
 
-/* TF1 ApplyAdam over a flat buffer; t is the 1-based step. */
-void rdo_adam_tf1(int64_t n, float* theta, float* m, float* v, const float* g, int64_t t,
+/* TF1 ApplyAdam functor (tensorflow/core/kernels/training_ops.cc) over a flat buffer:
+ *   alpha = lr*sqrt(1-b2p)/(1-b1p); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
+ *   var -= m*alpha/(sqrt(v)+eps).  b1p/b2p are the float32 beta powers for this step. */
+void rdo_adam_tf1(int64_t n, float* theta, float* m, float* v, const float* g, float b1p, float b2p,
                   float lr, float b1, float b2, float eps) {
-    double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, (double)t)) / (1.0 - pow((double)b1, (double)t));
-    float lrt = (float)lr_t;
+    const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
     for (int64_t i = 0; i < n; ++i) {
-        m[i] = b1 * m[i] + (1.f - b1) * g[i];
-        v[i] = b2 * v[i] + (1.f - b2) * g[i] * g[i];
-        theta[i] -= lrt * m[i] / (sqrtf(v[i]) + eps);
+        m[i] += (g[i] - m[i]) * (1.f - b1);
+        v[i] += (g[i] * g[i] - v[i]) * (1.f - b2);
+        theta[i] -= (m[i] * alpha) / (sqrtf(v[i]) + eps);
     }
 }
 

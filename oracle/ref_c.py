@@ -36,8 +36,8 @@ def lib():
         L.rdo_philox_reset.argtypes = [I64, I64, ctypes.c_uint64, ctypes.c_uint32, P]
         L.rdo_distill_step.argtypes = [I64, I64, I64, ctypes.c_uint64, I64, P, P, P, P, P, P, P,
                                        ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int]
-        L.rdo_adam_tf1.argtypes = [I64, P, P, P, P, I64, ctypes.c_float, ctypes.c_float,
-                                   ctypes.c_float, ctypes.c_float]
+        L.rdo_adam_tf1.argtypes = [I64, P, P, P, P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                   ctypes.c_float, ctypes.c_float, ctypes.c_float]
         L.rdo_constants.argtypes = [P]
         L.rdo_param_count.restype = ctypes.c_int
         _lib = L
@@ -104,6 +104,7 @@ def distill_step(state, step, teacher, student, *, seed=0, loss="mse", act_stude
     return grad, met
 
 
-def adam_tf1(theta, m, v, g, t, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8):
+def adam_tf1(theta, m, v, g, b1p, b2p, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8):
+    """One TF1 ApplyAdam; b1p/b2p = float32 beta powers of this step (b1**t, b2**t)."""
     lib().rdo_adam_tf1(theta.size, _p(theta), _p(m), _p(v), _p(np.ascontiguousarray(g, np.float32)),
-                       t, lr, b1, b2, eps)
+                       b1p, b2p, lr, b1, b2, eps)

@@ -30,6 +30,7 @@ SIGNATURES = {
     # reacher.h
     "rd_create": (INT, [ctypes.POINTER(P), I64, I64, U64, INT, P]),
     "rd_destroy": (INT, [P]),
+    "rd_set_stream": (INT, [P, P]),
     "rd_reset": (INT, [P, P]),
     "rd_step": (INT, [P, P, P, P, P]),
     "rd_set_state": (INT, [P, P, I32, I32]),

@@ -176,6 +176,12 @@ int rd_create(rd_env** out, int64_t n_envs, int64_t env_base, uint64_t seed, int
     return RD_OK;
 }
 
+int rd_set_stream(rd_env* e, void* hip_stream) {
+    if (!e) return rd::set_error(RD_EINVAL, "rd_set_stream: null handle");
+    e->stream = (hipStream_t)hip_stream;
+    return RD_OK;
+}
+
 int rd_destroy(rd_env* e) {
     if (!e) return RD_OK;
     rd::DeviceGuard g(e->device);

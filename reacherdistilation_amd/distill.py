@@ -1,0 +1,218 @@
+"""Host driver of the fused rollout + distillation step (include/reacher_distill.h).
+
+``DistillTrainer`` is the batched, device-resident form of the reference's MLP DAgger loop
+(reference mlp_train.py:18-204): per step it queries the teacher, runs the student
+forward/backward against the distillation loss (kl_loss, reference loss.py:3-13, or
+action-MSE), takes one TF1 Adam step (mlp_train.py:73-80) and steps N Reacher-v2 envs
+with the teacher mean (configs 2-4) or the student mean (DAgger, config 5).
+
+Multi-GPU: one process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm), envs
+sharded contiguously; the only exchange is one all_reduce(SUM) of the flat 5060-float
+student gradient per optimiser step.  Student weights start identical on every rank
+(same seed) and stay identical because every rank applies the same reduced gradient.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .policy import P_TOT, MlpPolicyParams, student_init, synthetic_teacher
+
+P = nat.P
+I32, I64, U64, F32, INT = nat.I32, nat.I64, nat.U64, nat.F32, nat.INT
+
+LOSSES = {"mse": 0, "kl": 1}
+ACTORS = {"teacher": 0, "student": 1}
+
+
+class RddConfig(ctypes.Structure):
+    _fields_ = [("n_envs", I64), ("n_envs_global", I64), ("env_base", I64), ("seed", U64),
+                ("loss", I32), ("act_with", I32), ("lr", F32), ("beta1", F32), ("beta2", F32),
+                ("eps", F32), ("grid", I32), ("metrics_len", I32)]
+
+
+nat.register({
+    "rdd_create": (INT, [ctypes.POINTER(P), ctypes.POINTER(RddConfig), INT, P]),
+    "rdd_destroy": (INT, [P]),
+    "rdd_param_count": (INT, []),
+    "rdd_set_stream": (INT, [P, P]),
+    "rdd_set_teacher": (INT, [P, P, P, P]),
+    "rdd_set_student": (INT, [P, P, P, P]),
+    "rdd_get_student": (INT, [P, P]),
+    "rdd_reset": (INT, [P]),
+    "rdd_rollout": (INT, [P]),
+    "rdd_apply": (INT, [P]),
+    "rdd_step": (INT, [P]),
+    "rdd_launch_stage": (INT, [P, INT]),
+    "rdd_grad_buffer": (P, [P]),
+    "rdd_bind_grad_buffer": (INT, [P, P]),
+    "rdd_forward": (INT, [P, P, I64, P, P]),
+    "rdd_get_env_state": (INT, [P, P]),
+    "rdd_set_env_state": (INT, [P, P]),
+    "rdd_get_counter": (INT, [P, ctypes.POINTER(I64)]),
+    "rdd_read_metrics": (INT, [P, I64, P]),
+})
+
+
+@dataclass
+class DistillConfig:
+    n_envs: int = 4096                 # envs on this rank
+    seed: int = 0                      # Philox reset seed
+    loss: str = "mse"                  # "mse" (configs 2,5) | "kl" (config 3, reference loss.py)
+    act_with: str = "teacher"          # "teacher" (configs 2-4) | "student" (DAgger, config 5)
+    lr: float = 1e-4                   # reference mlp_train.py:75
+    beta1: float = 0.9
+    beta2: float = 0.999
+    eps: float = 1e-8
+    teacher_seed: int = 1
+    student_seed: int = 2
+    grid: int = 0
+    metrics_len: int = 4096
+
+
+class DistillTrainer:
+    def __init__(self, cfg: DistillConfig, device="cuda:0", rank: int = 0, world_size: int = 1,
+                 process_group=None, teacher: MlpPolicyParams | None = None,
+                 student: MlpPolicyParams | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("DistillTrainer runs on a GPU (HIP) device only; there is no CPU path")
+        self.rank, self.world = rank, world_size
+        self.pg = process_group
+        self._lib = nat.load()
+        assert self._lib.rdd_param_count() == P_TOT
+        c = RddConfig(n_envs=cfg.n_envs, n_envs_global=cfg.n_envs * world_size, env_base=cfg.n_envs * rank,
+                      seed=cfg.seed % 2 ** 64, loss=LOSSES[cfg.loss], act_with=ACTORS[cfg.act_with], lr=cfg.lr,
+                      beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps, grid=cfg.grid, metrics_len=cfg.metrics_len)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            nat.check(self._lib.rdd_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,
+                                           nat.stream_handle(self.device)), "rdd_create")
+        self._h = h
+        self.teacher = teacher or synthetic_teacher(cfg.teacher_seed)
+        self.student = student or student_init(cfg.student_seed)
+        self.set_teacher(self.teacher)
+        self.set_student(self.student)
+        self.reset()
+        # the flat gradient lives in a torch tensor bound into the trainer, so the host
+        # all-reduces it in place (RCCL) between rdd_rollout and rdd_apply
+        self._grad = torch.zeros(P_TOT, dtype=torch.float32, device=self.device)
+        nat.check(self._lib.rdd_bind_grad_buffer(self._h, nat.ptr(self._grad)), "rdd_bind_grad_buffer")
+        self.steps = 0
+
+    # -- parameters ------------------------------------------------------------------
+    def set_teacher(self, p: MlpPolicyParams):
+        f, mu, sd = p.device_tensors(self.device)
+        nat.check(self._lib.rdd_set_teacher(self._h, nat.ptr(f), nat.ptr(mu), nat.ptr(sd)), "rdd_set_teacher")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def set_student(self, p: MlpPolicyParams):
+        f, mu, sd = p.device_tensors(self.device)
+        nat.check(self._lib.rdd_set_student(self._h, nat.ptr(f), nat.ptr(mu), nat.ptr(sd)), "rdd_set_student")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def student_params(self) -> torch.Tensor:
+        out = torch.empty(P_TOT, dtype=torch.float32, device=self.device)
+        nat.check(self._lib.rdd_get_student(self._h, nat.ptr(out)), "rdd_get_student")
+        return out
+
+    def reset(self):
+        nat.check(self._lib.rdd_reset(self._h), "rdd_reset")
+        self.steps = 0
+
+    # -- the step ----------------------------------------------------------------------
+    def step(self):
+        """One rollout + distill step over this rank's envs (+ gradient all-reduce)."""
+        if self.world == 1:
+            nat.check(self._lib.rdd_step(self._h), "rdd_step")
+        else:
+            nat.check(self._lib.rdd_rollout(self._h), "rdd_rollout")
+            self.allreduce_grad()
+            nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
+        self.steps += 1
+
+    def set_stream(self, stream: torch.cuda.Stream):
+        nat.check(self._lib.rdd_set_stream(self._h, ctypes.c_void_p(stream.cuda_stream)), "rdd_set_stream")
+
+    def capture(self, steps: int = 1) -> torch.cuda.CUDAGraph:
+        """Capture `steps` single-rank steps into a HIP graph (replay = `steps` steps, no
+        host launches).  The trainer's stream is restored afterwards."""
+        if self.world != 1:
+            raise RuntimeError("graph capture is for the single-rank step")
+        g = torch.cuda.CUDAGraph()
+        prev = torch.cuda.current_stream(self.device)
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g):
+            self.set_stream(torch.cuda.current_stream(self.device))
+            for _ in range(steps):
+                nat.check(self._lib.rdd_step(self._h), "rdd_step")
+        self.set_stream(prev)
+        return g
+
+    STAGE_ROLLOUT, STAGE_REDUCE, STAGE_APPLY, STAGE_REDUCE_APPLY = 1, 2, 3, 4
+
+    def launch(self, stage: int):
+        nat.check(self._lib.rdd_launch_stage(self._h, stage), "rdd_launch_stage")
+
+    def rollout(self):
+        nat.check(self._lib.rdd_rollout(self._h), "rdd_rollout")
+
+    def apply(self):
+        nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
+        self.steps += 1
+
+    def grad(self) -> torch.Tensor:
+        """The gradient of the last rollout (rank-local until all-reduced)."""
+        return self._grad
+
+    def allreduce_grad(self):
+        import torch.distributed as dist
+        dist.all_reduce(self._grad, op=dist.ReduceOp.SUM, group=self.pg)
+
+    # -- queries -----------------------------------------------------------------------
+    def forward(self, obs: torch.Tensor, teacher=True, student=True):
+        obs = obs.to(self.device, torch.float32).contiguous()
+        n = obs.shape[0]
+        t = torch.empty(n, 4, device=self.device) if teacher else None
+        s = torch.empty(n, 4, device=self.device) if student else None
+        nat.check(self._lib.rdd_forward(self._h, nat.ptr(obs), n, nat.ptr(t) if t is not None else None,
+                                        nat.ptr(s) if s is not None else None), "rdd_forward")
+        return t, s
+
+    def env_state(self) -> torch.Tensor:
+        st = torch.empty(8, self.cfg.n_envs, dtype=torch.float32, device=self.device)
+        nat.check(self._lib.rdd_get_env_state(self._h, nat.ptr(st)), "rdd_get_env_state")
+        return st
+
+    def set_env_state(self, st: torch.Tensor):
+        st = st.to(self.device, torch.float32).contiguous()
+        nat.check(self._lib.rdd_set_env_state(self._h, nat.ptr(st)), "rdd_set_env_state")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def counter(self) -> int:
+        c = ctypes.c_int64()
+        nat.check(self._lib.rdd_get_counter(self._h, ctypes.byref(c)), "rdd_get_counter")
+        return c.value
+
+    def metrics(self, count: int) -> np.ndarray:
+        """[count, 4] per step: sum reward, loss, sum (mu_s-mu_t)^2, envs (this rank)."""
+        out = np.zeros((count, 4), np.float64)
+        nat.check(self._lib.rdd_read_metrics(self._h, count, out.ctypes.data_as(ctypes.c_void_p)),
+                  "rdd_read_metrics")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            nat.load().rdd_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

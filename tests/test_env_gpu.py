@@ -128,20 +128,31 @@ def test_philox_resets_bit_exact(oracle_c):
     assert np.array_equal(st.cpu().numpy()[:6], oracle_c.philox_reset(n, base, seed, 1)[:6])
 
 
-def test_open_loop_episode_vs_oracle_f32(oracle_c):
-    """A full 50-step episode, teacher-like smooth actions, vs the C f32 oracle."""
+def test_open_loop_episode_vs_oracle(oracle_c):
+    """A full 50-step episode with smooth +-0.5 actions (larger than the teacher's) from
+    Philox resets, against the f64 oracle run from the same f32 reset state.  The HIP
+    kernel's error must stay within 1e-4 and within 3x the f32 C restatement's own error
+    (round-off growth through the 200x actuator gain is the limit, not the kernel)."""
     from reacherdistilation_amd.env import BatchedReacher
     n, seed = 4096, 5
     env = BatchedReacher(n, seed=seed, device=DEV)
-    o = env.reset()
-    ref = oracle_c.philox_reset(n, 0, seed, 0)
+    env.reset()
+    ref32 = oracle_c.philox_reset(n, 0, seed, 0)
+    ref64 = np.ascontiguousarray(ref32.astype(np.float64))
     rs = np.random.RandomState(9)
+    phase = rs.uniform(0, 6, (n, 1)) + np.array([0, 1])
+    e_gpu = e_c32 = 0.0
     for k in range(49):
-        a = (0.5 * np.sin(0.3 * k + rs.uniform(0, 6, (n, 1)) + np.array([0, 1]))).astype(np.float32)
+        a = (0.5 * np.sin(0.3 * k + phase)).astype(np.float32)
         o, r, d, _ = env.step(torch.from_numpy(a).to(DEV))
-        ob32, r32 = oracle_c.step(ref, a, np.float32)
-        np.testing.assert_allclose(o.cpu().numpy(), ob32, atol=OB_ATOL, rtol=OB_RTOL)
-        np.testing.assert_allclose(r.cpu().numpy(), r32, atol=R_ATOL, rtol=0)
+        ob32, _ = oracle_c.step(ref32, a, np.float32)
+        ob64, r64 = oracle_c.step(ref64, a, np.float64)
+        o = o.cpu().numpy()
+        np.testing.assert_allclose(o, ob64, atol=1e-4, rtol=1e-4)
+        np.testing.assert_allclose(r.cpu().numpy(), r64, atol=R_ATOL, rtol=0)
+        e_gpu = max(e_gpu, np.abs(o - ob64).max())
+        e_c32 = max(e_c32, np.abs(ob32 - ob64).max())
+    assert e_gpu <= 3 * e_c32 + 1e-6, (e_gpu, e_c32)
 
 
 def test_deterministic_bitwise():
