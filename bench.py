@@ -81,7 +81,7 @@ def cpu_baseline(workload, seconds, threads):
     while True:
         g, _ = ref_c.distill_step(state, steps, (t.flat, t.ob_mean, t.ob_std), (sp, s.ob_mean, s.ob_std),
                                   loss=workload["loss"], act_student=workload["act_with"] == "student",
-                                  nthreads=threads)
+                                  stagger=True, nthreads=threads)
         ref_c.adam_tf1(sp, m, v, g, b1p, b2p)
         b1p *= 0.9; b2p *= 0.999
         steps += 1

@@ -47,7 +47,20 @@ typedef struct {
     float lr, beta1, beta2, eps;   /* Adam (reference: 1e-4, .9, .999, 1e-8)         */
     int32_t grid;            /* rollout workgroups; 0 = auto (<= one per CU)          */
     int32_t metrics_len;     /* ring length of the per-step metrics history; 0 = 4096 */
+    int32_t stagger;         /* 0: lockstep TimeLimit (all envs share the episode phase);
+                                1: env g runs at phase C + (g / RDD_STAGGER_GROUP) % 50, so a
+                                   batch mixes all 50 episode phases (see below)          */
 } rdd_config;
+
+/* Staggered episodes.  The reference steps ONE env and trains on random windows drawn
+ * from past episodes (dataset.py:179-194), so a training batch mixes episode phases.  N
+ * envs in lockstep would instead hand the optimiser a batch in which every env is at the
+ * same step of its episode, and the student would chase the phase.
+ * With stagger = 1, env g's episode clock is offset by (g / 32) % 50 steps: its first
+ * episode is truncated to 50 - offset steps, every later one runs the full 50 steps, and
+ * the reset after an episode that ends at phase u draws Philox(seed, g, u / 50 + 1).
+ * Groups of 32 consecutive envs share an offset so that a wave's resets stay uniform. */
+#define RDD_STAGGER_GROUP 32
 
 typedef struct rdd_trainer rdd_trainer;
 

@@ -189,8 +189,10 @@ void rdo_adam_tf1(int64_t n, float* theta, float* m, float* v, const float* g, f
 }
 
 /* One rollout+distill step over n envs (lockstep), f32, the CPU baseline / f32 checker.
- *   state [8][n] SoA (q0,q1,v0,v1,tx,ty,dx,dy); step = global completed-step counter C
- *   (episode = C/50, t = C%50; done when t == 49 -> reset from Philox(seed, env_base+i, ep+1))
+ *   state [8][n] SoA (q0,q1,v0,v1,tx,ty,dx,dy); step = global completed-step counter C.
+ *   Env g = env_base+i runs at phase u = C + off(g), off(g) = stagger ? (g / 32) % 50 : 0
+ *   (episode = u/50, t = u%50; done when t == 49 -> reset from Philox(seed, g, episode+1)).
+ *   stagger = 0 is the lockstep TimeLimit; stagger = 1 spreads the envs' episode phases
  *   teacher/student: flat params + obfilter (mu, sd)
  *   loss: 0 = MSE(mean over n_global*2), 1 = KL(s||t) summed
  *   act_student: 0 = step env with teacher mean, 1 = with student mean (DAgger)
@@ -200,10 +202,8 @@ void rdo_adam_tf1(int64_t n, float* theta, float* m, float* v, const float* g, f
 void rdo_distill_step(int64_t n, int64_t n_global, int64_t env_base, uint64_t seed, int64_t step,
                       float* state, const float* tp, const float* tmu, const float* tsd,
                       const float* sp, const float* smu, const float* ssd, int loss, int act_student,
-                      float* grad, double* metrics, int nthreads) {
+                      int stagger, float* grad, double* metrics, int nthreads) {
     memset(grad, 0, sizeof(float) * P_TOT);
-    const int t_in_ep = (int)(step % 50);
-    const uint32_t ep = (uint32_t)(step / 50);
     double rsum = 0, lsum = 0, msum = 0;
     const float tls0 = tp[P_LS], tls1 = tp[P_LS + 1];
     const float sls0 = sp[P_LS], sls1 = sp[P_LS + 1];
@@ -241,11 +241,10 @@ void rdo_distill_step(int64_t n, int64_t n_global, int64_t env_base, uint64_t se
             float a1 = act_student ? fs.mean[1] : ft.mean[1];
             float obn[OBD];
             rsum += env_step_f32(s, a0, a1, obn);
-            if (t_in_ep == 49) {
+            const int64_t u = step + (stagger ? ((env_base + i) / 32) % 50 : 0);  /* RDD_STAGGER_GROUP */
+            if (u % 50 == 49) {
                 float dr[6];
-                double dummy_obs[OBD];
-                (void)dummy_obs;
-                rdo_philox_draw(seed, (uint64_t)(env_base + i), ep + 1, dr);
+                rdo_philox_draw(seed, (uint64_t)(env_base + i), (uint32_t)(u / 50 + 1), dr);
                 env_reset_f32(s, dr, obn);
             }
             for (int k = 0; k < 8; ++k) state[k * n + i] = s[k];

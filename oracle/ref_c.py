@@ -35,7 +35,7 @@ def lib():
         L.rdo_philox_draw.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P]
         L.rdo_philox_reset.argtypes = [I64, I64, ctypes.c_uint64, ctypes.c_uint32, P]
         L.rdo_distill_step.argtypes = [I64, I64, I64, ctypes.c_uint64, I64, P, P, P, P, P, P, P,
-                                       ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int]
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int]
         L.rdo_adam_tf1.argtypes = [I64, P, P, P, P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_float]
         L.rdo_constants.argtypes = [P]
@@ -90,7 +90,7 @@ def param_count():
 
 
 def distill_step(state, step, teacher, student, *, seed=0, loss="mse", act_student=False,
-                 n_global=None, env_base=0, nthreads=1):
+                 n_global=None, env_base=0, stagger=False, nthreads=1):
     """One rollout+distill step (f32, CPU).  teacher/student = (params, obmu, obsd).
     Returns (grad [P] f32, metrics [4] f64).  state modified in place."""
     n = state.shape[1]
@@ -100,7 +100,7 @@ def distill_step(state, step, teacher, student, *, seed=0, loss="mse", act_stude
     sp, smu, ssd = [np.ascontiguousarray(x, np.float32) for x in student]
     lib().rdo_distill_step(n, n_global or n, env_base, seed, step, _p(state), _p(tp), _p(tmu),
                            _p(tsd), _p(sp), _p(smu), _p(ssd), 0 if loss == "mse" else 1,
-                           1 if act_student else 0, _p(grad), _p(met), nthreads)
+                           1 if act_student else 0, 1 if stagger else 0, _p(grad), _p(met), nthreads)
     return grad, met
 
 

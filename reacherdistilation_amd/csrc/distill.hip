@@ -72,9 +72,9 @@ struct RolloutArgs {
     float* state;                          // [8][n]
     const float* tnet;                     // teacher: params[P], mu[11], sd[11] (contiguous)
     const float* snet;                     // student
-    const uint32_t* ctl;                   // [0] completed steps
+    uint32_t* ctl;                         // [0] completed steps, [4..7] snapshot
     float* ws;                             // [gridDim.x][P_PAD]
-    int loss, act_student;
+    int loss, act_student, stagger;
     float inv_n_global;
 };
 
@@ -89,6 +89,14 @@ __device__ __forceinline__ float tanh_f(float x) {
     // 1 - 2/(exp(2x)+1): one v_exp_f32 + one v_rcp_f32; saturates correctly at +-inf
     const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
     return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+}
+
+// The per-wave scratch is private to its wave: LDS instructions of one wave execute in
+// issue order, so staging needs only a compiler-level barrier, not s_barrier.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -194,8 +202,8 @@ __global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
     load_net(LS, a.snet);
 
     const uint32_t C = a.ctl[0];
-    const bool done_step = (C % rd::kEpisodeSteps) == rd::kEpisodeSteps - 1;
-    const uint32_t next_ep = C / rd::kEpisodeSteps + 1;
+    // snapshot of the step words for reduce_adam_kernel, which rewrites ctl[0..3]
+    if (blockIdx.x == 0 && threadIdx.x < 4) a.ctl[4 + threadIdx.x] = a.ctl[threadIdx.x];
 
     // teacher / student log-std (state independent)
     const float tl0 = a.tnet[P_LS], tl1 = a.tnet[P_LS + 1];
@@ -254,9 +262,14 @@ __global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
         const float ac0 = a.act_student ? ms0 : mt0;
         const float ac1 = a.act_student ? ms1 : mt1;
         const float rew = rd::env_step(st, ac0, ac1);
+        // episode clock of this env (RDD_STAGGER_GROUP envs share an offset: wave-uniform
+        // unless a tile straddles a group boundary)
+        const int64_t g = a.env_base + i;
+        const uint32_t u = C + (a.stagger ? (uint32_t)((g / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);
+        const bool done_step = (u % rd::kEpisodeSteps) == rd::kEpisodeSteps - 1;
         if (done_step) {
             float dr[6];
-            rd::philox_draw(a.seed, (uint64_t)(a.env_base + i), next_ep, dr);
+            rd::philox_draw(a.seed, (uint64_t)g, u / rd::kEpisodeSteps + 1, dr);
             rd::env_reset(st, dr);
         }
         if (valid && h == 0) {
@@ -296,7 +309,7 @@ __global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
             S[S_DM + 2 * c] = dm0;
             S[S_DM + 2 * c + 1] = dm1;
         }
-        __syncthreads();
+        wave_sync();
         // dW2 += H1^T dZ2 over the tile's 32 envs (K = env pairs)
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
@@ -334,7 +347,7 @@ __global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
             dZ[0][r] = acc0[r] * (1.0f - H1[0][r] * H1[0][r]);
             dZ[1][r] = acc1[r] * (1.0f - H1[1][r] * H1[1][r]);
         }
-        __syncthreads();
+        wave_sync();
         // stage dZ1 and the student's filtered observation z (cols 0..31, zero-padded)
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
@@ -342,7 +355,7 @@ __global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
             for (int r = 0; r < 16; ++r) S[S_B1 + c * LDW + 32 * kb + featD(r, h)] = dZ[kb][r];
 #pragma unroll
         for (int k = 0; k < 16; ++k) S[S_B0 + c * LDW + 16 * h + k] = (h == 0 && k < 12) ? z[k] : 0.0f;
-        __syncthreads();
+        wave_sync();
         // dW1 += z^T dZ1  (rows = input feature, only 0..10 meaningful)
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
@@ -353,9 +366,10 @@ __global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
         }
 #pragma unroll 8
         for (int e = 0; e < 32; ++e) gb1 += S[S_B1 + e * LDW + lane];
-        __syncthreads();
+        wave_sync();
     }
 
+    __syncthreads();   // the reduction below reuses every wave's scratch
     // ---------------------------------------------------------------- workgroup reduction
     float* R = lds + 2 * NET + wave * P_PAD;   // reuses the scratch (all tiles done)
 #pragma unroll
@@ -394,7 +408,9 @@ __global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
     }
 }
 
-// ctl words: [0] completed steps C, [1] arrival ticket, [2] beta1^t, [3] beta2^t (f32 bits)
+// ctl words: [0] completed steps C, [2] beta1^t, [3] beta2^t (f32 bits); [4..7] the
+// rollout's snapshot of [0..3], which this kernel reads so that block 0 may rewrite
+// [0..3] without racing the other blocks (no atomics, no fences: stream order suffices).
 struct ReduceArgs {
     const float* ws;
     int nblk;
@@ -409,28 +425,46 @@ struct ReduceArgs {
     float lr, b1, b2, eps;
 };
 
-__global__ __launch_bounds__(256) void reduce_adam_kernel(ReduceArgs a) {
-    const uint32_t C = a.ctl[0];
-    const float b1p = __uint_as_float(a.ctl[2]), b2p = __uint_as_float(a.ctl[3]);
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p < P_PAD) {
-        float g = 0.0f;
-        if (a.reduce) {
+constexpr int RED_COLS = 64;                        // params per reduce block
+constexpr int RED_ROWS = 16;                        // partial rows summed in parallel
+constexpr int RED_BLOCK = RED_COLS * RED_ROWS;
+constexpr int RED_GRID = (P_PAD + RED_COLS - 1) / RED_COLS;
+
+// Sum the rollout's per-workgroup partials (fixed order: deterministic), then TF1 Adam.
+__global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
+    __shared__ float part[RED_ROWS][RED_COLS];
+    const uint32_t C = a.ctl[4];
+    const float b1p = __uint_as_float(a.ctl[6]), b2p = __uint_as_float(a.ctl[7]);
+    const int col = threadIdx.x & (RED_COLS - 1), row = threadIdx.x / RED_COLS;
+    const int p = blockIdx.x * RED_COLS + col;
+    if (a.reduce) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        if (p < P_PAD) {
             const float* w = a.ws + p;
-            int b = 0;
-            float s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-            for (; b + 4 <= a.nblk; b += 4) {
+            int b = row;
+#pragma unroll 4
+            for (; b + 3 * RED_ROWS < a.nblk; b += 4 * RED_ROWS) {
                 s0 += w[(int64_t)b * P_PAD];
-                s1 += w[(int64_t)(b + 1) * P_PAD];
-                s2 += w[(int64_t)(b + 2) * P_PAD];
-                s3 += w[(int64_t)(b + 3) * P_PAD];
+                s1 += w[(int64_t)(b + RED_ROWS) * P_PAD];
+                s2 += w[(int64_t)(b + 2 * RED_ROWS) * P_PAD];
+                s3 += w[(int64_t)(b + 3 * RED_ROWS) * P_PAD];
             }
-            for (; b < a.nblk; ++b) s0 += w[(int64_t)b * P_PAD];
-            g = (s0 + s1) + (s2 + s3);
+            for (; b < a.nblk; b += RED_ROWS) s0 += w[(int64_t)b * P_PAD];
+        }
+        part[row][col] = (s0 + s1) + (s2 + s3);
+    }
+    __syncthreads();
+    if (row == 0 && p < P_PAD) {
+        float g;
+        if (a.reduce) {
+            float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < RED_ROWS; ++r) q[r & 3] += part[r][col];
+            g = (q[0] + q[1]) + (q[2] + q[3]);
             if (p < P_TOT) a.grad[p] = g;
             else a.hist[(int64_t)(C % (uint32_t)a.hist_len) * N_MET + (p - P_TOT)] = g;
-        } else if (p < P_TOT) {
-            g = a.grad[p];
+        } else {
+            g = p < P_TOT ? a.grad[p] : 0.f;
         }
         if (a.adam && p < P_TOT) {
             // TF1 ApplyAdam functor (training_ops.cc)
@@ -443,17 +477,10 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(ReduceArgs a) {
             a.params[p] -= (m * alpha) / (sqrtf(v) + a.eps);
         }
     }
-    if (!a.bump) return;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        // every block read ctl[0..3] above; the last arriver advances the step
-        const uint32_t ticket = __hip_atomic_fetch_add(&a.ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (ticket == gridDim.x - 1) {
-            a.ctl[1] = 0u;
-            a.ctl[0] = C + 1u;
-            a.ctl[2] = __float_as_uint(b1p * a.b1);
-            a.ctl[3] = __float_as_uint(b2p * a.b2);
-        }
+    if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ctl[0] = C + 1u;
+        a.ctl[2] = __float_as_uint(b1p * a.b1);
+        a.ctl[3] = __float_as_uint(b2p * a.b2);
     }
 }
 
@@ -469,8 +496,9 @@ __global__ __launch_bounds__(256) void reset_state_kernel(int64_t n, int64_t env
 }
 
 __global__ __launch_bounds__(256) void init_ctl_kernel(uint32_t* ctl, float b1, float b2) {
-    if (threadIdx.x == 0) {
-        ctl[0] = 0u; ctl[1] = 0u; ctl[2] = __float_as_uint(b1); ctl[3] = __float_as_uint(b2);
+    if (threadIdx.x < 2) {
+        const int o = 4 * threadIdx.x;   // live words and their snapshot
+        ctl[o] = 0u; ctl[o + 1] = 0u; ctl[o + 2] = __float_as_uint(b1); ctl[o + 3] = __float_as_uint(b2);
     }
 }
 
@@ -527,7 +555,7 @@ struct rdd_trainer {
     float* own_grad = nullptr;
     float* ws = nullptr;       // [grid][P_PAD]
     float* hist = nullptr;     // [hist_len][4]
-    uint32_t* ctl = nullptr;   // [4]
+    uint32_t* ctl = nullptr;   // [8]: step words + snapshot
 };
 
 namespace {
@@ -544,6 +572,7 @@ int launch_rollout(rdd_trainer* t) {
     a.ws = t->ws;
     a.loss = t->cfg.loss;
     a.act_student = t->cfg.act_with == RDD_ACT_STUDENT;
+    a.stagger = t->cfg.stagger;
     a.inv_n_global = 1.0f / (float)t->cfg.n_envs_global;
     hipLaunchKernelGGL(rollout_kernel, dim3(t->grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
@@ -568,7 +597,7 @@ int launch_reduce(rdd_trainer* t, int reduce, int adam, int bump) {
     a.b1 = t->cfg.beta1;
     a.b2 = t->cfg.beta2;
     a.eps = t->cfg.eps;
-    hipLaunchKernelGGL(reduce_adam_kernel, dim3((P_PAD + 255) / 256), dim3(256), 0, t->stream, a);
+    hipLaunchKernelGGL(reduce_adam_kernel, dim3(RED_GRID), dim3(RED_BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "reduce_adam_kernel launch");
     return RD_OK;
 }
@@ -590,7 +619,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     if (cfg->n_envs <= 0 || cfg->n_envs_global < cfg->n_envs || cfg->env_base < 0 ||
         cfg->n_envs > ((int64_t)1 << 31) || (cfg->loss != RDD_LOSS_MSE && cfg->loss != RDD_LOSS_KL) ||
         (cfg->act_with != RDD_ACT_TEACHER && cfg->act_with != RDD_ACT_STUDENT) || !(cfg->lr > 0) ||
-        cfg->grid < 0 || cfg->metrics_len < 0)
+        cfg->grid < 0 || cfg->metrics_len < 0 || (cfg->stagger != 0 && cfg->stagger != 1))
         return rd::set_error(RD_EINVAL, "rdd_create: bad config");
     rd::DeviceGuard g(device);
     RD_HIP(g.err, "rdd_create: hipSetDevice");
@@ -619,7 +648,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     t->grad = t->own_grad;
     alloc((void**)&t->ws, sizeof(float) * (size_t)t->grid * P_PAD);
     alloc((void**)&t->hist, sizeof(float) * (size_t)t->cfg.metrics_len * N_MET);
-    alloc((void**)&t->ctl, sizeof(uint32_t) * 4);
+    alloc((void**)&t->ctl, sizeof(uint32_t) * 8);
     if (e != hipSuccess) {
         rdd_destroy(t);
         return rd::hip_fail(e, "rdd_create: allocation");

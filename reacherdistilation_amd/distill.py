@@ -32,7 +32,7 @@ ACTORS = {"teacher": 0, "student": 1}
 class RddConfig(ctypes.Structure):
     _fields_ = [("n_envs", I64), ("n_envs_global", I64), ("env_base", I64), ("seed", U64),
                 ("loss", I32), ("act_with", I32), ("lr", F32), ("beta1", F32), ("beta2", F32),
-                ("eps", F32), ("grid", I32), ("metrics_len", I32)]
+                ("eps", F32), ("grid", I32), ("metrics_len", I32), ("stagger", I32)]
 
 
 nat.register({
@@ -72,6 +72,7 @@ class DistillConfig:
     student_seed: int = 2
     grid: int = 0
     metrics_len: int = 4096
+    stagger: bool = True               # spread episode phases over the batch (reacher_distill.h)
 
 
 class DistillTrainer:
@@ -88,7 +89,8 @@ class DistillTrainer:
         assert self._lib.rdd_param_count() == P_TOT
         c = RddConfig(n_envs=cfg.n_envs, n_envs_global=cfg.n_envs * world_size, env_base=cfg.n_envs * rank,
                       seed=cfg.seed % 2 ** 64, loss=LOSSES[cfg.loss], act_with=ACTORS[cfg.act_with], lr=cfg.lr,
-                      beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps, grid=cfg.grid, metrics_len=cfg.metrics_len)
+                      beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps, grid=cfg.grid, metrics_len=cfg.metrics_len,
+                      stagger=int(bool(cfg.stagger)))
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             nat.check(self._lib.rdd_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,
