@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from .dist import allreduce_sum_, shard
 from .policy import P_TOT, MlpPolicyParams, student_init, synthetic_teacher
 
 P = nat.P
@@ -60,7 +61,8 @@ nat.register({
 
 @dataclass
 class DistillConfig:
-    n_envs: int = 4096                 # envs on this rank
+    n_envs: int = 4096                 # envs on this rank (weak scaling: fixed per rank)
+    n_envs_global: int = 0             # if > 0: total envs, sharded over ranks (strong scaling)
     seed: int = 0                      # Philox reset seed
     loss: str = "mse"                  # "mse" (configs 2,5) | "kl" (config 3, reference loss.py)
     act_with: str = "teacher"          # "teacher" (configs 2-4) | "student" (DAgger, config 5)
@@ -87,7 +89,13 @@ class DistillTrainer:
         self.pg = process_group
         self._lib = nat.load()
         assert self._lib.rdd_param_count() == P_TOT
-        c = RddConfig(n_envs=cfg.n_envs, n_envs_global=cfg.n_envs * world_size, env_base=cfg.n_envs * rank,
+        if cfg.n_envs_global > 0:
+            self.n_local, self.env_base = shard(cfg.n_envs_global, rank, world_size)
+            self.n_global = cfg.n_envs_global
+        else:
+            self.n_local, self.env_base = cfg.n_envs, cfg.n_envs * rank
+            self.n_global = cfg.n_envs * world_size
+        c = RddConfig(n_envs=self.n_local, n_envs_global=self.n_global, env_base=self.env_base,
                       seed=cfg.seed % 2 ** 64, loss=LOSSES[cfg.loss], act_with=ACTORS[cfg.act_with], lr=cfg.lr,
                       beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps, grid=cfg.grid, metrics_len=cfg.metrics_len,
                       stagger=int(bool(cfg.stagger)))
@@ -173,8 +181,7 @@ class DistillTrainer:
         return self._grad
 
     def allreduce_grad(self):
-        import torch.distributed as dist
-        dist.all_reduce(self._grad, op=dist.ReduceOp.SUM, group=self.pg)
+        allreduce_sum_(self._grad, self.pg)
 
     # -- queries -----------------------------------------------------------------------
     def forward(self, obs: torch.Tensor, teacher=True, student=True):
@@ -187,7 +194,7 @@ class DistillTrainer:
         return t, s
 
     def env_state(self) -> torch.Tensor:
-        st = torch.empty(8, self.cfg.n_envs, dtype=torch.float32, device=self.device)
+        st = torch.empty(8, self.n_local, dtype=torch.float32, device=self.device)
         nat.check(self._lib.rdd_get_env_state(self._h, nat.ptr(st)), "rdd_get_env_state")
         return st
 

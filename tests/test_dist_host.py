@@ -1,0 +1,99 @@
+"""Multi-rank path on CPU (gloo, world_size 2): env sharding + the one gradient all-reduce.
+
+Each rank runs the C f32 oracle's rollout+distill step on its contiguous shard (global env
+ids, MSE normalised by the GLOBAL env count, staggered clocks keyed by global id: the
+contract rollout_kernel implements, include/reacher_distill.h), all-reduces the flat
+gradient with torch.distributed (gloo) and applies TF1 Adam.  The result must equal the
+single-rank full batch up to f32 summation order (rtol 1e-5 on the gradient).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from reacherdistilation_amd.dist import allreduce_sum_, shard
+
+
+def test_shard_covers_all_envs():
+    for n, w in [(8, 1), (10, 3), (262144, 8), (1048576, 8), (4097, 2)]:
+        parts = [shard(n, r, w) for r in range(w)]
+        assert sum(p[0] for p in parts) == n
+        assert parts[0][1] == 0
+        for (n0, b0), (n1, b1) in zip(parts, parts[1:]):
+            assert b1 == b0 + n0 and abs(n1 - n0) <= 1
+    with pytest.raises(ValueError):
+        shard(1, 0, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+N_GLOBAL, SEED, STEPS = 1000, 4, 3
+
+
+def _nets():
+    from reacherdistilation_amd.policy import student_init, synthetic_teacher
+    t, s = synthetic_teacher(1), student_init(2)
+    return (t.flat, t.ob_mean, t.ob_std), s
+
+
+def _run(rank, world, port, out):
+    from oracle import ref_c
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, base = shard(N_GLOBAL, rank, world)
+    tnet, s = _nets()
+    sp = s.flat.copy()
+    P = ref_c.param_count()
+    m, v = np.zeros(P, np.float32), np.zeros(P, np.float32)
+    state = ref_c.philox_reset(n, base, SEED, 0)
+    b1p, b2p = np.float32(0.9), np.float32(0.999)
+    grads = []
+    for k in range(STEPS):
+        g, met = ref_c.distill_step(state, k, tnet, (sp, s.ob_mean, s.ob_std), seed=SEED, loss="mse",
+                                    n_global=N_GLOBAL, env_base=base, stagger=True, nthreads=1)
+        gt = torch.from_numpy(g)
+        allreduce_sum_(gt)
+        grads.append(gt.numpy().copy())
+        ref_c.adam_tf1(sp, m, v, gt.numpy(), float(b1p), float(b2p), lr=1e-3)
+        b1p, b2p = np.float32(b1p * np.float32(0.9)), np.float32(b2p * np.float32(0.999))
+    out[rank] = (np.stack(grads), sp, state)
+    dist.destroy_process_group()
+
+
+def test_two_rank_allreduce_equals_full_batch(oracle_c):
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_run, args=(world, _free_port(), out), nprocs=world, join=True)
+    g0, p0, st0 = out[0]
+    g1, p1, st1 = out[1]
+    # every rank holds the same reduced gradient and therefore the same student
+    assert np.array_equal(g0, g1) and np.array_equal(p0, p1)
+    # ... which is the full single-rank batch
+    tnet, s = _nets()
+    sp = s.flat.copy()
+    P = oracle_c.param_count()
+    m, v = np.zeros(P, np.float32), np.zeros(P, np.float32)
+    state = oracle_c.philox_reset(N_GLOBAL, 0, SEED, 0)
+    b1p, b2p = np.float32(0.9), np.float32(0.999)
+    for k in range(STEPS):
+        g, _ = oracle_c.distill_step(state, k, tnet, (sp, s.ob_mean, s.ob_std), seed=SEED, loss="mse",
+                                     stagger=True, nthreads=1)
+        np.testing.assert_allclose(g0[k], g, rtol=1e-5, atol=1e-6 * np.abs(g).max())
+        oracle_c.adam_tf1(sp, m, v, g, float(b1p), float(b2p), lr=1e-3)
+        b1p, b2p = np.float32(b1p * np.float32(0.9)), np.float32(b2p * np.float32(0.999))
+    np.testing.assert_allclose(p0, sp, atol=2e-5)
+    # the shards' env states are the full batch's, split contiguously
+    n0 = shard(N_GLOBAL, 0, world)[0]
+    np.testing.assert_allclose(np.concatenate([st0, st1], axis=1), state, atol=2e-5)
+    assert st0.shape[1] == n0
