@@ -13,7 +13,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shares torch's libamdhip64)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libreacher.so")
+# RD_LIB selects a diagnostic build (e.g. libreacher_stamps.so); default: the product library
+LIB_PATH = os.path.join(HERE, os.environ.get("RD_LIB", "libreacher.so"))
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int32

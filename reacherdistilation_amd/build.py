@@ -57,8 +57,17 @@ def resource_usage():
     subprocess.call(cmd)
 
 
+def build_stamps():
+    """Diagnostic build with per-wave phase stamps (scripts/stamps.py); never the product."""
+    out = os.path.join(HERE, "libreacher_stamps.so")
+    subprocess.check_call([HIPCC, *FLAGS, "-DRD_STAMPS", "-o", out, *sources()])
+    return out
+
+
 if __name__ == "__main__":
     if "--usage" in sys.argv:
         resource_usage()
+    elif "--stamps" in sys.argv:
+        build_stamps()
     else:
         build(force="--force" in sys.argv)

@@ -6,21 +6,28 @@
 // env.step(action) with auto-reset; per-workgroup gradient partials go to a workspace.
 // reduce_adam_kernel then sums the partials and applies TF1 Adam (mlp_train.py:73-80).
 //
-// MI355X mapping (DESIGN.md §Kernels):
-//  * a wave owns a 32-env tile; lane l = (env c = l&31, half h = l>>5).  Both halves
-//    integrate the env's physics (so every lane holds the full observation) and the
-//    networks run on v_mfma_f32_32x32x2_f32 in the transposed orientation
-//    Z^T[feature x env] = W^T[feature x in] . X^T[in x env]:  the accumulator of one
-//    layer (feature rows in registers, env on the lane) IS the B operand of the next
-//    layer, so activations never leave registers in the forward/backward chain.
-//  * weights of both nets live in LDS (W2 padded to 65 columns: the same copy is read
-//    row-wise for W^T.X and column-wise for W.dZ without bank conflicts).
-//  * weight gradients (sums over envs) are MFMAs with the env as K: H1 and dZ are
-//    transposed through a per-wave LDS scratch; accumulators persist across the tiles a
-//    wave processes and are reduced once per workgroup at the end.
+// MI355X mapping (DESIGN.md §3):
+//  * 512-thread workgroups (8 waves = 2 per SIMD, <= 256 VGPR+AGPR each) so that one
+//    wave's VALU work (physics, tanh, staging) issues while its SIMD partner's MFMAs run.
+//  * a wave owns a GROUP of 64 envs: the physics runs once per env (one env per lane);
+//    the networks run on 16-env TILES (4 per group) with v_mfma_f32_16x16x4_f32 in the
+//    transposed orientation Z^T[feature x env] = W^T[feature x in] . X^T[in x env]:
+//    lane l = (env j = l&15, k-group g = l>>4); a layer's accumulator (features 4g+r in
+//    registers, env on the lane) IS the B operand of the next layer (k-step r uses the
+//    features {4g + r}), so activations never leave registers in the forward/backward
+//    chain.  Layer-1 bias rides in the K padding (input 11 = 1).
+//  * weights of both nets live in LDS for the whole launch as [k][j][fb] images (one
+//    conflict-free ds_read_b128 feeds the 4 MFMAs of a k-step, prefetched a step ahead);
+//    the student also keeps W2^T for dH1 = W2 . dZ2.
+//  * weight gradients (sums over envs) are MFMAs with the env as K: H1, dZ2 and dZ1 are
+//    transposed through a per-wave LDS scratch (private to the wave: ordered by a
+//    wave-level barrier, never s_barrier); accumulators persist across the wave's tiles
+//    and are reduced once per workgroup, in a fixed order (deterministic).
 //  * exact f32 arithmetic throughout (f32-input MFMA = k-ordered fmaf chain).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <stdlib.h>
 
 #include <new>
 
@@ -30,7 +37,7 @@
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int OBD = 11, HID = 64, ACD = 2;
 constexpr int P_W1 = 0;
@@ -44,27 +51,38 @@ constexpr int P_TOT = P_LS + ACD;        // 5060
 constexpr int P_PAD = P_TOT + 4;         // + metrics: reward, loss, sq err, envs
 constexpr int N_MET = 4;
 
-constexpr int WAVES = 4, BLOCK = 64 * WAVES;
-constexpr int LDW = 65;   // padded row length of W2 and of the scratch tiles
+constexpr int WAVES = 8, BLOCK = 64 * WAVES;   // rollout: 2 waves per SIMD
+constexpr int FWAVES = 4, FBLOCK = 64 * FWAVES; // forward_kernel
+constexpr int GROUP = 64;                      // envs per wave pass (one per lane)
+constexpr int TILE = 16;                       // envs per MFMA tile
 
-// per-network LDS image (floats)
-constexpr int N_W1 = 0;                  // [12][64], row 11 = 0 (K padded to 12)
-constexpr int N_B1 = N_W1 + 12 * HID;
-constexpr int N_W2 = N_B1 + HID;         // [64][65]
-constexpr int N_B2 = N_W2 + HID * LDW;
+// ---------------------------------------------------------------- LDS image of a net
+// Weight images are [k][j][fb] = W[k][16 fb + j]: the four A operands a lane needs for one
+// k-step (output blocks fb = 0..3, row j) are one 16-B ds_read_b128, and a 16-lane group
+// reads one contiguous 256-B row: conflict-free, no padding.
+constexpr int N_W1 = 0;                  // [12][16][4]: rows 0..10 = W1, row 11 = b1
+constexpr int N_W2 = N_W1 + 12 * HID;    // [64][16][4]
+constexpr int N_B2 = N_W2 + HID * HID;   // [64]
 constexpr int N_W3 = N_B2 + HID;         // [64][2]
-constexpr int N_B3 = N_W3 + HID * ACD;
-constexpr int N_LS = N_B3 + ACD;
-constexpr int N_MU = N_LS + ACD;         // [12]
-constexpr int N_RS = N_MU + 12;          // [12] 1/std (0 in the pad)
-constexpr int NET = ((N_RS + 12) + 3) & ~3;
-// per-wave scratch (floats)
-constexpr int S_TILE = 32 * LDW;
-constexpr int S_B0 = 0, S_B1 = S_TILE, S_B2 = 2 * S_TILE, S_DM = 3 * S_TILE;
-constexpr int SCR = 3 * S_TILE + 64;
-constexpr int LDS_FLOATS = 2 * NET + WAVES * SCR;
-static_assert(WAVES * P_PAD <= WAVES * SCR, "final reduction must fit in the scratch");
+constexpr int N_B3 = N_W3 + HID * ACD;   // [2]
+constexpr int N_LS = N_B3 + ACD;         // [2]
+constexpr int N_MU = N_LS + ACD;         // [12] filter mean (0 for the bias input 11)
+constexpr int N_RS = N_MU + 12;          // [12] 1/std     (1 for the bias input 11)
+constexpr int NET = (N_RS + 12 + 3) & ~3;
+constexpr int N_W2T = NET;               // student only: [j][i&15][i>>4] = W2[i][j]
+constexpr int NET_S = NET + HID * HID;
+static_assert(N_B2 % 4 == 0 && N_W3 % 4 == 0 && NET % 4 == 0, "16-B aligned LDS vectors");
+
+// ---------------------------------------------------------------- per-wave scratch
+constexpr int SOS = 12;                  // raw obs rows (11 + the bias input = 1)
+constexpr int SAS = 68;                  // transposed activation rows [env][64 + pad]
+constexpr int S_OB = 0;                  // [64][12]
+constexpr int S_A = S_OB + GROUP * SOS;  // [16][SAS]  H1^T, then dZ1^T
+constexpr int S_B = S_A + TILE * SAS;    // [16][SAS]  dZ2^T
+constexpr int SCR = S_B + TILE * SAS;
+constexpr int LDS_FLOATS = NET + NET_S + WAVES * SCR;
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+static_assert(4 * P_PAD <= WAVES * SCR, "final reduction must fit in the scratch");
 
 struct RolloutArgs {
     int64_t n, env_base;
@@ -76,14 +94,13 @@ struct RolloutArgs {
     float* ws;                             // [gridDim.x][P_PAD]
     int loss, act_student, stagger;
     float inv_n_global;
+    unsigned long long* dbg;               // RD_STAMPS builds: [grid*WAVES][16] stamp sums
+    int prio_mode;                         // experiment knob (RDD_PRIO_MODE env var)
 };
 
-__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
-
-// accumulator register r of lane-half h holds feature row featD(r, h) (+32 per block)
-__device__ __forceinline__ int featD(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ float tanh_f(float x) {
     // 1 - 2/(exp(2x)+1): one v_exp_f32 + one v_rcp_f32; saturates correctly at +-inf
@@ -99,26 +116,66 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// x + x from the partner row (lane ^ 16) / half (lane ^ 32): v_permlane16/32_swap (VALU,
+// no LDS round trip).  Every lane gets the bitwise-identical sum.
+__device__ __forceinline__ float xsum16(float x) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float xsum32(float x) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
 
-// global net = params[P] | mu[11] | sd[11]  ->  LDS image
-__device__ void load_net(float* L, const float* g) {
+// state row k of env i: (state + k n)[i] -- uniform 64-bit row base, 32-bit lane offset
+__device__ __forceinline__ void load_state(const float* s, int64_t n, uint32_t i, rd::State& st) {
+    st.q0 = (s + 0 * n)[i]; st.q1 = (s + 1 * n)[i]; st.v0 = (s + 2 * n)[i]; st.v1 = (s + 3 * n)[i];
+    st.tx = (s + 4 * n)[i]; st.ty = (s + 5 * n)[i]; st.dx = (s + 6 * n)[i]; st.dy = (s + 7 * n)[i];
+}
+
+// Diagnostic build only (-DRD_STAMPS, libreacher_stamps.so): per-wave s_memtime stamps
+// of the kernel's phases into a debug buffer nothing else reads.
+#ifdef RD_STAMPS
+#define STAMP(idx)                                                                      \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        unsigned long long t_;                                                          \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        if (lane == 0 && a.dbg) a.dbg[(blockIdx.x * WAVES + wave) * 16 + (idx)] += t_;   \
+    } while (0)
+#else
+#define STAMP(idx) do {} while (0)
+#endif
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// global net = params[P] | mu[11] | sd[11]  ->  LDS image (+ W2^T if `transposed`)
+__device__ void load_net(float* L, const float* g, bool transposed, int nthreads) {
     const float* mu = g + P_TOT;
     const float* sd = g + P_TOT + OBD;
-    for (int i = threadIdx.x; i < 12 * HID; i += BLOCK) {
-        const int k = i >> 6;
-        L[N_W1 + i] = k < OBD ? g[P_W1 + i] : 0.0f;
+    for (int i = threadIdx.x; i < 12 * HID; i += nthreads) {
+        const int k = i >> 6, f = i & 63;
+        L[N_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = k < OBD ? g[P_W1 + i] : g[P_B1 + f];
     }
-    for (int i = threadIdx.x; i < HID * HID; i += BLOCK) L[N_W2 + (i >> 6) * LDW + (i & 63)] = g[P_W2 + i];
-    for (int i = threadIdx.x; i < HID; i += BLOCK) {
-        L[N_B1 + i] = g[P_B1 + i];
-        L[N_B2 + i] = g[P_B2 + i];
+    for (int i = threadIdx.x; i < HID * HID; i += nthreads) {
+        const int k = i >> 6, f = i & 63;
+        L[N_W2 + k * HID + (f & 15) * 4 + (f >> 4)] = g[P_W2 + i];
     }
-    for (int i = threadIdx.x; i < HID * ACD; i += BLOCK) L[N_W3 + i] = g[P_W3 + i];
+    if (transposed)   // k fastest across lanes: the LDS writes spread over the banks
+        for (int i = threadIdx.x; i < HID * HID; i += nthreads) {
+            const int f = i >> 6, k = i & 63;
+            L[N_W2T + f * HID + (k & 15) * 4 + (k >> 4)] = g[P_W2 + k * HID + f];
+        }
+    for (int i = threadIdx.x; i < HID; i += nthreads) L[N_B2 + i] = g[P_B2 + i];
+    for (int i = threadIdx.x; i < HID * ACD; i += nthreads) L[N_W3 + i] = g[P_W3 + i];
     if (threadIdx.x < ACD) {
         L[N_B3 + threadIdx.x] = g[P_B3 + threadIdx.x];
         L[N_LS + threadIdx.x] = g[P_LS + threadIdx.x];
@@ -126,80 +183,78 @@ __device__ void load_net(float* L, const float* g) {
     if (threadIdx.x < 12) {
         const int k = threadIdx.x;
         L[N_MU + k] = k < OBD ? mu[k] : 0.0f;
-        L[N_RS + k] = k < OBD ? 1.0f / sd[k] : 0.0f;
+        L[N_RS + k] = k < OBD ? 1.0f / sd[k] : 1.0f;
     }
 }
 
-// MlpPolicy forward for the lane's env (obs in registers): H1, H2 in accumulator layout,
-// z = filtered observation, (m0, m1) = action mean (identical in both halves).
-__device__ __forceinline__ void mlp_forward(const float* L, const float ob[OBD], int lane, f32x16 (&H1)[2],
-                                            f32x16 (&H2)[2], float (&z)[12], float& m0, float& m1) {
-    const int h = lane >> 5, c = lane & 31;
+// MlpPolicy forward of the 16-env tile whose raw observations are rows ob[0..15] of the
+// wave's obs scratch (row stride SOS, component 11 = 1).  Lane (j, g):
+// H1, H2 = hidden activations, features 16 fb + 4 g + r of env j; (m0, m1) = action mean
+// of env j (identical in the four k-groups).
+__device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int j, int g, f32x4 (&H1)[4],
+                                            f32x4 (&H2)[4], float& m0, float& m1) {
+    f32x4 acc[4];
 #pragma unroll
-    for (int k = 0; k < OBD; ++k) z[k] = fminf(fmaxf((ob[k] - L[N_MU + k]) * L[N_RS + k], -5.0f), 5.0f);
-    z[11] = 0.0f;
-    f32x16 a0, a1;
+    for (int fb = 0; fb < 4; ++fb) acc[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // layer 1: K = 12 (11 filtered inputs + the bias input), k-step s covers inputs 4s+g
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        a0[r] = L[N_B1 + featD(r, h)];
-        a1[r] = L[N_B1 + 32 + featD(r, h)];
+    for (int s = 0; s < 3; ++s) {
+        const int k = 4 * s + g;
+        const float z = fminf(fmaxf((ob[j * SOS + k] - L[N_MU + k]) * L[N_RS + k], -5.0f), 5.0f);
+        const f32x4 w = ld4(L + N_W1 + k * HID + 4 * j);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], z, acc[fb]);
     }
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-        const float b = h ? z[2 * s + 1] : z[2 * s];
-        const float* w = L + N_W1 + (2 * s + h) * HID + c;
-        a0 = mfma(w[0], b, a0);
-        a1 = mfma(w[32], b, a1);
-    }
+    for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        H1[0][r] = tanh_f(a0[r]);
-        H1[1][r] = tanh_f(a1[r]);
-    }
+        for (int r = 0; r < 4; ++r) H1[fb][r] = tanh_f(acc[fb][r]);
+    // layer 2: K = 64; k-step (kb, r) uses features 16 kb + 4 g + r = this lane's H1[kb][r]
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        a0[r] = L[N_B2 + featD(r, h)];
-        a1[r] = L[N_B2 + 32 + featD(r, h)];
-    }
+    for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + N_B2 + 16 * fb + 4 * g);
+    // A operands prefetched one k-step ahead (LDS latency vs 4 MFMAs of 32 cycles)
+    f32x4 wn = ld4(L + N_W2 + (4 * g) * HID + 4 * j);
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float b = H1[kb][r];
-            const float* w = L + N_W2 + (32 * kb + featD(r, h)) * LDW + c;
-            a0 = mfma(w[0], b, a0);
-            a1 = mfma(w[32], b, a1);
+        for (int r = 0; r < 4; ++r) {
+            const f32x4 w = wn;
+            if (kb * 4 + r < 15) {
+                const int kn = (r == 3) ? 16 * (kb + 1) + 4 * g : 16 * kb + 4 * g + r + 1;
+                wn = ld4(L + N_W2 + kn * HID + 4 * j);
+            }
+#pragma unroll
+            for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], H1[kb][r], acc[fb]);
         }
     float p0 = 0.0f, p1 = 0.0f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        H2[0][r] = tanh_f(a0[r]);
-        H2[1][r] = tanh_f(a1[r]);
+    for (int fb = 0; fb < 4; ++fb) {
+        const f32x4 wa = ld4(L + N_W3 + (16 * fb + 4 * g) * 2);       // W3[f][0..1], f = 16fb+4g+0,1
+        const f32x4 wb = ld4(L + N_W3 + (16 * fb + 4 * g) * 2 + 4);   // f = 16fb+4g+2,3
+#pragma unroll
+        for (int r = 0; r < 4; ++r) H2[fb][r] = tanh_f(acc[fb][r]);
+        p0 = fmaf(H2[fb][0], wa[0], p0); p1 = fmaf(H2[fb][0], wa[1], p1);
+        p0 = fmaf(H2[fb][1], wa[2], p0); p1 = fmaf(H2[fb][1], wa[3], p1);
+        p0 = fmaf(H2[fb][2], wb[0], p0); p1 = fmaf(H2[fb][2], wb[1], p1);
+        p0 = fmaf(H2[fb][3], wb[2], p0); p1 = fmaf(H2[fb][3], wb[3], p1);
     }
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int f = 32 * kb + featD(r, h);
-            p0 = fmaf(H2[kb][r], L[N_W3 + 2 * f], p0);
-            p1 = fmaf(H2[kb][r], L[N_W3 + 2 * f + 1], p1);
-        }
-    p0 += __shfl_xor(p0, 32);
-    p1 += __shfl_xor(p1, 32);
+    p0 = xsum32(xsum16(p0));
+    p1 = xsum32(xsum16(p1));
     m0 = p0 + L[N_B3];
     m1 = p1 + L[N_B3 + 1];
 }
 
-__global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
+__global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
     float* LT = lds;
     float* LS = lds + NET;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int h = lane >> 5, c = lane & 31;
-    float* S = lds + 2 * NET + wave * SCR;
+    const int j = lane & 15, g = lane >> 4;
+    float* S = lds + NET + NET_S + wave * SCR;
 
-    load_net(LT, a.tnet);
-    load_net(LS, a.snet);
+    STAMP(0);
+    load_net(LT, a.tnet, false, BLOCK);
+    load_net(LS, a.snet, true, BLOCK);
 
     const uint32_t C = a.ctl[0];
     // snapshot of the step words for reduce_adam_kernel, which rewrites ctl[0..3]
@@ -210,202 +265,264 @@ __global__ __launch_bounds__(BLOCK, 1) void rollout_kernel(RolloutArgs a) {
     const float sl0 = a.snet[P_LS], sl1 = a.snet[P_LS + 1];
     const float tv0 = __expf(2.0f * tl0), tv1 = __expf(2.0f * tl1);
     const float sv0 = __expf(2.0f * sl0), sv1 = __expf(2.0f * sl1);
+    const float rtv0 = 1.0f / tv0, rtv1 = 1.0f / tv1;
 
-    f32x16 gW2[2][2], gW1[2];
+    // gradient accumulators, persistent over the wave's tiles
+    f32x4 gW2[4][4], gW1[4];
+    // db2, dW3 partial sums of lane (j, g): feature 16 nb + j over envs e = g (mod 4)
+    float gb2[4], gw3a[4], gw3b[4];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        gW2[0][0][r] = gW2[0][1][r] = gW2[1][0][r] = gW2[1][1][r] = 0.0f;
-        gW1[0][r] = gW1[1][r] = 0.0f;
+    for (int x = 0; x < 4; ++x) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) gW2[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+        gW1[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+        gb2[x] = gw3a[x] = gw3b[x] = 0.0f;
     }
-    float gb1 = 0, gb2 = 0, gw3a = 0, gw3b = 0, gb3a = 0, gb3b = 0, gls0 = 0, gls1 = 0;
+    float gb3a = 0, gb3b = 0, gls0 = 0, gls1 = 0;
     float met_r = 0, met_l = 0, met_m = 0, met_n = 0;
+    // student filter of input j for the dW1 A operand (lane-constant)
     __syncthreads();
+    const float smu = j < 12 ? LS[N_MU + j] : 0.0f, srs = j < 12 ? LS[N_RS + j] : 0.0f;
+    STAMP(1);
 
-    const int64_t ntiles = (a.n + 31) / 32;
-    for (int64_t t0 = (int64_t)blockIdx.x * WAVES; t0 < ntiles; t0 += (int64_t)gridDim.x * WAVES) {
-        const int64_t i = (t0 + wave) * 32 + c;
+    const int64_t ngroups = (a.n + GROUP - 1) / GROUP;
+    for (int64_t grp = (int64_t)blockIdx.x * WAVES + wave; grp < ngroups; grp += (int64_t)gridDim.x * WAVES) {
+        STAMP(2);   // (summed over the wave's groups)
+        const int64_t base = grp * GROUP;
+        const int64_t i = base + lane;
         const bool valid = i < a.n;
-        // ---------------------------------------------------------------- observe
+        // ------------------------------------------------------------ observe (one env per lane)
+        const uint32_t iu = (uint32_t)i;   // n <= 2^31: 32-bit lane offsets, uniform row bases
         rd::State st{};
-        if (valid) {
-            const float* s = a.state;
-            const int64_t n = a.n;
-            st.q0 = s[i]; st.q1 = s[n + i]; st.v0 = s[2 * n + i]; st.v1 = s[3 * n + i];
-            st.tx = s[4 * n + i]; st.ty = s[5 * n + i]; st.dx = s[6 * n + i]; st.dy = s[7 * n + i];
+        if (valid) load_state(a.state, a.n, iu, st);
+        {
+            float ob[OBD];
+            rd::observe(st, ob);
+            float* o = S + S_OB + lane * SOS;
+            st4(o, f32x4{ob[0], ob[1], ob[2], ob[3]});
+            st4(o + 4, f32x4{ob[4], ob[5], ob[6], ob[7]});
+            st4(o + 8, f32x4{ob[8], ob[9], ob[10], 1.0f});
         }
-        float ob[OBD];
-        rd::observe(st, ob);
-        // ---------------------------------------------------------------- teacher
-        float mt0, mt1, ms0, ms1;
-        f32x16 H1[2], H2[2];
-        float z[12];
-        mlp_forward(LT, ob, lane, H1, H2, z, mt0, mt1);
-        // ---------------------------------------------------------------- student
-        mlp_forward(LS, ob, lane, H1, H2, z, ms0, ms1);
-        // ---------------------------------------------------------------- loss
-        const float d0 = ms0 - mt0, d1 = ms1 - mt1;
-        float dm0, dm1, dl0 = 0.0f, dl1 = 0.0f, lossv;
-        if (a.loss == RDD_LOSS_MSE) {
-            dm0 = d0 * a.inv_n_global;
-            dm1 = d1 * a.inv_n_global;
-            lossv = (d0 * d0 + d1 * d1) * (0.5f * a.inv_n_global);
-        } else {
-            dm0 = d0 / tv0;
-            dm1 = d1 / tv1;
-            dl0 = sv0 / tv0 - 1.0f;
-            dl1 = sv1 / tv1 - 1.0f;
-            lossv = (tl0 - sl0 + (sv0 + d0 * d0) / (2.0f * tv0) - 0.5f) +
-                    (tl1 - sl1 + (sv1 + d1 * d1) / (2.0f * tv1) - 0.5f);
+        wave_sync();
+        STAMP(3);
+        float act0 = 0.0f, act1 = 0.0f;
+        const int ntile = (int)min((int64_t)(GROUP / TILE), (a.n - base + TILE - 1) / TILE);
+        for (int t = 0; t < ntile; ++t) {
+            if (a.prio_mode == 1) {          // SIMD partners (w, w+4): alternate the winner per tile
+                if (wave >= 4 && (t & 1) == 0) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            } else if (a.prio_mode == 2) {   // younger half always first
+                if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+            } else if (a.prio_mode == 3) {   // younger half first on its first group
+                if (wave >= 4 && grp < (int64_t)gridDim.x * WAVES) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+            const bool tvalid = base + TILE * t + j < a.n;
+            const float* obt = S + S_OB + TILE * t * SOS;
+            f32x4 H1[4], H2[4];
+            float mt0, mt1, ms0, ms1;
+            // ------------------------------------------------------------ teacher, student
+            mlp_forward(LT, obt, j, g, H1, H2, mt0, mt1);
+            mlp_forward(LS, obt, j, g, H1, H2, ms0, ms1);
+            if (g == t) {   // this lane steps env 16 t + j
+                act0 = a.act_student ? ms0 : mt0;
+                act1 = a.act_student ? ms1 : mt1;
+            }
+            // ------------------------------------------------------------ loss
+            const float d0 = ms0 - mt0, d1 = ms1 - mt1;
+            float dm0, dm1, dl0 = 0.0f, dl1 = 0.0f, lossv;
+            if (a.loss == RDD_LOSS_MSE) {
+                dm0 = d0 * a.inv_n_global;
+                dm1 = d1 * a.inv_n_global;
+                lossv = (d0 * d0 + d1 * d1) * (0.5f * a.inv_n_global);
+            } else {
+                dm0 = d0 * rtv0;
+                dm1 = d1 * rtv1;
+                dl0 = sv0 * rtv0 - 1.0f;
+                dl1 = sv1 * rtv1 - 1.0f;
+                lossv = (tl0 - sl0 + (sv0 + d0 * d0) * (0.5f * rtv0) - 0.5f) +
+                        (tl1 - sl1 + (sv1 + d1 * d1) * (0.5f * rtv1) - 0.5f);
+            }
+            if (!tvalid) { dm0 = dm1 = dl0 = dl1 = 0.0f; }
+            if (g == 0 && tvalid) {
+                met_l += lossv;
+                met_m += d0 * d0 + d1 * d1;
+                gb3a += dm0; gb3b += dm1; gls0 += dl0; gls1 += dl1;
+            }
+            // ------------------------------------------------------------ backward
+            // stage H1^T, H2^T (env-major rows) and the env's dmean (pad columns 64, 65)
+            float* SA = S + S_A;
+            float* SB = S + S_B;
+#pragma unroll
+            for (int fb = 0; fb < 4; ++fb) {
+                st4(SA + j * SAS + 16 * fb + 4 * g, H1[fb]);
+                st4(SB + j * SAS + 16 * fb + 4 * g, H2[fb]);
+            }
+            if (g == 0) { SB[j * SAS + 64] = dm0; SB[j * SAS + 65] = dm1; }
+            wave_sync();
+            // dW3 partials: lane (j, g) sums H2[16 nb + j][e] dm[e] over the tile's envs e = 4s+g
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const float* row = SB + (4 * s + g) * SAS;
+                const float e0 = row[64], e1 = row[65];
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb) {
+                    const float h = row[16 * nb + j];
+                    gw3a[nb] = fmaf(h, e0, gw3a[nb]);
+                    gw3b[nb] = fmaf(h, e1, gw3b[nb]);
+                }
+            }
+            // dZ2 = (W3 . dmean) * (1 - H2^2)   (accumulator layout)
+            f32x4 dZ[4];
+#pragma unroll
+            for (int fb = 0; fb < 4; ++fb) {
+                const f32x4 wa = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2);
+                const f32x4 wb = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2 + 4);
+                const float w0[4] = {wa[0], wa[2], wb[0], wb[2]}, w1[4] = {wa[1], wa[3], wb[1], wb[3]};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float h = H2[fb][r];
+                    dZ[fb][r] = fmaf(w0[r], dm0, w1[r] * dm1) * fmaf(-h, h, 1.0f);
+                }
+            }
+            wave_sync();   // every lane's H2^T reads are done
+#pragma unroll
+            for (int fb = 0; fb < 4; ++fb) st4(SB + j * SAS + 16 * fb + 4 * g, dZ[fb]);
+            wave_sync();
+            // dW2 += H1^T dZ2 over the tile's 16 envs (K = env, 4 per k-step)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                float x[4], y[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    x[b] = SA[(4 * s + g) * SAS + 16 * b + j];
+                    y[b] = SB[(4 * s + g) * SAS + 16 * b + j];
+                    gb2[b] += y[b];   // db2 partial: dZ2[16 b + j][e], e = 4s+g
+                }
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[mb], y[nb], gW2[mb][nb]);
+            }
+            // dH1 = W2 . dZ2  (A = W2^T image, B = dZ2 in accumulator layout)
+            f32x4 acc[4];
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
+#pragma unroll
+            for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const f32x4 w = wn;
+                    if (fb * 4 + r < 15) {
+                        const int kn = (r == 3) ? 16 * (fb + 1) + 4 * g : 16 * fb + 4 * g + r + 1;
+                        wn = ld4(LS + N_W2T + kn * HID + 4 * j);
+                    }
+#pragma unroll
+                    for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
+                }
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[mb][r] *= fmaf(-H1[mb][r], H1[mb][r], 1.0f);
+            wave_sync();   // every lane's dW2 reads of SA are done
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) st4(SA + j * SAS + 16 * mb + 4 * g, acc[mb]);
+            wave_sync();
+            // dW1 (+ db1 as input row 11) += z^T dZ1; A = student-filtered inputs of env 4s+g
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const float x = obt[(4 * s + g) * SOS + (j < 12 ? j : 0)];
+                const float z = j < 12 ? fminf(fmaxf((x - smu) * srs, -5.0f), 5.0f) : 0.0f;
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, SA[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
+            }
+            wave_sync();   // SA/SB are rewritten by the next tile
         }
-        if (!valid) { dm0 = dm1 = dl0 = dl1 = 0.0f; }
-        // ---------------------------------------------------------------- env.step
-        const float ac0 = a.act_student ? ms0 : mt0;
-        const float ac1 = a.act_student ? ms1 : mt1;
-        const float rew = rd::env_step(st, ac0, ac1);
-        // episode clock of this env (RDD_STAGGER_GROUP envs share an offset: wave-uniform
-        // unless a tile straddles a group boundary)
-        const int64_t g = a.env_base + i;
-        const uint32_t u = C + (a.stagger ? (uint32_t)((g / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);
+        STAMP(4);
+        // ------------------------------------------------------------ env.step (one env per lane)
+        if (valid) load_state(a.state, a.n, iu, st);   // re-read (L2-resident): no live range across the tiles
+        const float rew = rd::env_step(st, act0, act1);
+        // episode clock of this env (RDD_STAGGER_GROUP envs share an offset)
+        const int64_t gid = a.env_base + i;
+        const uint32_t u = C + (a.stagger ? (uint32_t)((gid / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);
         const bool done_step = (u % rd::kEpisodeSteps) == rd::kEpisodeSteps - 1;
         if (done_step) {
             float dr[6];
-            rd::philox_draw(a.seed, (uint64_t)g, u / rd::kEpisodeSteps + 1, dr);
+            rd::philox_draw(a.seed, (uint64_t)gid, u / rd::kEpisodeSteps + 1, dr);
             rd::env_reset(st, dr);
         }
-        if (valid && h == 0) {
+        if (valid) {
             float* s = a.state;
             const int64_t n = a.n;
-            s[i] = st.q0; s[n + i] = st.q1; s[2 * n + i] = st.v0; s[3 * n + i] = st.v1;
-            if (done_step) { s[4 * n + i] = st.tx; s[5 * n + i] = st.ty; }
-            s[6 * n + i] = st.dx; s[7 * n + i] = st.dy;
+            (s + 0 * n)[iu] = st.q0; (s + 1 * n)[iu] = st.q1; (s + 2 * n)[iu] = st.v0; (s + 3 * n)[iu] = st.v1;
+            if (done_step) { (s + 4 * n)[iu] = st.tx; (s + 5 * n)[iu] = st.ty; }
+            (s + 6 * n)[iu] = st.dx; (s + 7 * n)[iu] = st.dy;
             met_r += rew;
-            met_l += lossv;
-            met_m += d0 * d0 + d1 * d1;
             met_n += 1.0f;
-            gb3a += dm0; gb3b += dm1; gls0 += dl0; gls1 += dl1;
         }
-        // ---------------------------------------------------------------- backward
-        // dZ2 = (W3 . dmean) * (1 - H2^2)   (registers, accumulator layout)
-        f32x16 dZ[2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int f = 32 * kb + featD(r, h);
-                const float dh = fmaf(LS[N_W3 + 2 * f], dm0, LS[N_W3 + 2 * f + 1] * dm1);
-                dZ[kb][r] = dh * (1.0f - H2[kb][r] * H2[kb][r]);
-            }
-        // stage H1 | dZ2 | H2 | dmean (env-major rows) for the env-summed products
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int f = 32 * kb + featD(r, h);
-                S[S_B0 + c * LDW + f] = H1[kb][r];
-                S[S_B1 + c * LDW + f] = dZ[kb][r];
-                S[S_B2 + c * LDW + f] = H2[kb][r];
-            }
-        if (h == 0) {
-            S[S_DM + 2 * c] = dm0;
-            S[S_DM + 2 * c + 1] = dm1;
-        }
-        wave_sync();
-        // dW2 += H1^T dZ2 over the tile's 32 envs (K = env pairs)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const float* r0 = S + S_B0 + (2 * s + h) * LDW + c;
-            const float* r1 = S + S_B1 + (2 * s + h) * LDW + c;
-            const float x0 = r0[0], x1 = r0[32], y0 = r1[0], y1 = r1[32];
-            gW2[0][0] = mfma(x0, y0, gW2[0][0]);
-            gW2[0][1] = mfma(x0, y1, gW2[0][1]);
-            gW2[1][0] = mfma(x1, y0, gW2[1][0]);
-            gW2[1][1] = mfma(x1, y1, gW2[1][1]);
-        }
-        // db2, dW3: lane = feature, loop over envs
-#pragma unroll 8
-        for (int e = 0; e < 32; ++e) {
-            gb2 += S[S_B1 + e * LDW + lane];
-            const float hv = S[S_B2 + e * LDW + lane];
-            gw3a = fmaf(hv, S[S_DM + 2 * e], gw3a);
-            gw3b = fmaf(hv, S[S_DM + 2 * e + 1], gw3b);
-        }
-        // dH1 = W2 . dZ2  (A = W2 read column-wise from the padded image)
-        f32x16 acc0, acc1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.0f;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int k = 32 * kb + featD(r, h);
-                const float b = dZ[kb][r];
-                acc0 = mfma(LS[N_W2 + c * LDW + k], b, acc0);
-                acc1 = mfma(LS[N_W2 + (32 + c) * LDW + k], b, acc1);
-            }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            dZ[0][r] = acc0[r] * (1.0f - H1[0][r] * H1[0][r]);
-            dZ[1][r] = acc1[r] * (1.0f - H1[1][r] * H1[1][r]);
-        }
-        wave_sync();
-        // stage dZ1 and the student's filtered observation z (cols 0..31, zero-padded)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) S[S_B1 + c * LDW + 32 * kb + featD(r, h)] = dZ[kb][r];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) S[S_B0 + c * LDW + 16 * h + k] = (h == 0 && k < 12) ? z[k] : 0.0f;
-        wave_sync();
-        // dW1 += z^T dZ1  (rows = input feature, only 0..10 meaningful)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const float x = S[S_B0 + (2 * s + h) * LDW + c];
-            const float* r1 = S + S_B1 + (2 * s + h) * LDW + c;
-            gW1[0] = mfma(x, r1[0], gW1[0]);
-            gW1[1] = mfma(x, r1[32], gW1[1]);
-        }
-#pragma unroll 8
-        for (int e = 0; e < 32; ++e) gb1 += S[S_B1 + e * LDW + lane];
-        wave_sync();
+        STAMP(5);
     }
 
-    __syncthreads();   // the reduction below reuses every wave's scratch
+    STAMP(6);
     // ---------------------------------------------------------------- workgroup reduction
-    float* R = lds + 2 * NET + wave * P_PAD;   // reuses the scratch (all tiles done)
+    // per-lane partials over the env axis (k-groups g) -> one value per feature
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                R[P_W2 + (32 * mb + featD(r, h)) * HID + 32 * nb + c] = gW2[mb][nb][r];
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int k = featD(r, h);
-            if (k < OBD) R[P_W1 + k * HID + 32 * nb + c] = gW1[nb][r];
-        }
-    R[P_B1 + lane] = gb1;
-    R[P_B2 + lane] = gb2;
-    R[P_W3 + 2 * lane] = gw3a;
-    R[P_W3 + 2 * lane + 1] = gw3b;
+    for (int nb = 0; nb < 4; ++nb) {
+        gb2[nb] = xsum32(xsum16(gb2[nb]));
+        gw3a[nb] = xsum32(xsum16(gw3a[nb]));
+        gw3b[nb] = xsum32(xsum16(gw3b[nb]));
+    }
     gb3a = wave_sum(gb3a); gb3b = wave_sum(gb3b);
     gls0 = wave_sum(gls0); gls1 = wave_sum(gls1);
     met_r = wave_sum(met_r); met_l = wave_sum(met_l); met_m = wave_sum(met_m); met_n = wave_sum(met_n);
-    if (lane == 0) {
-        R[P_B3] = gb3a; R[P_B3 + 1] = gb3b; R[P_LS] = gls0; R[P_LS + 1] = gls1;
-        R[P_TOT] = met_r; R[P_TOT + 1] = met_l; R[P_TOT + 2] = met_m; R[P_TOT + 3] = met_n;
-    }
-    __syncthreads();
-    const float* R0 = lds + 2 * NET;
-    float* out = a.ws + (int64_t)blockIdx.x * P_PAD;
-    for (int p = threadIdx.x; p < P_PAD; p += BLOCK) {
-        float s = R0[p];
+    __syncthreads();   // every wave is done with its scratch
+    STAMP(9);
+    // waves 0-3 store into region w, then waves 4-7 add into region w-4 (fixed order)
+    float* R = lds + NET + NET_S + (wave & 3) * P_PAD;
 #pragma unroll
-        for (int w = 1; w < WAVES; ++w) s += R0[w * P_PAD + p];
-        out[p] = s;
+    for (int phase = 0; phase < 2; ++phase) {
+        if ((wave >> 2) == phase) {
+            auto put = [&](int p, float v) { R[p] = phase ? R[p] + v : v; };
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        put(P_W2 + (16 * mb + 4 * g + r) * HID + 16 * nb + j, gW2[mb][nb][r]);
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int k = 4 * g + r;
+                    if (k < OBD) put(P_W1 + k * HID + 16 * nb + j, gW1[nb][r]);
+                    else if (k == OBD) put(P_B1 + 16 * nb + j, gW1[nb][r]);
+                }
+            if (g == 0) {
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb) {
+                    const int f = 16 * nb + j;
+                    put(P_B2 + f, gb2[nb]);
+                    put(P_W3 + 2 * f, gw3a[nb]);
+                    put(P_W3 + 2 * f + 1, gw3b[nb]);
+                }
+            }
+            if (lane == 0) {
+                put(P_B3, gb3a); put(P_B3 + 1, gb3b); put(P_LS, gls0); put(P_LS + 1, gls1);
+                put(P_TOT, met_r); put(P_TOT + 1, met_l); put(P_TOT + 2, met_m); put(P_TOT + 3, met_n);
+            }
+        }
+        __syncthreads();
     }
+    const float* R0 = lds + NET + NET_S;
+    float* out = a.ws + (int64_t)blockIdx.x * P_PAD;
+    for (int p = threadIdx.x; p < P_PAD; p += BLOCK)
+        out[p] = (R0[p] + R0[P_PAD + p]) + (R0[2 * P_PAD + p] + R0[3 * P_PAD + p]);
+    STAMP(7);
+#ifdef RD_STAMPS
+    if (lane == 0 && a.dbg) a.dbg[(blockIdx.x * WAVES + wave) * 16 + 8] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // ctl words: [0] completed steps C, [2] beta1^t, [3] beta2^t (f32 bits); [4..7] the
@@ -502,34 +619,40 @@ __global__ __launch_bounds__(256) void init_ctl_kernel(uint32_t* ctl, float b1, 
     }
 }
 
-// policy query: obs rows -> pdflat of teacher and/or student (one 32-env tile per wave)
-__global__ __launch_bounds__(BLOCK, 1) void forward_kernel(const float* tnet, const float* snet, const float* obs,
-                                                           int64_t n, float* tflat, float* sflat) {
-    __shared__ __attribute__((aligned(16))) float lds[2 * NET];
-    load_net(lds, tnet);
-    load_net(lds + NET, snet);
+// policy query: obs rows -> pdflat of teacher and/or student (one 16-env tile per wave pass)
+__global__ __launch_bounds__(FBLOCK) void forward_kernel(const float* tnet, const float* snet, const float* obs,
+                                                         int64_t n, float* tflat, float* sflat) {
+    __shared__ __attribute__((aligned(16))) float lds[2 * NET + FWAVES * TILE * SOS];
+    load_net(lds, tnet, false, FBLOCK);
+    load_net(lds + NET, snet, false, FBLOCK);
     __syncthreads();
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31;
-    const int64_t ntiles = (n + 31) / 32;
-    for (int64_t t0 = (int64_t)blockIdx.x * WAVES + wave; t0 < ntiles; t0 += (int64_t)gridDim.x * WAVES) {
-        const int64_t i = t0 * 32 + c;
-        float ob[OBD];
-#pragma unroll
-        for (int k = 0; k < OBD; ++k) ob[k] = i < n ? obs[i * OBD + k] : 0.0f;
-        f32x16 H1[2], H2[2];
-        float z[12], m0, m1;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    float* ob = lds + 2 * NET + wave * TILE * SOS;
+    const int64_t ntiles = (n + TILE - 1) / TILE;
+    for (int64_t t = (int64_t)blockIdx.x * FWAVES + wave; t < ntiles; t += (int64_t)gridDim.x * FWAVES) {
+        // raw observations of the tile's 16 envs -> scratch rows (component 11 = 1)
+        for (int x = lane; x < TILE * SOS; x += 64) {
+            const int e = x / SOS, k = x % SOS;
+            const int64_t i = t * TILE + e;
+            ob[x] = k == OBD ? 1.0f : (i < n ? obs[i * OBD + k] : 0.0f);
+        }
+        wave_sync();
+        const int64_t i = t * TILE + j;
+        f32x4 H1[4], H2[4];
+        float m0, m1;
         for (int net = 0; net < 2; ++net) {
             float* out = net ? sflat : tflat;
             if (!out) continue;   // wave-uniform
             const float* L = lds + net * NET;
-            mlp_forward(L, ob, lane, H1, H2, z, m0, m1);
-            if (i < n && lane < 32) {
+            mlp_forward(L, ob, j, g, H1, H2, m0, m1);
+            if (i < n && g == 0) {
                 out[i * 4 + 0] = m0;
                 out[i * 4 + 1] = m1;
                 out[i * 4 + 2] = L[N_LS];
                 out[i * 4 + 3] = L[N_LS + 1];
             }
         }
+        wave_sync();
     }
 }
 
@@ -556,6 +679,8 @@ struct rdd_trainer {
     float* ws = nullptr;       // [grid][P_PAD]
     float* hist = nullptr;     // [hist_len][4]
     uint32_t* ctl = nullptr;   // [8]: step words + snapshot
+    unsigned long long* dbg = nullptr;   // RD_STAMPS builds only
+    int prio_mode = 0;
 };
 
 namespace {
@@ -573,6 +698,8 @@ int launch_rollout(rdd_trainer* t) {
     a.loss = t->cfg.loss;
     a.act_student = t->cfg.act_with == RDD_ACT_STUDENT;
     a.stagger = t->cfg.stagger;
+    a.dbg = t->dbg;
+    a.prio_mode = t->prio_mode;
     a.inv_n_global = 1.0f / (float)t->cfg.n_envs_global;
     hipLaunchKernelGGL(rollout_kernel, dim3(t->grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
@@ -626,11 +753,12 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     rdd_trainer* t = new (std::nothrow) rdd_trainer();
     if (!t) return rd::set_error(RD_EINVAL, "rdd_create: out of host memory");
     t->cfg = *cfg;
+    if (const char* pm = getenv("RDD_PRIO_MODE")) t->prio_mode = atoi(pm);
     if (t->cfg.metrics_len == 0) t->cfg.metrics_len = 4096;
     t->device = device;
     t->stream = (hipStream_t)hip_stream;
-    const int64_t ntiles = (cfg->n_envs + 31) / 32;
-    const int64_t want = (ntiles + WAVES - 1) / WAVES;
+    const int64_t ngroups = (cfg->n_envs + GROUP - 1) / GROUP;
+    const int64_t want = (ngroups + WAVES - 1) / WAVES;
     const int cap = cfg->grid > 0 ? cfg->grid : num_cus(device);
     t->grid = (int)(want < cap ? want : cap);
     const size_t netf = P_TOT + 2 * OBD;
@@ -649,6 +777,9 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     alloc((void**)&t->ws, sizeof(float) * (size_t)t->grid * P_PAD);
     alloc((void**)&t->hist, sizeof(float) * (size_t)t->cfg.metrics_len * N_MET);
     alloc((void**)&t->ctl, sizeof(uint32_t) * 8);
+#ifdef RD_STAMPS
+    alloc((void**)&t->dbg, sizeof(unsigned long long) * (size_t)t->grid * WAVES * 16);
+#endif
     if (e != hipSuccess) {
         rdd_destroy(t);
         return rd::hip_fail(e, "rdd_create: allocation");
@@ -661,7 +792,7 @@ int rdd_destroy(rdd_trainer* t) {
     if (!t) return RD_OK;
     rd::DeviceGuard g(t->device);
     for (void* p : {(void*)t->state, (void*)t->tnet, (void*)t->snet, (void*)t->m, (void*)t->v, (void*)t->own_grad,
-                    (void*)t->ws, (void*)t->hist, (void*)t->ctl})
+                    (void*)t->ws, (void*)t->hist, (void*)t->ctl, (void*)t->dbg})
         if (p) (void)hipFree(p);
     delete t;
     return RD_OK;
@@ -756,10 +887,10 @@ int rdd_forward(rdd_trainer* t, const float* obs, int64_t n, float* tflat, float
     if (!t || !obs || n <= 0) return rd::set_error(RD_EINVAL, "rdd_forward: bad argument");
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_forward: hipSetDevice");
-    const int64_t ntiles = (n + 31) / 32;
-    int64_t blocks = (ntiles + WAVES - 1) / WAVES;
-    if (blocks > 4 * num_cus(t->device)) blocks = 4 * num_cus(t->device);
-    hipLaunchKernelGGL(forward_kernel, dim3((unsigned)blocks), dim3(BLOCK), 0, t->stream, t->tnet, t->snet, obs,
+    const int64_t ntiles = (n + TILE - 1) / TILE;
+    int64_t blocks = (ntiles + FWAVES - 1) / FWAVES;
+    if (blocks > 2 * num_cus(t->device)) blocks = 2 * num_cus(t->device);
+    hipLaunchKernelGGL(forward_kernel, dim3((unsigned)blocks), dim3(FBLOCK), 0, t->stream, t->tnet, t->snet, obs,
                        n, tflat, sflat);
     RD_HIP(hipGetLastError(), "forward_kernel launch");
     return RD_OK;
@@ -812,5 +943,18 @@ int rdd_read_metrics(rdd_trainer* t, int64_t count, double* out) {
     delete[] host;
     return RD_OK;
 }
+
+#ifdef RD_STAMPS
+// Diagnostic build only: copy (and zero) the per-wave stamp sums [grid*8][16] to the host.
+int rdd_debug_stamps(rdd_trainer* t, unsigned long long* out, int64_t cap) {
+    if (!t || !out || !t->dbg) return rd::set_error(RD_EINVAL, "rdd_debug_stamps: bad argument");
+    const int64_t cnt = (int64_t)t->grid * WAVES * 16;
+    if (cap < cnt) return rd::set_error(RD_EINVAL, "rdd_debug_stamps: need %lld", (long long)cnt);
+    RD_HIP(hipStreamSynchronize(t->stream), "rdd_debug_stamps");
+    RD_HIP(hipMemcpy(out, t->dbg, sizeof(unsigned long long) * cnt, hipMemcpyDeviceToHost), "rdd_debug_stamps");
+    RD_HIP(hipMemset(t->dbg, 0, sizeof(unsigned long long) * cnt), "rdd_debug_stamps");
+    return (int)cnt;
+}
+#endif
 
 }  // extern "C"

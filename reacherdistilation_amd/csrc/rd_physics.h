@@ -41,14 +41,37 @@ struct State {
     float q0, q1, v0, v1, tx, ty, dx, dy;   // (dx,dy) = fingertip - target at the held kinematics
 };
 
-__device__ __forceinline__ void sincos_acc(float x, float* s, float* c) { sincosf(x, s, c); }
+// sin and cos together for the joint angles (|x| < 8192 rad: the arm angle resets every 50
+// steps, |q| stays < ~30).  Cody-Waite reduction by pi/2 with a 3-part constant (fma, exact
+// k*C1) and Cephes' minimax polynomials on [-pi/4, pi/4]: <= 2 ulp, ~20 VALU instead of the
+// ~45 of the libm path.  Larger arguments take the libm path (never on the hot path).
+__device__ __forceinline__ void sincos_acc(float x, float* s, float* c) {
+    if (__builtin_expect(fabsf(x) > 8192.0f, 0)) {
+        sincosf(x, s, c);
+        return;
+    }
+    const float k = rintf(x * 0.636619772367581343f);          // 2/pi
+    float r = __fmaf_rn(k, -1.5703125f, x);                     // exact: k*1.5703125 fits
+    r = __fmaf_rn(k, -4.837512969970703125e-4f, r);
+    r = __fmaf_rn(k, -7.54978995489188216e-8f, r);
+    const float z = r * r;
+    float ps = __fmaf_rn(-1.9515295891e-4f, z, 8.3321608736e-3f);
+    ps = __fmaf_rn(ps, z, -1.6666654611e-1f);
+    const float sr = __fmaf_rn(ps * z, r, r);
+    float pc = __fmaf_rn(2.443315711809948e-5f, z, -1.388731625493765e-3f);
+    pc = __fmaf_rn(pc, z, 4.166664568298827e-2f);
+    const float cr = __fmaf_rn(pc * z, z, __fmaf_rn(-0.5f, z, 1.0f));
+    const int q = (int)k & 3;
+    const float sv = (q & 1) ? cr : sr;
+    const float cv = (q & 1) ? sr : cr;
+    *s = (q & 2) ? -sv : sv;
+    *c = ((q + 1) & 2) ? -cv : cv;
+}
 
-// One MuJoCo forward pass -> constrained qacc of the two arm dofs.
-__device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, float c1,
-                                     float& a0, float& a1) {
+// One MuJoCo forward pass -> constrained qacc of the two arm dofs; (s, c) = sin, cos q1.
+__device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, float v1, float c0, float c1,
+                                        float& a0, float& a1) {
     const float A0 = (float)kA0, I2 = (float)kI2, HC = (float)kHC;
-    float s, c;
-    sincos_acc(q1, &s, &c);
     const float m11 = A0 + I2 + 2.0f * HC * c + 1.0f;
     const float m12 = I2 + HC * c;
     const float m22 = I2 + 1.0f;
@@ -56,7 +79,7 @@ __device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, flo
     const float b1 = HC * s * v0 * v0;
     const float t0 = 200.0f * c0 - v0 - b0;
     const float t1 = 200.0f * c1 - v1 - b1;
-    const float rdet = 1.0f / (m11 * m22 - m12 * m12);
+    const float rdet = __builtin_amdgcn_rcpf(m11 * m22 - m12 * m12);   // 1 ulp
     const float i11 = m22 * rdet, i12 = -m12 * rdet, i22 = m11 * rdet;
     a0 = i11 * t0 + i12 * t1;
     a1 = i12 * t0 + i22 * t1;
@@ -76,6 +99,12 @@ __device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, flo
     }
 }
 
+__device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, float c1, float& a0, float& a1) {
+    float s, c;
+    sincos_acc(q1, &s, &c);
+    qacc_sc(q1, s, c, v0, v1, c0, c1, a0, a1);
+}
+
 // env.step on one env: returns the reward (computed from the held stale fingertip,
 // float32 ctrl cost of the UNCLIPPED action), advances the state by 2 RK4 substeps.
 __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
@@ -84,7 +113,7 @@ __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
     const float c0 = fminf(fmaxf(a0, -1.0f), 1.0f);   // ctrlrange +-1 (ctrllimited)
     const float c1 = fminf(fmaxf(a1, -1.0f), 1.0f);
     float q0 = st.q0, q1 = st.q1, v0 = st.v0, v1 = st.v1;
-    float kq0 = q0, kq1 = q1;
+    float kq0 = q0, kq1 = q1, s4 = 0.0f, c4 = 1.0f;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
         float k1a, k1b, k2a, k2b, k3a, k3b, k4a, k4b;
@@ -96,16 +125,18 @@ __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
         const float v0d = v0 + h * k3a, v1d = v1 + h * k3b;
         kq0 = q0 + h * v0c;
         kq1 = q1 + h * v1c;
-        qacc(kq1, v0d, v1d, c0, c1, k4a, k4b);
+        sincos_acc(kq1, &s4, &c4);   // also the held kinematics' q1 after the 2nd substep
+        qacc_sc(kq1, s4, c4, v0d, v1d, c0, c1, k4a, k4b);
         const float b1 = 1.0f / 6.0f, b2 = 1.0f / 3.0f;
         q0 += h * (v0 * b1 + v0b * b2 + v0c * b2 + v0d * b1);
         q1 += h * (v1 * b1 + v1b * b2 + v1c * b2 + v1d * b1);
         v0 += h * (k1a * b1 + k2a * b2 + k3a * b2 + k4a * b1);
         v1 += h * (k1b * b1 + k2b * b2 + k3b * b2 + k4b * b1);
     }
-    float s0, c0k, s01, c01;
+    float s0, c0k;
     sincos_acc(kq0, &s0, &c0k);
-    sincos_acc(kq0 + kq1, &s01, &c01);
+    const float s01 = __fmaf_rn(s0, c4, c0k * s4);    // sin(kq0 + kq1)
+    const float c01 = __fmaf_rn(c0k, c4, -s0 * s4);   // cos(kq0 + kq1)
     st.q0 = q0; st.q1 = q1; st.v0 = v0; st.v1 = v1;
     st.dx = 0.1f * c0k + 0.11f * c01 - st.tx;
     st.dy = 0.1f * s0 + 0.11f * s01 - st.ty;
