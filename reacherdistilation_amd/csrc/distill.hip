@@ -73,16 +73,26 @@ constexpr int N_W2T = NET;               // student only: [j][i&15][i>>4] = W2[i
 constexpr int NET_S = NET + HID * HID;
 static_assert(N_B2 % 4 == 0 && N_W3 % 4 == 0 && NET % 4 == 0, "16-B aligned LDS vectors");
 
-// ---------------------------------------------------------------- per-wave scratch
-constexpr int SOS = 12;                  // raw obs rows (11 + the bias input = 1)
-constexpr int SAS = 68;                  // transposed activation rows [env][64 + pad]
-constexpr int S_OB = 0;                  // [64][12]
-constexpr int S_A = S_OB + GROUP * SOS;  // [16][SAS]  H1^T, then dZ1^T
-constexpr int S_B = S_A + TILE * SAS;    // [16][SAS]  dZ2^T
-constexpr int SCR = S_B + TILE * SAS;
-constexpr int LDS_FLOATS = NET + NET_S + WAVES * SCR;
+// ---------------------------------------------------------------- per-pair scratch
+// Waves w and w + 4 of a workgroup share a SIMD.  They form a PAIR with fixed roles:
+// the producer (w < 4) computes observations, teacher and student forwards, the loss and
+// dZ2; the consumer (w + 4) computes the weight gradients and dH1/dZ1 and steps the envs.
+// They hand over one 16-env tile at a time through an LDS slot guarded by two counters.
+constexpr int PAIRS = WAVES / 2;
+constexpr int SOS = 12;                         // raw obs rows (11 + the bias input = 1)
+constexpr int SAS = 68;                         // transposed activation rows [env][64 + pad]
+constexpr int P_SO = 0;                         // [2][64][12] raw obs, by group parity
+constexpr int P_ACT = P_SO + 2 * GROUP * SOS;   // [2][64][2] actions, by group parity
+constexpr int P_H1T = P_ACT + 2 * GROUP * 2;    // slot: H1^T [16][SAS]
+constexpr int P_DZT = P_H1T + TILE * SAS;       // slot: dZ2^T [16][SAS]
+constexpr int P_SA = P_DZT + TILE * SAS;        // consumer-private: dZ1^T [16][SAS]
+constexpr int P_FLAGS = P_SA + TILE * SAS;      // u32 [0] tiles published [1] tiles consumed [2] groups done
+constexpr int PSCR = P_FLAGS + 4;
+constexpr int LDS_FLOATS = NET + NET_S + PAIRS * PSCR;
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
-static_assert(4 * P_PAD <= WAVES * SCR, "final reduction must fit in the scratch");
+static_assert(PSCR % 4 == 0 && P_H1T % 4 == 0 && P_DZT % 4 == 0 && P_SA % 4 == 0, "16-B aligned scratch");
+static_assert(PAIRS * P_PAD <= LDS_FLOATS, "final reduction must fit in the LDS");
+constexpr uint32_t SPIN_LIMIT = 1u << 22;       // ~0.1 s of s_sleep: a broken hand-off ends the launch
 
 struct RolloutArgs {
     int64_t n, env_base;
@@ -95,7 +105,6 @@ struct RolloutArgs {
     int loss, act_student, stagger;
     float inv_n_global;
     unsigned long long* dbg;               // RD_STAMPS builds: [grid*WAVES][16] stamp sums
-    int prio_mode;                         // experiment knob (RDD_PRIO_MODE env var)
 };
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
@@ -244,285 +253,333 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
     m1 = p1 + L[N_B3 + 1];
 }
 
+// Hand-off counters live in LDS; each is written by one wave only.  Acquire/release at
+// workgroup scope order the slot data (LDS) around them.  A spin that exceeds SPIN_LIMIT
+// raises ctl[8] and returns false: the caller leaves its loop, so the launch always ends.
+__device__ __forceinline__ bool wait_ge(const uint32_t* f, uint32_t target, uint32_t* err) {
+    for (uint32_t spins = 0;; ++spins) {
+        if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+        if (spins > SPIN_LIMIT) {
+            if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+__device__ __forceinline__ void publish(uint32_t* f, uint32_t v) {
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
     float* LT = lds;
     float* LS = lds + NET;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
-    float* S = lds + NET + NET_S + wave * SCR;
+    const int pair = wave & (PAIRS - 1);
+    const bool producer = wave < PAIRS;
+    float* PS = lds + NET + NET_S + pair * PSCR;
+    uint32_t* flags = reinterpret_cast<uint32_t*>(lds + NET + NET_S + pair * PSCR + P_FLAGS);
+    uint32_t* err = a.ctl + 8;
 
     STAMP(0);
     load_net(LT, a.tnet, false, BLOCK);
     load_net(LS, a.snet, true, BLOCK);
+    if (threadIdx.x < PAIRS * 4)
+        reinterpret_cast<uint32_t*>(lds + NET + NET_S + (threadIdx.x >> 2) * PSCR + P_FLAGS)[threadIdx.x & 3] = 0u;
 
     const uint32_t C = a.ctl[0];
     // snapshot of the step words for reduce_adam_kernel, which rewrites ctl[0..3]
     if (blockIdx.x == 0 && threadIdx.x < 4) a.ctl[4 + threadIdx.x] = a.ctl[threadIdx.x];
-
-    // teacher / student log-std (state independent)
-    const float tl0 = a.tnet[P_LS], tl1 = a.tnet[P_LS + 1];
-    const float sl0 = a.snet[P_LS], sl1 = a.snet[P_LS + 1];
-    const float tv0 = __expf(2.0f * tl0), tv1 = __expf(2.0f * tl1);
-    const float sv0 = __expf(2.0f * sl0), sv1 = __expf(2.0f * sl1);
-    const float rtv0 = 1.0f / tv0, rtv1 = 1.0f / tv1;
-
-    // gradient accumulators, persistent over the wave's tiles
-    f32x4 gW2[4][4], gW1[4];
-    // db2, dW3 partial sums of lane (j, g): feature 16 nb + j over envs e = g (mod 4)
-    float gb2[4], gw3a[4], gw3b[4];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-#pragma unroll
-        for (int y = 0; y < 4; ++y) gW2[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-        gW1[x] = f32x4{0.f, 0.f, 0.f, 0.f};
-        gb2[x] = gw3a[x] = gw3b[x] = 0.0f;
-    }
-    float gb3a = 0, gb3b = 0, gls0 = 0, gls1 = 0;
-    float met_r = 0, met_l = 0, met_m = 0, met_n = 0;
-    // student filter of input j for the dW1 A operand (lane-constant)
     __syncthreads();
-    const float smu = j < 12 ? LS[N_MU + j] : 0.0f, srs = j < 12 ? LS[N_RS + j] : 0.0f;
     STAMP(1);
 
     const int64_t ngroups = (a.n + GROUP - 1) / GROUP;
-    for (int64_t grp = (int64_t)blockIdx.x * WAVES + wave; grp < ngroups; grp += (int64_t)gridDim.x * WAVES) {
-        STAMP(2);   // (summed over the wave's groups)
-        const int64_t base = grp * GROUP;
-        const int64_t i = base + lane;
-        const bool valid = i < a.n;
-        // ------------------------------------------------------------ observe (one env per lane)
-        const uint32_t iu = (uint32_t)i;   // n <= 2^31: 32-bit lane offsets, uniform row bases
-        rd::State st{};
-        if (valid) load_state(a.state, a.n, iu, st);
-        {
-            float ob[OBD];
-            rd::observe(st, ob);
-            float* o = S + S_OB + lane * SOS;
-            st4(o, f32x4{ob[0], ob[1], ob[2], ob[3]});
-            st4(o + 4, f32x4{ob[4], ob[5], ob[6], ob[7]});
-            st4(o + 8, f32x4{ob[8], ob[9], ob[10], 1.0f});
+    const int64_t gstride = (int64_t)gridDim.x * PAIRS;
+    const int64_t gfirst = (int64_t)blockIdx.x * PAIRS + pair;
+
+    if (producer) {
+        // ============================================================ producer wave
+        // partial sums: dW3 (env j of this lane, features 16x+4g+r), db3, dlogstd, metrics
+        f32x4 gw3a[4], gw3b[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) gw3a[x] = gw3b[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float gb3a = 0, gb3b = 0, gls0 = 0, gls1 = 0, met_l = 0, met_m = 0;
+        const float tl0 = a.tnet[P_LS], tl1 = a.tnet[P_LS + 1];
+        const float sl0 = a.snet[P_LS], sl1 = a.snet[P_LS + 1];
+        const float sv0 = __expf(2.0f * sl0), sv1 = __expf(2.0f * sl1);
+        const float rtv0 = 1.0f / __expf(2.0f * tl0), rtv1 = 1.0f / __expf(2.0f * tl1);
+        uint32_t tiles = 0;
+        uint32_t k = 0;
+        bool ok = true;
+        for (int64_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
+            // the consumer is done with group k-2 (same obs/action buffers)
+            if (k >= 2 && !(ok = wait_ge(flags + 2, k - 1, err))) break;
+            const int64_t base = grp * GROUP;
+            const int64_t i = base + lane;
+            float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
+            float* act = PS + P_ACT + (k & 1) * GROUP * 2;
+            {
+                rd::State st{};
+                if (i < a.n) load_state(a.state, a.n, (uint32_t)i, st);
+                float ob[OBD];
+                rd::observe(st, ob);
+                float* o = obs + lane * SOS;
+                st4(o, f32x4{ob[0], ob[1], ob[2], ob[3]});
+                st4(o + 4, f32x4{ob[4], ob[5], ob[6], ob[7]});
+                st4(o + 8, f32x4{ob[8], ob[9], ob[10], 1.0f});
+            }
+            wave_sync();
+            const int ntile = (int)min((int64_t)(GROUP / TILE), (a.n - base + TILE - 1) / TILE);
+            for (int t = 0; t < ntile; ++t) {
+                const bool tvalid = base + TILE * t + j < a.n;
+                const float* obt = obs + TILE * t * SOS;
+                f32x4 H1[4], H2[4];
+                float mt0, mt1, ms0, ms1;
+                mlp_forward(LT, obt, j, g, H1, H2, mt0, mt1);
+                mlp_forward(LS, obt, j, g, H1, H2, ms0, ms1);
+                // loss
+                const float d0 = ms0 - mt0, d1 = ms1 - mt1;
+                float dm0, dm1, dl0 = 0.0f, dl1 = 0.0f, lossv;
+                if (a.loss == RDD_LOSS_MSE) {
+                    dm0 = d0 * a.inv_n_global;
+                    dm1 = d1 * a.inv_n_global;
+                    lossv = (d0 * d0 + d1 * d1) * (0.5f * a.inv_n_global);
+                } else {
+                    dm0 = d0 * rtv0;
+                    dm1 = d1 * rtv1;
+                    dl0 = sv0 * rtv0 - 1.0f;
+                    dl1 = sv1 * rtv1 - 1.0f;
+                    lossv = (tl0 - sl0 + (sv0 + d0 * d0) * (0.5f * rtv0) - 0.5f) +
+                            (tl1 - sl1 + (sv1 + d1 * d1) * (0.5f * rtv1) - 0.5f);
+                }
+                if (!tvalid) { dm0 = dm1 = dl0 = dl1 = 0.0f; }
+                if (g == 0 && tvalid) {
+                    met_l += lossv;
+                    met_m += d0 * d0 + d1 * d1;
+                    gb3a += dm0; gb3b += dm1; gls0 += dl0; gls1 += dl1;
+                    act[(TILE * t + j) * 2] = a.act_student ? ms0 : mt0;
+                    act[(TILE * t + j) * 2 + 1] = a.act_student ? ms1 : mt1;
+                }
+                // dW3 partials (env j of this lane) and dZ2 = (W3 . dmean) * (1 - H2^2)
+                f32x4 dZ[4];
+#pragma unroll
+                for (int fb = 0; fb < 4; ++fb) {
+                    const f32x4 wa = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2);
+                    const f32x4 wb = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2 + 4);
+                    const float w0[4] = {wa[0], wa[2], wb[0], wb[2]}, w1[4] = {wa[1], wa[3], wb[1], wb[3]};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float h = H2[fb][r];
+                        gw3a[fb][r] = fmaf(h, dm0, gw3a[fb][r]);
+                        gw3b[fb][r] = fmaf(h, dm1, gw3b[fb][r]);
+                        dZ[fb][r] = fmaf(w0[r], dm0, w1[r] * dm1) * fmaf(-h, h, 1.0f);
+                    }
+                }
+                // hand the tile over: H1^T, dZ2^T (env-major rows) into the slot
+                STAMP(2);
+                if (!(ok = wait_ge(flags + 1, tiles, err))) break;
+                STAMP(3);
+                float* h1t = PS + P_H1T;
+                float* dzt = PS + P_DZT;
+#pragma unroll
+                for (int fb = 0; fb < 4; ++fb) {
+                    st4(h1t + j * SAS + 16 * fb + 4 * g, H1[fb]);
+                    st4(dzt + j * SAS + 16 * fb + 4 * g, dZ[fb]);
+                }
+                publish(flags, ++tiles);
+            }
         }
-        wave_sync();
-        STAMP(3);
-        float act0 = 0.0f, act1 = 0.0f;
-        const int ntile = (int)min((int64_t)(GROUP / TILE), (a.n - base + TILE - 1) / TILE);
-        for (int t = 0; t < ntile; ++t) {
-            if (a.prio_mode == 1) {          // SIMD partners (w, w+4): alternate the winner per tile
-                if (wave >= 4 && (t & 1) == 0) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            } else if (a.prio_mode == 2) {   // younger half always first
-                if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-            } else if (a.prio_mode == 3) {   // younger half first on its first group
-                if (wave >= 4 && grp < (int64_t)gridDim.x * WAVES) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-            const bool tvalid = base + TILE * t + j < a.n;
-            const float* obt = S + S_OB + TILE * t * SOS;
-            f32x4 H1[4], H2[4];
-            float mt0, mt1, ms0, ms1;
-            // ------------------------------------------------------------ teacher, student
-            mlp_forward(LT, obt, j, g, H1, H2, mt0, mt1);
-            mlp_forward(LS, obt, j, g, H1, H2, ms0, ms1);
-            if (g == t) {   // this lane steps env 16 t + j
-                act0 = a.act_student ? ms0 : mt0;
-                act1 = a.act_student ? ms1 : mt1;
-            }
-            // ------------------------------------------------------------ loss
-            const float d0 = ms0 - mt0, d1 = ms1 - mt1;
-            float dm0, dm1, dl0 = 0.0f, dl1 = 0.0f, lossv;
-            if (a.loss == RDD_LOSS_MSE) {
-                dm0 = d0 * a.inv_n_global;
-                dm1 = d1 * a.inv_n_global;
-                lossv = (d0 * d0 + d1 * d1) * (0.5f * a.inv_n_global);
-            } else {
-                dm0 = d0 * rtv0;
-                dm1 = d1 * rtv1;
-                dl0 = sv0 * rtv0 - 1.0f;
-                dl1 = sv1 * rtv1 - 1.0f;
-                lossv = (tl0 - sl0 + (sv0 + d0 * d0) * (0.5f * rtv0) - 0.5f) +
-                        (tl1 - sl1 + (sv1 + d1 * d1) * (0.5f * rtv1) - 0.5f);
-            }
-            if (!tvalid) { dm0 = dm1 = dl0 = dl1 = 0.0f; }
-            if (g == 0 && tvalid) {
-                met_l += lossv;
-                met_m += d0 * d0 + d1 * d1;
-                gb3a += dm0; gb3b += dm1; gls0 += dl0; gls1 += dl1;
-            }
-            // ------------------------------------------------------------ backward
-            // stage H1^T, H2^T (env-major rows) and the env's dmean (pad columns 64, 65)
-            float* SA = S + S_A;
-            float* SB = S + S_B;
+        // ------------------------------------------------------------ this wave's share
 #pragma unroll
-            for (int fb = 0; fb < 4; ++fb) {
-                st4(SA + j * SAS + 16 * fb + 4 * g, H1[fb]);
-                st4(SB + j * SAS + 16 * fb + 4 * g, H2[fb]);
-            }
-            if (g == 0) { SB[j * SAS + 64] = dm0; SB[j * SAS + 65] = dm1; }
-            wave_sync();
-            // dW3 partials: lane (j, g) sums H2[16 nb + j][e] dm[e] over the tile's envs e = 4s+g
+        for (int x = 0; x < 4; ++x)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const float* row = SB + (4 * s + g) * SAS;
-                const float e0 = row[64], e1 = row[65];
+            for (int r = 0; r < 4; ++r)   // sum over the env axis (the 16 lanes of a row)
 #pragma unroll
-                for (int nb = 0; nb < 4; ++nb) {
-                    const float h = row[16 * nb + j];
-                    gw3a[nb] = fmaf(h, e0, gw3a[nb]);
-                    gw3b[nb] = fmaf(h, e1, gw3b[nb]);
+                for (int o = 8; o >= 1; o >>= 1) {
+                    gw3a[x][r] += __shfl_xor(gw3a[x][r], o, 16);
+                    gw3b[x][r] += __shfl_xor(gw3b[x][r], o, 16);
                 }
-            }
-            // dZ2 = (W3 . dmean) * (1 - H2^2)   (accumulator layout)
-            f32x4 dZ[4];
-#pragma unroll
-            for (int fb = 0; fb < 4; ++fb) {
-                const f32x4 wa = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2);
-                const f32x4 wb = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2 + 4);
-                const float w0[4] = {wa[0], wa[2], wb[0], wb[2]}, w1[4] = {wa[1], wa[3], wb[1], wb[3]};
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float h = H2[fb][r];
-                    dZ[fb][r] = fmaf(w0[r], dm0, w1[r] * dm1) * fmaf(-h, h, 1.0f);
-                }
-            }
-            wave_sync();   // every lane's H2^T reads are done
-#pragma unroll
-            for (int fb = 0; fb < 4; ++fb) st4(SB + j * SAS + 16 * fb + 4 * g, dZ[fb]);
-            wave_sync();
-            // dW2 += H1^T dZ2 over the tile's 16 envs (K = env, 4 per k-step)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                float x[4], y[4];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    x[b] = SA[(4 * s + g) * SAS + 16 * b + j];
-                    y[b] = SB[(4 * s + g) * SAS + 16 * b + j];
-                    gb2[b] += y[b];   // db2 partial: dZ2[16 b + j][e], e = 4s+g
-                }
-#pragma unroll
-                for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                    for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[mb], y[nb], gW2[mb][nb]);
-            }
-            // dH1 = W2 . dZ2  (A = W2^T image, B = dZ2 in accumulator layout)
-            f32x4 acc[4];
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-            f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
+        gb3a = wave_sum(gb3a); gb3b = wave_sum(gb3b);
+        gls0 = wave_sum(gls0); gls1 = wave_sum(gls1);
+        met_l = wave_sum(met_l); met_m = wave_sum(met_m);
+        STAMP(6);
+        __syncthreads();   // (one of the two barriers every wave meets) weights/scratch are free
+        STAMP(9);
+        float* R = lds + pair * P_PAD;   // pair p fills region p; its two waves write disjoint entries
+        if (j == 0) {
 #pragma unroll
             for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const f32x4 w = wn;
-                    if (fb * 4 + r < 15) {
-                        const int kn = (r == 3) ? 16 * (fb + 1) + 4 * g : 16 * fb + 4 * g + r + 1;
-                        wn = ld4(LS + N_W2T + kn * HID + 4 * j);
+                    const int f = 16 * fb + 4 * g + r;
+                    R[P_W3 + 2 * f] = gw3a[fb][r];
+                    R[P_W3 + 2 * f + 1] = gw3b[fb][r];
+                }
+        }
+        if (lane == 0) {
+            R[P_B3] = gb3a; R[P_B3 + 1] = gb3b; R[P_LS] = gls0; R[P_LS + 1] = gls1;
+            R[P_TOT + 1] = met_l; R[P_TOT + 2] = met_m;
+        }
+    } else {
+        // ============================================================ consumer wave
+        // partial sums: dW2, dW1 (+db1 in row 11), db2 (envs 4s+g of feature 16x+j), rewards
+        f32x4 gW2[4][4], gW1[4];
+        float gb2[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+#pragma unroll
+            for (int y = 0; y < 4; ++y) gW2[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+            gW1[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+            gb2[x] = 0.0f;
+        }
+        float met_r = 0, met_n = 0;
+        // student filter of input j for the dW1 A operand (lane-constant)
+        const float smu = j < 12 ? LS[N_MU + j] : 0.0f, srs = j < 12 ? LS[N_RS + j] : 0.0f;
+        uint32_t tiles = 0;
+        uint32_t k = 0;
+        bool ok = true;
+        for (int64_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
+            const int64_t base = grp * GROUP;
+            const int64_t i = base + lane;
+            const float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
+            const float* act = PS + P_ACT + (k & 1) * GROUP * 2;
+            const int ntile = (int)min((int64_t)(GROUP / TILE), (a.n - base + TILE - 1) / TILE);
+            for (int t = 0; t < ntile; ++t) {
+                STAMP(2);
+                if (!(ok = wait_ge(flags, tiles + 1, err))) break;
+                STAMP(3);
+                // read the whole slot, then free it for the producer's next tile
+                const float* h1t = PS + P_H1T;
+                const float* dzt = PS + P_DZT;
+                float x[4][4], y[4][4];
+                f32x4 H1[4], dZ[4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
+                        y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
                     }
 #pragma unroll
-                    for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
+                for (int b = 0; b < 4; ++b) {
+                    H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
+                    dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
                 }
+                publish(flags + 1, ++tiles);
+                // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
 #pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
+                for (int s = 0; s < 4; ++s) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[mb][r] *= fmaf(-H1[mb][r], H1[mb][r], 1.0f);
-            wave_sync();   // every lane's dW2 reads of SA are done
+                    for (int b = 0; b < 4; ++b) gb2[b] += y[s][b];
 #pragma unroll
-            for (int mb = 0; mb < 4; ++mb) st4(SA + j * SAS + 16 * mb + 4 * g, acc[mb]);
-            wave_sync();
-            // dW1 (+ db1 as input row 11) += z^T dZ1; A = student-filtered inputs of env 4s+g
+                    for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const float x = obt[(4 * s + g) * SOS + (j < 12 ? j : 0)];
-                const float z = j < 12 ? fminf(fmaxf((x - smu) * srs, -5.0f), 5.0f) : 0.0f;
+                        for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[s][mb], y[s][nb], gW2[mb][nb]);
+                }
+                // dH1 = W2 . dZ2 (A = W2^T image), dZ1 = dH1 * (1 - H1^2)
+                f32x4 acc[4];
 #pragma unroll
-                for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, SA[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
+                for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
+#pragma unroll
+                for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const f32x4 w = wn;
+                        if (fb * 4 + r < 15) {
+                            const int kn = (r == 3) ? 16 * (fb + 1) + 4 * g : 16 * fb + 4 * g + r + 1;
+                            wn = ld4(LS + N_W2T + kn * HID + 4 * j);
+                        }
+#pragma unroll
+                        for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
+                    }
+                float* sa = PS + P_SA;
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[mb][r] *= fmaf(-H1[mb][r], H1[mb][r], 1.0f);
+                    st4(sa + j * SAS + 16 * mb + 4 * g, acc[mb]);
+                }
+                wave_sync();
+                // dW1 (+ db1 as input row 11) += z^T dZ1; A = student-filtered inputs of env 4s+g
+                const float* obt = obs + TILE * t * SOS;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const float xv = obt[(4 * s + g) * SOS + (j < 12 ? j : 0)];
+                    const float z = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, sa[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
+                }
+                wave_sync();   // sa is rewritten by the next tile
             }
-            wave_sync();   // SA/SB are rewritten by the next tile
+            if (!ok) break;
+            // ---------------------------------------------------------- env.step (one env per lane)
+            STAMP(4);
+            const uint32_t iu = (uint32_t)i;
+            const bool valid = i < a.n;
+            rd::State st{};
+            if (valid) load_state(a.state, a.n, iu, st);
+            const float act0 = act[lane * 2], act1 = act[lane * 2 + 1];
+            const float rew = rd::env_step(st, act0, act1);
+            // episode clock of this env (RDD_STAGGER_GROUP envs share an offset)
+            const int64_t gid = a.env_base + i;
+            const uint32_t u = C + (a.stagger ? (uint32_t)((gid / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);
+            const bool done_step = (u % rd::kEpisodeSteps) == rd::kEpisodeSteps - 1;
+            if (done_step) {
+                float dr[6];
+                rd::philox_draw(a.seed, (uint64_t)gid, u / rd::kEpisodeSteps + 1, dr);
+                rd::env_reset(st, dr);
+            }
+            if (valid) {
+                float* s = a.state;
+                const int64_t n = a.n;
+                (s + 0 * n)[iu] = st.q0; (s + 1 * n)[iu] = st.q1; (s + 2 * n)[iu] = st.v0; (s + 3 * n)[iu] = st.v1;
+                if (done_step) { (s + 4 * n)[iu] = st.tx; (s + 5 * n)[iu] = st.ty; }
+                (s + 6 * n)[iu] = st.dx; (s + 7 * n)[iu] = st.dy;
+                met_r += rew;
+                met_n += 1.0f;
+            }
+            publish(flags + 2, k + 1);   // obs/action buffers of group k may be reused
+            STAMP(5);
         }
-        STAMP(4);
-        // ------------------------------------------------------------ env.step (one env per lane)
-        if (valid) load_state(a.state, a.n, iu, st);   // re-read (L2-resident): no live range across the tiles
-        const float rew = rd::env_step(st, act0, act1);
-        // episode clock of this env (RDD_STAGGER_GROUP envs share an offset)
-        const int64_t gid = a.env_base + i;
-        const uint32_t u = C + (a.stagger ? (uint32_t)((gid / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);
-        const bool done_step = (u % rd::kEpisodeSteps) == rd::kEpisodeSteps - 1;
-        if (done_step) {
-            float dr[6];
-            rd::philox_draw(a.seed, (uint64_t)gid, u / rd::kEpisodeSteps + 1, dr);
-            rd::env_reset(st, dr);
-        }
-        if (valid) {
-            float* s = a.state;
-            const int64_t n = a.n;
-            (s + 0 * n)[iu] = st.q0; (s + 1 * n)[iu] = st.q1; (s + 2 * n)[iu] = st.v0; (s + 3 * n)[iu] = st.v1;
-            if (done_step) { (s + 4 * n)[iu] = st.tx; (s + 5 * n)[iu] = st.ty; }
-            (s + 6 * n)[iu] = st.dx; (s + 7 * n)[iu] = st.dy;
-            met_r += rew;
-            met_n += 1.0f;
-        }
-        STAMP(5);
-    }
-
-    STAMP(6);
-    // ---------------------------------------------------------------- workgroup reduction
-    // per-lane partials over the env axis (k-groups g) -> one value per feature
+        // ------------------------------------------------------------ this wave's share
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-        gb2[nb] = xsum32(xsum16(gb2[nb]));
-        gw3a[nb] = xsum32(xsum16(gw3a[nb]));
-        gw3b[nb] = xsum32(xsum16(gw3b[nb]));
-    }
-    gb3a = wave_sum(gb3a); gb3b = wave_sum(gb3b);
-    gls0 = wave_sum(gls0); gls1 = wave_sum(gls1);
-    met_r = wave_sum(met_r); met_l = wave_sum(met_l); met_m = wave_sum(met_m); met_n = wave_sum(met_n);
-    __syncthreads();   // every wave is done with its scratch
-    STAMP(9);
-    // waves 0-3 store into region w, then waves 4-7 add into region w-4 (fixed order)
-    float* R = lds + NET + NET_S + (wave & 3) * P_PAD;
+        for (int x = 0; x < 4; ++x) gb2[x] = xsum32(xsum16(gb2[x]));   // over the k-groups g
+        met_r = wave_sum(met_r); met_n = wave_sum(met_n);
+        STAMP(6);
+        __syncthreads();   // (one of the two barriers every wave meets) weights/scratch are free
+        STAMP(9);
+        float* R = lds + pair * P_PAD;
 #pragma unroll
-    for (int phase = 0; phase < 2; ++phase) {
-        if ((wave >> 2) == phase) {
-            auto put = [&](int p, float v) { R[p] = phase ? R[p] + v : v; };
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        put(P_W2 + (16 * mb + 4 * g + r) * HID + 16 * nb + j, gW2[mb][nb][r]);
+        for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int k = 4 * g + r;
-                    if (k < OBD) put(P_W1 + k * HID + 16 * nb + j, gW1[nb][r]);
-                    else if (k == OBD) put(P_B1 + 16 * nb + j, gW1[nb][r]);
-                }
-            if (g == 0) {
+                for (int r = 0; r < 4; ++r) R[P_W2 + (16 * mb + 4 * g + r) * HID + 16 * nb + j] = gW2[mb][nb][r];
 #pragma unroll
-                for (int nb = 0; nb < 4; ++nb) {
-                    const int f = 16 * nb + j;
-                    put(P_B2 + f, gb2[nb]);
-                    put(P_W3 + 2 * f, gw3a[nb]);
-                    put(P_W3 + 2 * f + 1, gw3b[nb]);
-                }
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int kk = 4 * g + r;
+                if (kk < OBD) R[P_W1 + kk * HID + 16 * nb + j] = gW1[nb][r];
+                else if (kk == OBD) R[P_B1 + 16 * nb + j] = gW1[nb][r];
             }
-            if (lane == 0) {
-                put(P_B3, gb3a); put(P_B3 + 1, gb3b); put(P_LS, gls0); put(P_LS + 1, gls1);
-                put(P_TOT, met_r); put(P_TOT + 1, met_l); put(P_TOT + 2, met_m); put(P_TOT + 3, met_n);
-            }
+        if (g == 0) {
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) R[P_B2 + 16 * nb + j] = gb2[nb];
         }
-        __syncthreads();
+        if (lane == 0) { R[P_TOT] = met_r; R[P_TOT + 3] = met_n; }
     }
-    const float* R0 = lds + NET + NET_S;
+
+    // Both roles passed exactly one s_barrier above (a wave-level count on gfx950, so the
+    // two call sites pair up); this second one publishes the regions.
+    __syncthreads();
     float* out = a.ws + (int64_t)blockIdx.x * P_PAD;
     for (int p = threadIdx.x; p < P_PAD; p += BLOCK)
-        out[p] = (R0[p] + R0[P_PAD + p]) + (R0[2 * P_PAD + p] + R0[3 * P_PAD + p]);
+        out[p] = (lds[p] + lds[P_PAD + p]) + (lds[2 * P_PAD + p] + lds[3 * P_PAD + p]);
     STAMP(7);
-#ifdef RD_STAMPS
-    if (lane == 0 && a.dbg) a.dbg[(blockIdx.x * WAVES + wave) * 16 + 8] = __builtin_amdgcn_s_memrealtime();
-#endif
 }
 
 // ctl words: [0] completed steps C, [2] beta1^t, [3] beta2^t (f32 bits); [4..7] the
@@ -678,9 +735,9 @@ struct rdd_trainer {
     float* own_grad = nullptr;
     float* ws = nullptr;       // [grid][P_PAD]
     float* hist = nullptr;     // [hist_len][4]
-    uint32_t* ctl = nullptr;   // [8]: step words + snapshot
+    uint32_t* ctl = nullptr;   // [16]: step words, snapshot, [8] hand-off timeout flag
     unsigned long long* dbg = nullptr;   // RD_STAMPS builds only
-    int prio_mode = 0;
+
 };
 
 namespace {
@@ -699,7 +756,6 @@ int launch_rollout(rdd_trainer* t) {
     a.act_student = t->cfg.act_with == RDD_ACT_STUDENT;
     a.stagger = t->cfg.stagger;
     a.dbg = t->dbg;
-    a.prio_mode = t->prio_mode;
     a.inv_n_global = 1.0f / (float)t->cfg.n_envs_global;
     hipLaunchKernelGGL(rollout_kernel, dim3(t->grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
@@ -753,7 +809,6 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     rdd_trainer* t = new (std::nothrow) rdd_trainer();
     if (!t) return rd::set_error(RD_EINVAL, "rdd_create: out of host memory");
     t->cfg = *cfg;
-    if (const char* pm = getenv("RDD_PRIO_MODE")) t->prio_mode = atoi(pm);
     if (t->cfg.metrics_len == 0) t->cfg.metrics_len = 4096;
     t->device = device;
     t->stream = (hipStream_t)hip_stream;
@@ -776,7 +831,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     t->grad = t->own_grad;
     alloc((void**)&t->ws, sizeof(float) * (size_t)t->grid * P_PAD);
     alloc((void**)&t->hist, sizeof(float) * (size_t)t->cfg.metrics_len * N_MET);
-    alloc((void**)&t->ctl, sizeof(uint32_t) * 8);
+    alloc((void**)&t->ctl, sizeof(uint32_t) * 16);
 #ifdef RD_STAMPS
     alloc((void**)&t->dbg, sizeof(unsigned long long) * (size_t)t->grid * WAVES * 16);
 #endif
