@@ -111,10 +111,12 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float tanh_f(float x) {
-    // 1 - 2/(exp(2x)+1): one v_exp_f32 + one v_rcp_f32; saturates correctly at +-inf
-    const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
-    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+// Forward weight images are pre-scaled by 2 log2(e), so a layer's accumulator is already
+// y = 2 log2(e) z and tanh(z) = 1 - 2/(2^y + 1): v_exp_f32 + v_add + v_rcp_f32 + v_fma.
+// (The backward only needs tanh's output; W2^T for dH1 keeps the unscaled weights.)
+constexpr float kTanhScale = 2.8853900817779268f;
+__device__ __forceinline__ float tanh_pre(float y) {
+    return fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(y) + 1.0f), 1.0f);
 }
 
 // The per-wave scratch is private to its wave: LDS instructions of one wave execute in
@@ -166,24 +168,25 @@ __device__ __forceinline__ void load_state(const float* s, int64_t n, uint32_t i
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
-// global net = params[P] | mu[11] | sd[11]  ->  LDS image (+ W2^T if `transposed`)
+// global net = params[P] | mu[11] | sd[11]  ->  LDS image (+ W2^T if `transposed`); the
+// forward images of W1, b1, W2, b2 carry the tanh scale (kTanhScale)
 __device__ void load_net(float* L, const float* g, bool transposed, int nthreads) {
     const float* mu = g + P_TOT;
     const float* sd = g + P_TOT + OBD;
     for (int i = threadIdx.x; i < 12 * HID; i += nthreads) {
         const int k = i >> 6, f = i & 63;
-        L[N_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = k < OBD ? g[P_W1 + i] : g[P_B1 + f];
+        L[N_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * (k < OBD ? g[P_W1 + i] : g[P_B1 + f]);
     }
     for (int i = threadIdx.x; i < HID * HID; i += nthreads) {
         const int k = i >> 6, f = i & 63;
-        L[N_W2 + k * HID + (f & 15) * 4 + (f >> 4)] = g[P_W2 + i];
+        L[N_W2 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * g[P_W2 + i];
     }
     if (transposed)   // k fastest across lanes: the LDS writes spread over the banks
         for (int i = threadIdx.x; i < HID * HID; i += nthreads) {
             const int f = i >> 6, k = i & 63;
             L[N_W2T + f * HID + (k & 15) * 4 + (k >> 4)] = g[P_W2 + k * HID + f];
         }
-    for (int i = threadIdx.x; i < HID; i += nthreads) L[N_B2 + i] = g[P_B2 + i];
+    for (int i = threadIdx.x; i < HID; i += nthreads) L[N_B2 + i] = kTanhScale * g[P_B2 + i];
     for (int i = threadIdx.x; i < HID * ACD; i += nthreads) L[N_W3 + i] = g[P_W3 + i];
     if (threadIdx.x < ACD) {
         L[N_B3 + threadIdx.x] = g[P_B3 + threadIdx.x];
@@ -217,7 +220,7 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) H1[fb][r] = tanh_f(acc[fb][r]);
+        for (int r = 0; r < 4; ++r) H1[fb][r] = tanh_pre(acc[fb][r]);
     // layer 2: K = 64; k-step (kb, r) uses features 16 kb + 4 g + r = this lane's H1[kb][r]
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + N_B2 + 16 * fb + 4 * g);
@@ -241,7 +244,7 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
         const f32x4 wa = ld4(L + N_W3 + (16 * fb + 4 * g) * 2);       // W3[f][0..1], f = 16fb+4g+0,1
         const f32x4 wb = ld4(L + N_W3 + (16 * fb + 4 * g) * 2 + 4);   // f = 16fb+4g+2,3
 #pragma unroll
-        for (int r = 0; r < 4; ++r) H2[fb][r] = tanh_f(acc[fb][r]);
+        for (int r = 0; r < 4; ++r) H2[fb][r] = tanh_pre(acc[fb][r]);
         p0 = fmaf(H2[fb][0], wa[0], p0); p1 = fmaf(H2[fb][0], wa[1], p1);
         p0 = fmaf(H2[fb][1], wa[2], p0); p1 = fmaf(H2[fb][1], wa[3], p1);
         p0 = fmaf(H2[fb][2], wb[0], p0); p1 = fmaf(H2[fb][2], wb[1], p1);
@@ -251,6 +254,86 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
     p1 = xsum32(xsum16(p1));
     m0 = p0 + L[N_B3];
     m1 = p1 + L[N_B3 + 1];
+}
+
+// Teacher and student forwards of one tile, interleaved layer by layer: 8 independent
+// accumulator chains per layer, and one net's tanh can issue behind the other's MFMAs.
+// Returns the student's hidden activations (needed by the backward) and both means.
+__device__ __forceinline__ void mlp_forward_pair(const float* LT, const float* LS, const float* ob, int j, int g,
+                                                 f32x4 (&H1)[4], f32x4 (&H2)[4], float& mt0, float& mt1,
+                                                 float& ms0, float& ms1) {
+    f32x4 at[4], as[4];
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) at[fb] = as[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        const int k = 4 * s + g;
+        const float x = ob[j * SOS + k];
+        const float zt = fminf(fmaxf((x - LT[N_MU + k]) * LT[N_RS + k], -5.0f), 5.0f);
+        const float zs = fminf(fmaxf((x - LS[N_MU + k]) * LS[N_RS + k], -5.0f), 5.0f);
+        const f32x4 wt = ld4(LT + N_W1 + k * HID + 4 * j);
+        const f32x4 ws = ld4(LS + N_W1 + k * HID + 4 * j);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            at[fb] = mfma(wt[fb], zt, at[fb]);
+            as[fb] = mfma(ws[fb], zs, as[fb]);
+        }
+    }
+    f32x4 T1[4];
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            T1[fb][r] = tanh_pre(at[fb][r]);
+            H1[fb][r] = tanh_pre(as[fb][r]);
+        }
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) {
+        at[fb] = ld4(LT + N_B2 + 16 * fb + 4 * g);
+        as[fb] = ld4(LS + N_B2 + 16 * fb + 4 * g);
+    }
+    f32x4 wtn = ld4(LT + N_W2 + (4 * g) * HID + 4 * j);
+    f32x4 wsn = ld4(LS + N_W2 + (4 * g) * HID + 4 * j);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const f32x4 wt = wtn, ws = wsn;
+            if (kb * 4 + r < 15) {
+                const int kn = (r == 3) ? 16 * (kb + 1) + 4 * g : 16 * kb + 4 * g + r + 1;
+                wtn = ld4(LT + N_W2 + kn * HID + 4 * j);
+                wsn = ld4(LS + N_W2 + kn * HID + 4 * j);
+            }
+#pragma unroll
+            for (int fb = 0; fb < 4; ++fb) {
+                at[fb] = mfma(wt[fb], T1[kb][r], at[fb]);
+                as[fb] = mfma(ws[fb], H1[kb][r], as[fb]);
+            }
+        }
+    float pt0 = 0.0f, pt1 = 0.0f, ps0 = 0.0f, ps1 = 0.0f;
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) {
+        const f32x4 ta = ld4(LT + N_W3 + (16 * fb + 4 * g) * 2), tb = ld4(LT + N_W3 + (16 * fb + 4 * g) * 2 + 4);
+        const f32x4 sa = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2), sb = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2 + 4);
+        f32x4 t2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            t2[r] = tanh_pre(at[fb][r]);
+            H2[fb][r] = tanh_pre(as[fb][r]);
+        }
+        pt0 = fmaf(t2[0], ta[0], pt0); pt1 = fmaf(t2[0], ta[1], pt1);
+        pt0 = fmaf(t2[1], ta[2], pt0); pt1 = fmaf(t2[1], ta[3], pt1);
+        pt0 = fmaf(t2[2], tb[0], pt0); pt1 = fmaf(t2[2], tb[1], pt1);
+        pt0 = fmaf(t2[3], tb[2], pt0); pt1 = fmaf(t2[3], tb[3], pt1);
+        ps0 = fmaf(H2[fb][0], sa[0], ps0); ps1 = fmaf(H2[fb][0], sa[1], ps1);
+        ps0 = fmaf(H2[fb][1], sa[2], ps0); ps1 = fmaf(H2[fb][1], sa[3], ps1);
+        ps0 = fmaf(H2[fb][2], sb[0], ps0); ps1 = fmaf(H2[fb][2], sb[1], ps1);
+        ps0 = fmaf(H2[fb][3], sb[2], ps0); ps1 = fmaf(H2[fb][3], sb[3], ps1);
+    }
+    mt0 = xsum32(xsum16(pt0)) + LT[N_B3];
+    mt1 = xsum32(xsum16(pt1)) + LT[N_B3 + 1];
+    ms0 = xsum32(xsum16(ps0)) + LS[N_B3];
+    ms1 = xsum32(xsum16(ps1)) + LS[N_B3 + 1];
 }
 
 // Hand-off counters live in LDS; each is written by one wave only.  Acquire/release at
@@ -337,8 +420,9 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 const float* obt = obs + TILE * t * SOS;
                 f32x4 H1[4], H2[4];
                 float mt0, mt1, ms0, ms1;
-                mlp_forward(LT, obt, j, g, H1, H2, mt0, mt1);
-                mlp_forward(LS, obt, j, g, H1, H2, ms0, ms1);
+                STAMP(10);
+                mlp_forward_pair(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                STAMP(12);
                 // loss
                 const float d0 = ms0 - mt0, d1 = ms1 - mt1;
                 float dm0, dm1, dl0 = 0.0f, dl1 = 0.0f, lossv;
@@ -468,6 +552,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
                 }
                 publish(flags + 1, ++tiles);
+                STAMP(13);
                 // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
@@ -495,6 +580,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
 #pragma unroll
                         for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
                     }
+                STAMP(14);
                 float* sa = PS + P_SA;
 #pragma unroll
                 for (int mb = 0; mb < 4; ++mb) {
@@ -513,6 +599,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, sa[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
                 }
                 wave_sync();   // sa is rewritten by the next tile
+                STAMP(15);
             }
             if (!ok) break;
             // ---------------------------------------------------------- env.step (one env per lane)

@@ -46,6 +46,17 @@ def main():
         "epilogue_reduce": float(np.median(d(9, 7))),
         "total": float(np.median(d(0, 7))),
     }
+    prod = (np.flatnonzero(active) % 8) < 4
+    res["producer_teacher_fwd"] = float(np.median(d(10, 11)[prod]))
+    res["producer_student_fwd"] = float(np.median(d(11, 12)[prod]))
+    res["producer_loss_dz2_to_wait"] = float(np.median((d(12, 2))[prod]))
+    res["producer_wait"] = float(np.median(d(2, 3)[prod]))
+    res["producer_slot_write"] = float(np.median((d(3, 10) )[prod]))
+    res["consumer_wait"] = float(np.median(d(2, 3)[~prod]))
+    res["consumer_slot_read"] = float(np.median(d(3, 13)[~prod]))
+    res["consumer_dw2_dh1"] = float(np.median(d(13, 14)[~prod]))
+    res["consumer_dz1_dw1"] = float(np.median(d(14, 15)[~prod]))
+    res["consumer_physics"] = float(np.median(d(4, 5)[~prod]))
     # per wave slot (0-3 dispatched first; w and w+4 share a SIMD): time to finish the groups
     widx = np.flatnonzero(active) % 8
     res["finish_by_wave_slot"] = [float(np.median(d(0, 6)[widx == w])) for w in range(8)]
