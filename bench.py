@@ -43,9 +43,13 @@ WORKLOADS = {
                desc="BASELINE config 3: 65,536 envs/GPU, Gaussian KL(s||t) distillation, fp32"),
     "c4": dict(envs=262144, loss="mse", act_with="teacher",
                desc="BASELINE config 4: 262,144 envs per GPU, RCCL student-grad all-reduce, MSE, fp32"),
-    "c5": dict(envs=131072, loss="mse", act_with="student",
-               desc="BASELINE config 5 shard: DAgger (student acts, teacher relabels), 131,072 envs/GPU, MSE"),
+    "c5": dict(envs=131072, loss="mse", act_with="student", student_dtype="bf16",
+               desc="BASELINE config 5 shard: DAgger (student acts, teacher relabels), 1,048,576 envs over 8 GPUs "
+                    "= 131,072 envs/GPU, bf16 student MLP (f32 master + Adam), f32 teacher, MSE"),
 }
+# FLOPs per env-step by MFMA precision: teacher forward f32; student fwd + bwd f32 or bf16
+FLOP_TEACHER = 2 * (11 * 64 + 64 * 64 + 64 * 2)
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -104,15 +108,24 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # RD_BENCH_ONE_DEVICE=1 + RD_DIST_BACKEND=gloo rehearse the N > 1 path with every rank
+    # on cuda:0 (a 1-GPU box); the driver's multi-GPU runs use one GPU per rank over RCCL.
+    if os.environ.get("RD_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("RD_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
     wl = WORKLOADS[args.workload]
     n = args.envs_per_gpu or wl["envs"]
-    cfg = DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr)
+    sdt = wl.get("student_dtype", "f32")
+    cfg = DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr, student_dtype=sdt)
     tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world)
 
     def one_step(ev=None):
@@ -162,6 +175,10 @@ def main():
         value = n * world * args.steps / elapsed
         launch_s = kern_ms * 1e-3
         achieved = FLOP_PER_ENV_STEP * n / launch_s / 1e12
+        peak = PEAK_F32_TFLOPS
+        if sdt == "bf16":   # mixed: the MFMA-time-weighted peak of f32 teacher + bf16 student FLOPs
+            f_s = FLOP_PER_ENV_STEP - FLOP_TEACHER
+            peak = FLOP_PER_ENV_STEP / (FLOP_TEACHER / PEAK_F32_TFLOPS + f_s / PEAK_BF16_TFLOPS)
         traffic = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}.json")
         if os.path.exists(pmc):
@@ -170,17 +187,17 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32",
+            "vs_baseline": None, "dtype": "f32" if sdt == "f32" else "bf16 student (f32 accumulate) + f32 teacher",
             "data": "synthetic: Philox(seed 0) Reacher-v2 resets, seeded synthetic teacher (normc, fixture logstd) "
                     "and student (2x64 MlpPolicy)",
             "config": {"workload": args.workload, "description": wl["desc"], "envs_per_gpu": n,
-                       "envs_total": n * world, "student": "MlpPolicy 2x64 tanh (5060 params)",
+                       "envs_total": n * world, "student": f"MlpPolicy 2x64 tanh (5060 params, {sdt})",
                        "teacher": "MlpPolicy 2x64 tanh", "loss": wl["loss"], "act_with": wl["act_with"],
                        "optimizer": f"TF1 Adam lr {args.lr}, 1 step per env-step",
                        "parallelism": f"dp{world}"},
             "student_mse": mse,
             "roofline": {"kernel": "rollout_kernel", "bound": "mfma", "achieved": achieved,
-                         "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS,
+                         "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": traffic, "flop_per_env_step": FLOP_PER_ENV_STEP,
                          "launch_us": kern_ms * 1e3,
                          "hbm_gbs_algorithmic": BYTES_PER_ENV_STEP * n / launch_s / 1e9},

@@ -50,7 +50,18 @@ typedef struct {
     int32_t stagger;         /* 0: lockstep TimeLimit (all envs share the episode phase);
                                 1: env g runs at phase C + (g / RDD_STAGGER_GROUP) % 50, so a
                                    batch mixes all 50 episode phases (see below)          */
+    int32_t student_dtype;   /* RDD_DTYPE_F32, or RDD_DTYPE_BF16 (BASELINE config 5: bf16
+                                student MLP; see below)                                  */
 } rdd_config;
+
+/* Student precision.  RDD_DTYPE_F32: every product exact f32 (v_mfma_f32_16x16x4_f32).
+ * RDD_DTYPE_BF16 (mixed precision, f32 master weights + f32 Adam): the student's weight
+ * matrices W1, W2, W3 are used as bf16 roundings of the master, and the MFMA operands
+ * built from activations / back-propagated errors (z, h1, dZ2, dZ1) are rounded to bf16;
+ * biases, log-std, tanh, the loss and every accumulation stay f32.  The teacher is f32
+ * either way.  oracle/policy_np.py forward_bf16/backward_bf16 define the arithmetic. */
+#define RDD_DTYPE_F32 0
+#define RDD_DTYPE_BF16 1
 
 /* Staggered episodes.  The reference steps ONE env and trains on random windows drawn
  * from past episodes (dataset.py:179-194), so a training batch mixes episode phases.  N

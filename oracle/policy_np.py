@@ -53,6 +53,46 @@ def forward(p, obmu, obsd, ob):
     return dict(z=z, h1=h1, h2=h2, mean=mean, logstd=q["ls"])
 
 
+def bf16(x):
+    """Round to the nearest bf16 (ties to even), returned as float64 values.  The kernel's
+    v_cvt_pk_bf16_f32 rounds this way (include/reacher_distill.h RDD_DTYPE_BF16)."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def forward_bf16(p, obmu, obsd, ob):
+    """The bf16-student forward (RDD_DTYPE_BF16): weight matrices and the MFMA operands z, h1
+    rounded to bf16; biases, tanh, layer-3 inputs (h2) and accumulations in f32 (f64 here).
+    z is formed in f32 exactly as the kernel does ((ob - mu) * (1/sd), clipped)."""
+    q = unpack(p)
+    ob32 = np.asarray(ob, np.float32)
+    rs = (np.float32(1) / np.asarray(obsd, np.float32)).astype(np.float32)
+    z = np.clip((ob32 - np.asarray(obmu, np.float32)) * rs, np.float32(-5), np.float32(5)).astype(np.float32)
+    zb = bf16(z)
+    h1 = np.tanh(zb @ bf16(q["W1"]) + q["b1"])
+    h2 = np.tanh(bf16(h1) @ bf16(q["W2"]) + q["b2"])
+    mean = h2 @ bf16(q["W3"]) + q["b3"]
+    return dict(z=z.astype(np.float64), zb=zb, h1=h1, h2=h2, mean=mean, logstd=q["ls"])
+
+
+def backward_bf16(p, fs, dmean, dls):
+    """Gradients of the bf16 student as the kernel forms them: dZ2 = (W3b dmean)(1 - h2^2);
+    dW2 = bf16(h1)^T bf16(dZ2); db2 = sum dZ2; dH1 = bf16(W2) bf16(dZ2); dZ1 = dH1 (1 - h1^2);
+    dW1 = bf16(z)^T bf16(dZ1); db1 = sum bf16(dZ1) (the bias row of the same product)."""
+    q = unpack(p)
+    g = dict(W3=fs["h2"].T @ dmean, b3=dmean.sum(0), ls=np.asarray(dls, np.float64))
+    dz2 = (dmean @ bf16(q["W3"]).T) * (1 - fs["h2"] ** 2)
+    dz2b = bf16(dz2)
+    g["W2"] = bf16(fs["h1"]).T @ dz2b
+    g["b2"] = dz2.sum(0)
+    dz1 = (dz2b @ bf16(q["W2"]).T) * (1 - fs["h1"] ** 2)
+    dz1b = bf16(dz1)
+    g["W1"] = fs["zb"].T @ dz1b
+    g["b1"] = dz1b.sum(0)
+    return pack(g["W1"], g["b1"], g["W2"], g["b2"], g["W3"], g["b3"], g["ls"])
+
+
 def loss_and_dmean(fs, ft, loss, n_global):
     """Returns (loss, dL/dmean_s [N,2], dL/dlogstd_s [2], sum sq action error)."""
     diff = fs["mean"] - ft["mean"]

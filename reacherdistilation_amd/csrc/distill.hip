@@ -336,6 +336,131 @@ __device__ __forceinline__ void mlp_forward_pair(const float* LT, const float* L
     ms1 = xsum32(xsum16(ps1)) + LS[N_B3 + 1];
 }
 
+// ---------------------------------------------------------------- bf16 student (RDD_DTYPE_BF16)
+// v_mfma_f32_16x16x32_bf16 (lane l: A[row l&15][k 8(l>>4)+jj], B[k 8(l>>4)+jj][col l&15],
+// jj = 0..7) for the layers and dH1, v_mfma_f32_16x16x16_bf16 (k = 4(l>>4)+jj, jj = 0..3)
+// where K is the tile's 16 envs (dW2, dW1).  C/D layout as the f32 forms.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma_k32(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_k16(s16x4 a, s16x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ unsigned short bf16_bits(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
+__device__ __forceinline__ float bf16_round(float x) { return (float)(__bf16)x; }
+__device__ __forceinline__ s16x4 pack4(float a, float b, float c, float d) {
+    return s16x4{(short)bf16_bits(a), (short)bf16_bits(b), (short)bf16_bits(c), (short)bf16_bits(d)};
+}
+__device__ __forceinline__ bf16x8 pack8(f32x4 lo, f32x4 hi) {
+    return bf16x8{(__bf16)lo[0], (__bf16)lo[1], (__bf16)lo[2], (__bf16)lo[3],
+                  (__bf16)hi[0], (__bf16)hi[1], (__bf16)hi[2], (__bf16)hi[3]};
+}
+__device__ __forceinline__ bf16x8 ldbf8(const float* base, int half) {
+    return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const unsigned short*>(base) + half);
+}
+
+// Student image in the bf16 mode (offsets in floats; bf16 arrays hold 2 per float):
+//   W1 A operands [g 4][fb 4][i 16][jj 8] = W1[8g+jj][16fb+i] (0 beyond input 10)
+//   W2 forward    [s 2][g 4][fb 4][i 16][jj 8] = W2[kp(s,g,jj)][16fb+i]
+//   W2 for dH1    [s 2][g 4][mb 4][i 16][jj 8] = W2[16mb+i][kp(s,g,jj)]
+//   kp(s,g,jj) = 32s + 4g + (jj&3) + 16(jj>>2): the k order in which a layer's accumulator
+//   (lane g holds features 16fb+4g+r) feeds the next 16x16x32 step with no lane movement.
+//   f32: b1, b2, W3 (bf16-rounded values), b3, logstd, filter mean, 1/std.
+constexpr int NB_W1 = 0;
+constexpr int NB_W2F = NB_W1 + 4 * 4 * 16 * 8 / 2;
+constexpr int NB_W2B = NB_W2F + 2 * 4 * 4 * 16 * 8 / 2;
+constexpr int NB_B1 = NB_W2B + 2 * 4 * 4 * 16 * 8 / 2;
+constexpr int NB_B2 = NB_B1 + HID;
+constexpr int NB_W3 = NB_B2 + HID;
+constexpr int NB_B3 = NB_W3 + HID * ACD;
+constexpr int NB_LS = NB_B3 + ACD;
+constexpr int NB_MU = NB_LS + ACD;
+constexpr int NB_RS = NB_MU + 12;
+static_assert(NB_RS + 12 <= NET_S && NB_B1 % 4 == 0 && NB_W3 % 4 == 0, "bf16 student image");
+
+__device__ __forceinline__ int kperm(int s, int g, int jj) { return 32 * s + 4 * g + (jj & 3) + 16 * (jj >> 2); }
+
+__device__ void load_net_bf16(float* L, const float* g, int nthreads) {
+    unsigned short* w1 = reinterpret_cast<unsigned short*>(L + NB_W1);
+    unsigned short* w2f = reinterpret_cast<unsigned short*>(L + NB_W2F);
+    unsigned short* w2b = reinterpret_cast<unsigned short*>(L + NB_W2B);
+    for (int x = threadIdx.x; x < 4 * 4 * 16 * 8; x += nthreads) {
+        const int jj = x & 7, i = (x >> 3) & 15, fb = (x >> 7) & 3, gg = x >> 9;
+        const int k = 8 * gg + jj;
+        w1[x] = bf16_bits(k < OBD ? g[P_W1 + k * HID + 16 * fb + i] : 0.0f);
+    }
+    for (int x = threadIdx.x; x < 2 * 4 * 4 * 16 * 8; x += nthreads) {
+        const int jj = x & 7, i = (x >> 3) & 15, b = (x >> 7) & 3, gg = (x >> 9) & 3, s = x >> 11;
+        const int kp = kperm(s, gg, jj);
+        w2f[x] = bf16_bits(g[P_W2 + kp * HID + 16 * b + i]);
+        w2b[x] = bf16_bits(g[P_W2 + (16 * b + i) * HID + kp]);
+    }
+    for (int x = threadIdx.x; x < HID; x += nthreads) {
+        L[NB_B1 + x] = g[P_B1 + x];
+        L[NB_B2 + x] = g[P_B2 + x];
+    }
+    for (int x = threadIdx.x; x < HID * ACD; x += nthreads) L[NB_W3 + x] = bf16_round(g[P_W3 + x]);
+    if (threadIdx.x < ACD) {
+        L[NB_B3 + threadIdx.x] = g[P_B3 + threadIdx.x];
+        L[NB_LS + threadIdx.x] = g[P_LS + threadIdx.x];
+    }
+    if (threadIdx.x < 12) {
+        const int k = threadIdx.x;
+        L[NB_MU + k] = k < OBD ? g[P_TOT + k] : 0.0f;
+        L[NB_RS + k] = k < OBD ? 1.0f / g[P_TOT + OBD + k] : 1.0f;
+    }
+}
+
+// bf16-student forward of a 16-env tile (same outputs/layouts as mlp_forward).
+__device__ __forceinline__ void mlp_forward_bf16(const float* L, const float* ob, int j, int g, f32x4 (&H1)[4],
+                                                 f32x4 (&H2)[4], float& m0, float& m1) {
+    f32x4 acc[4];
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NB_B1 + 16 * fb + 4 * g);
+    // layer 1: one K = 32 step, lane group g supplies inputs 8g .. 8g+7 (zero past input 10)
+    bf16x8 zb;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        const int k = 8 * g + jj;
+        const int kc = k < OBD ? k : 0;
+        const float z = fminf(fmaxf((ob[j * SOS + kc] - L[NB_MU + kc]) * L[NB_RS + kc], -5.0f), 5.0f);
+        zb[jj] = (__bf16)(k < OBD ? z : 0.0f);
+    }
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma_k32(ldbf8(L + NB_W1, ((g * 4 + fb) * 16 + j) * 8), zb, acc[fb]);
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) H1[fb][r] = tanh_pre(kTanhScale * acc[fb][r]);
+    // layer 2: two K = 32 steps over the permuted feature order kperm
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NB_B2 + 16 * fb + 4 * g);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const bf16x8 hb = pack8(H1[2 * s], H1[2 * s + 1]);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb)
+            acc[fb] = mfma_k32(ldbf8(L + NB_W2F, (((s * 4 + g) * 4 + fb) * 16 + j) * 8), hb, acc[fb]);
+    }
+    float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) {
+        const f32x4 wa = ld4(L + NB_W3 + (16 * fb + 4 * g) * 2);
+        const f32x4 wb = ld4(L + NB_W3 + (16 * fb + 4 * g) * 2 + 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) H2[fb][r] = tanh_pre(kTanhScale * acc[fb][r]);
+        p0 = fmaf(H2[fb][0], wa[0], p0); p1 = fmaf(H2[fb][0], wa[1], p1);
+        p0 = fmaf(H2[fb][1], wa[2], p0); p1 = fmaf(H2[fb][1], wa[3], p1);
+        p0 = fmaf(H2[fb][2], wb[0], p0); p1 = fmaf(H2[fb][2], wb[1], p1);
+        p0 = fmaf(H2[fb][3], wb[2], p0); p1 = fmaf(H2[fb][3], wb[3], p1);
+    }
+    m0 = xsum32(xsum16(p0)) + L[NB_B3];
+    m1 = xsum32(xsum16(p1)) + L[NB_B3 + 1];
+}
+
 // Hand-off counters live in LDS; each is written by one wave only.  Acquire/release at
 // workgroup scope order the slot data (LDS) around them.  A spin that exceeds SPIN_LIMIT
 // raises ctl[8] and returns false: the caller leaves its loop, so the launch always ends.
@@ -354,6 +479,7 @@ __device__ __forceinline__ void publish(uint32_t* f, uint32_t v) {
     __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+template <bool BS>   // BS: bf16 student (RDD_DTYPE_BF16)
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
     float* LT = lds;
@@ -368,7 +494,9 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
 
     STAMP(0);
     load_net(LT, a.tnet, false, BLOCK);
-    load_net(LS, a.snet, true, BLOCK);
+    if constexpr (BS) load_net_bf16(LS, a.snet, BLOCK);
+    else load_net(LS, a.snet, true, BLOCK);
+    constexpr int SW3 = BS ? NB_W3 : N_W3, SMU = BS ? NB_MU : N_MU, SRS = BS ? NB_RS : N_RS;
     if (threadIdx.x < PAIRS * 4)
         reinterpret_cast<uint32_t*>(lds + NET + NET_S + (threadIdx.x >> 2) * PSCR + P_FLAGS)[threadIdx.x & 3] = 0u;
 
@@ -421,7 +549,12 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 f32x4 H1[4], H2[4];
                 float mt0, mt1, ms0, ms1;
                 STAMP(10);
-                mlp_forward_pair(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                if constexpr (BS) {
+                    mlp_forward(LT, obt, j, g, H1, H2, mt0, mt1);
+                    mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
+                } else {
+                    mlp_forward_pair(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                }
                 STAMP(12);
                 // loss
                 const float d0 = ms0 - mt0, d1 = ms1 - mt1;
@@ -450,8 +583,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 f32x4 dZ[4];
 #pragma unroll
                 for (int fb = 0; fb < 4; ++fb) {
-                    const f32x4 wa = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2);
-                    const f32x4 wb = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2 + 4);
+                    const f32x4 wa = ld4(LS + SW3 + (16 * fb + 4 * g) * 2);
+                    const f32x4 wb = ld4(LS + SW3 + (16 * fb + 4 * g) * 2 + 4);
                     const float w0[4] = {wa[0], wa[2], wb[0], wb[2]}, w1[4] = {wa[1], wa[3], wb[1], wb[3]};
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -520,7 +653,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         }
         float met_r = 0, met_n = 0;
         // student filter of input j for the dW1 A operand (lane-constant)
-        const float smu = j < 12 ? LS[N_MU + j] : 0.0f, srs = j < 12 ? LS[N_RS + j] : 0.0f;
+        const float smu = j < 12 ? LS[SMU + j] : 0.0f, srs = j < 12 ? LS[SRS + j] : 0.0f;
         uint32_t tiles = 0;
         uint32_t k = 0;
         bool ok = true;
@@ -537,49 +670,86 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 // read the whole slot, then free it for the producer's next tile
                 const float* h1t = PS + P_H1T;
                 const float* dzt = PS + P_DZT;
-                float x[4][4], y[4][4];
-                f32x4 H1[4], dZ[4];
-#pragma unroll
-                for (int s = 0; s < 4; ++s)
+                f32x4 H1[4], dZ[4], acc[4];
+                if constexpr (BS) {
+                    // dW2 operands over the tile's envs 4g..4g+3 (K = 16 envs), rounded to bf16
+                    s16x4 xa[4], yb[4];
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
-                        x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
-                        y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
+                        float xv[4], yv[4];
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {
+                            xv[jj] = h1t[(4 * g + jj) * SAS + 16 * b + j];   // H1[16b + j][env 4g+jj]
+                            yv[jj] = dzt[(4 * g + jj) * SAS + 16 * b + j];   // dZ2[16b + j][env 4g+jj]
+                        }
+                        gb2[b] += (yv[0] + yv[1]) + (yv[2] + yv[3]);         // db2 partial (f32)
+                        xa[b] = pack4(xv[0], xv[1], xv[2], xv[3]);
+                        yb[b] = pack4(yv[0], yv[1], yv[2], yv[3]);
                     }
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
-                    dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
-                }
-                publish(flags + 1, ++tiles);
-                STAMP(13);
-                // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) gb2[b] += y[s][b];
+                    for (int b = 0; b < 4; ++b) {
+                        H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
+                        dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
+                    }
+                    publish(flags + 1, ++tiles);
+                    STAMP(13);
 #pragma unroll
                     for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-                        for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[s][mb], y[s][nb], gW2[mb][nb]);
-                }
-                // dH1 = W2 . dZ2 (A = W2^T image), dZ1 = dH1 * (1 - H1^2)
-                f32x4 acc[4];
+                        for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma_k16(xa[mb], yb[nb], gW2[mb][nb]);
+                    // dH1 = W2 . dZ2: two K = 32 steps, dZ2 in accumulator layout = the B operand
 #pragma unroll
-                for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
+                    for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int fb = 0; fb < 4; ++fb)
+                    for (int s = 0; s < 2; ++s) {
+                        const bf16x8 db = pack8(dZ[2 * s], dZ[2 * s + 1]);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const f32x4 w = wn;
-                        if (fb * 4 + r < 15) {
-                            const int kn = (r == 3) ? 16 * (fb + 1) + 4 * g : 16 * fb + 4 * g + r + 1;
-                            wn = ld4(LS + N_W2T + kn * HID + 4 * j);
+                        for (int mb = 0; mb < 4; ++mb)
+                            acc[mb] = mfma_k32(ldbf8(LS + NB_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8), db, acc[mb]);
+                    }
+                } else {
+                    float x[4][4], y[4][4];
+#pragma unroll
+                    for (int s = 0; s < 4; ++s)
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
+                            y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
                         }
 #pragma unroll
-                        for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
+                    for (int b = 0; b < 4; ++b) {
+                        H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
+                        dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
                     }
+                    publish(flags + 1, ++tiles);
+                    STAMP(13);
+                    // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) gb2[b] += y[s][b];
+#pragma unroll
+                        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                            for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[s][mb], y[s][nb], gW2[mb][nb]);
+                    }
+                    // dH1 = W2 . dZ2 (A = W2^T image)
+#pragma unroll
+                    for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
+#pragma unroll
+                    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const f32x4 w = wn;
+                            if (fb * 4 + r < 15) {
+                                const int kn = (r == 3) ? 16 * (fb + 1) + 4 * g : 16 * fb + 4 * g + r + 1;
+                                wn = ld4(LS + N_W2T + kn * HID + 4 * j);
+                            }
+#pragma unroll
+                            for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
+                        }
+                }
                 STAMP(14);
                 float* sa = PS + P_SA;
 #pragma unroll
@@ -591,12 +761,28 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 wave_sync();
                 // dW1 (+ db1 as input row 11) += z^T dZ1; A = student-filtered inputs of env 4s+g
                 const float* obt = obs + TILE * t * SOS;
+                if constexpr (BS) {   // K = the tile's 16 envs (4g + jj), operands rounded to bf16
+                    float zz[4];
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const float xv = obt[(4 * s + g) * SOS + (j < 12 ? j : 0)];
-                    const float z = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const float xv = obt[(4 * g + jj) * SOS + (j < 12 ? j : 0)];
+                        zz[jj] = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
+                    }
+                    const s16x4 za = pack4(zz[0], zz[1], zz[2], zz[3]);
 #pragma unroll
-                    for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, sa[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
+                    for (int nb = 0; nb < 4; ++nb) {
+                        const float* c = sa + 16 * nb + j;
+                        gW1[nb] = mfma_k16(za, pack4(c[(4 * g) * SAS], c[(4 * g + 1) * SAS], c[(4 * g + 2) * SAS],
+                                                     c[(4 * g + 3) * SAS]), gW1[nb]);
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const float xv = obt[(4 * s + g) * SOS + (j < 12 ? j : 0)];
+                        const float z = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
+#pragma unroll
+                        for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, sa[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
+                    }
                 }
                 wave_sync();   // sa is rewritten by the next tile
                 STAMP(15);
@@ -764,14 +950,16 @@ __global__ __launch_bounds__(256) void init_ctl_kernel(uint32_t* ctl, float b1, 
 }
 
 // policy query: obs rows -> pdflat of teacher and/or student (one 16-env tile per wave pass)
+template <bool BS>
 __global__ __launch_bounds__(FBLOCK) void forward_kernel(const float* tnet, const float* snet, const float* obs,
                                                          int64_t n, float* tflat, float* sflat) {
-    __shared__ __attribute__((aligned(16))) float lds[2 * NET + FWAVES * TILE * SOS];
+    __shared__ __attribute__((aligned(16))) float lds[NET + NET_S + FWAVES * TILE * SOS];
     load_net(lds, tnet, false, FBLOCK);
-    load_net(lds + NET, snet, false, FBLOCK);
+    if constexpr (BS) load_net_bf16(lds + NET, snet, FBLOCK);
+    else load_net(lds + NET, snet, false, FBLOCK);
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
-    float* ob = lds + 2 * NET + wave * TILE * SOS;
+    float* ob = lds + NET + NET_S + wave * TILE * SOS;
     const int64_t ntiles = (n + TILE - 1) / TILE;
     for (int64_t t = (int64_t)blockIdx.x * FWAVES + wave; t < ntiles; t += (int64_t)gridDim.x * FWAVES) {
         // raw observations of the tile's 16 envs -> scratch rows (component 11 = 1)
@@ -788,12 +976,18 @@ __global__ __launch_bounds__(FBLOCK) void forward_kernel(const float* tnet, cons
             float* out = net ? sflat : tflat;
             if (!out) continue;   // wave-uniform
             const float* L = lds + net * NET;
-            mlp_forward(L, ob, j, g, H1, H2, m0, m1);
+            float ls0 = L[N_LS], ls1 = L[N_LS + 1];
+            if (BS && net == 1) {
+                mlp_forward_bf16(L, ob, j, g, H1, H2, m0, m1);
+                ls0 = L[NB_LS]; ls1 = L[NB_LS + 1];
+            } else {
+                mlp_forward(L, ob, j, g, H1, H2, m0, m1);
+            }
             if (i < n && g == 0) {
                 out[i * 4 + 0] = m0;
                 out[i * 4 + 1] = m1;
-                out[i * 4 + 2] = L[N_LS];
-                out[i * 4 + 3] = L[N_LS + 1];
+                out[i * 4 + 2] = ls0;
+                out[i * 4 + 3] = ls1;
             }
         }
         wave_sync();
@@ -844,7 +1038,10 @@ int launch_rollout(rdd_trainer* t) {
     a.stagger = t->cfg.stagger;
     a.dbg = t->dbg;
     a.inv_n_global = 1.0f / (float)t->cfg.n_envs_global;
-    hipLaunchKernelGGL(rollout_kernel, dim3(t->grid), dim3(BLOCK), 0, t->stream, a);
+    if (t->cfg.student_dtype == RDD_DTYPE_BF16)
+        hipLaunchKernelGGL(rollout_kernel<true>, dim3(t->grid), dim3(BLOCK), 0, t->stream, a);
+    else
+        hipLaunchKernelGGL(rollout_kernel<false>, dim3(t->grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
     return RD_OK;
 }
@@ -889,7 +1086,8 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     if (cfg->n_envs <= 0 || cfg->n_envs_global < cfg->n_envs || cfg->env_base < 0 ||
         cfg->n_envs > ((int64_t)1 << 31) || (cfg->loss != RDD_LOSS_MSE && cfg->loss != RDD_LOSS_KL) ||
         (cfg->act_with != RDD_ACT_TEACHER && cfg->act_with != RDD_ACT_STUDENT) || !(cfg->lr > 0) ||
-        cfg->grid < 0 || cfg->metrics_len < 0 || (cfg->stagger != 0 && cfg->stagger != 1))
+        cfg->grid < 0 || cfg->metrics_len < 0 || (cfg->stagger != 0 && cfg->stagger != 1) ||
+        (cfg->student_dtype != RDD_DTYPE_F32 && cfg->student_dtype != RDD_DTYPE_BF16))
         return rd::set_error(RD_EINVAL, "rdd_create: bad config");
     rd::DeviceGuard g(device);
     RD_HIP(g.err, "rdd_create: hipSetDevice");
@@ -1032,8 +1230,12 @@ int rdd_forward(rdd_trainer* t, const float* obs, int64_t n, float* tflat, float
     const int64_t ntiles = (n + TILE - 1) / TILE;
     int64_t blocks = (ntiles + FWAVES - 1) / FWAVES;
     if (blocks > 2 * num_cus(t->device)) blocks = 2 * num_cus(t->device);
-    hipLaunchKernelGGL(forward_kernel, dim3((unsigned)blocks), dim3(FBLOCK), 0, t->stream, t->tnet, t->snet, obs,
-                       n, tflat, sflat);
+    if (t->cfg.student_dtype == RDD_DTYPE_BF16)
+        hipLaunchKernelGGL(forward_kernel<true>, dim3((unsigned)blocks), dim3(FBLOCK), 0, t->stream, t->tnet, t->snet,
+                           obs, n, tflat, sflat);
+    else
+        hipLaunchKernelGGL(forward_kernel<false>, dim3((unsigned)blocks), dim3(FBLOCK), 0, t->stream, t->tnet,
+                           t->snet, obs, n, tflat, sflat);
     RD_HIP(hipGetLastError(), "forward_kernel launch");
     return RD_OK;
 }

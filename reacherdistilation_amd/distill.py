@@ -28,12 +28,14 @@ I32, I64, U64, F32, INT = nat.I32, nat.I64, nat.U64, nat.F32, nat.INT
 
 LOSSES = {"mse": 0, "kl": 1}
 ACTORS = {"teacher": 0, "student": 1}
+DTYPES = {"f32": 0, "bf16": 1}
 
 
 class RddConfig(ctypes.Structure):
     _fields_ = [("n_envs", I64), ("n_envs_global", I64), ("env_base", I64), ("seed", U64),
                 ("loss", I32), ("act_with", I32), ("lr", F32), ("beta1", F32), ("beta2", F32),
-                ("eps", F32), ("grid", I32), ("metrics_len", I32), ("stagger", I32)]
+                ("eps", F32), ("grid", I32), ("metrics_len", I32), ("stagger", I32),
+                ("student_dtype", I32)]
 
 
 nat.register({
@@ -75,6 +77,7 @@ class DistillConfig:
     grid: int = 0
     metrics_len: int = 4096
     stagger: bool = True               # spread episode phases over the batch (reacher_distill.h)
+    student_dtype: str = "f32"         # "f32" | "bf16" (BASELINE config 5: bf16 student MLP)
 
 
 class DistillTrainer:
@@ -98,7 +101,7 @@ class DistillTrainer:
         c = RddConfig(n_envs=self.n_local, n_envs_global=self.n_global, env_base=self.env_base,
                       seed=cfg.seed % 2 ** 64, loss=LOSSES[cfg.loss], act_with=ACTORS[cfg.act_with], lr=cfg.lr,
                       beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps, grid=cfg.grid, metrics_len=cfg.metrics_len,
-                      stagger=int(bool(cfg.stagger)))
+                      stagger=int(bool(cfg.stagger)), student_dtype=DTYPES[cfg.student_dtype])
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             nat.check(self._lib.rdd_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,

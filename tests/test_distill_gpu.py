@@ -197,3 +197,64 @@ def test_graph_capture_replay_matches_eager():
     assert b.counter() == a.counter() == 12
     assert torch.equal(a.student_params(), b.student_params())
     assert torch.equal(a.env_state(), b.env_state())
+
+
+# ---------------------------------------------------------------- bf16 student (config 5)
+# Tolerances: the kernel and oracle/policy_np.forward_bf16/backward_bf16 round the same
+# operands to bf16; they differ by f32-vs-f64 accumulation order and the kernel's 2-ulp
+# tanh, which can flip a bf16 rounding (one bf16 ulp = 2^-8 relative) of an activation now
+# and then.  So: means within 1e-3 (max) and 2e-5 (median); the gradient within 1e-2 of its
+# max entry.  Each check also asserts the kernel is much closer to the bf16 definition than
+# to the f32 student, i.e. the bf16 arithmetic is the one implemented.
+
+def test_bf16_forward_matches_bf16_oracle():
+    n = 4096
+    tr = _trainer(128, student_dtype="bf16")
+    rs = np.random.RandomState(5)
+    tr.student.flat[pn.P_B1:pn.P_W2] = rs.uniform(-.2, .2, 64)
+    tr.student.flat[pn.P_W3:pn.P_B3] = rs.normal(0, .3, 128)
+    tr.student.ob_mean[:] = rs.uniform(-.1, .1, 11); tr.student.ob_std[:] = rs.uniform(.5, 2, 11)
+    tr.set_student(tr.student)
+    ob = _obs_from_state(np.stack([rs.uniform(-3, 3, n), rs.uniform(-3, 3, n), rs.uniform(-9, 9, n),
+                                   rs.uniform(-9, 9, n), rs.uniform(-.2, .2, n), rs.uniform(-.2, .2, n),
+                                   rs.uniform(-.3, .3, n), rs.uniform(-.3, .3, n)])).astype(np.float32)
+    _, s = tr.forward(torch.tensor(ob))
+    got = s.cpu().numpy()[:, :2]
+    p, mu, sd = _np_params(tr.student)
+    fb = pn.forward_bf16(p, mu, sd, ob)
+    f32 = pn.forward(p, mu, sd, ob.astype(np.float64))
+    e_b = np.abs(got - fb["mean"])
+    e_f = np.abs(got - f32["mean"])
+    assert e_b.max() < 1e-3 and np.median(e_b) < 2e-5, (e_b.max(), np.median(e_b))
+    assert np.median(e_f) > 10 * np.median(e_b), (np.median(e_f), np.median(e_b))
+
+
+@pytest.mark.parametrize("loss", ["mse", "kl"])
+def test_bf16_rollout_gradient_matches_bf16_oracle(loss):
+    n = 65536
+    tr = _trainer(n, loss=loss, act="student", student_dtype="bf16")
+    st0 = tr.env_state().cpu().numpy()
+    sp = tr.student_params().cpu().numpy().astype(np.float64)
+    tr.rollout()
+    g = tr.grad().cpu().numpy()
+    ob = _obs_from_state(st0).astype(np.float32)
+    fs = pn.forward_bf16(sp, *_np_params(tr.student)[1:], ob)
+    ft = pn.forward(*_np_params(tr.teacher), ob.astype(np.float64))
+    L, dmean, dls, sq = pn.loss_and_dmean(fs, ft, loss, n)
+    gb = pn.backward_bf16(sp, fs, dmean, dls)
+    fs32 = pn.forward(sp, *_np_params(tr.student)[1:], ob.astype(np.float64))
+    g32 = pn.backward(sp, fs32, *pn.loss_and_dmean(fs32, ft, loss, n)[1:3])
+    err_b = np.abs(g - gb).max() / np.abs(gb).max()
+    err_f = np.abs(g - g32).max() / np.abs(g32).max()
+    assert err_b < 1e-2, err_b
+    assert err_f > 2 * err_b, (err_f, err_b)
+
+
+def test_bf16_dagger_student_learns():
+    """DAgger with the bf16 student (config 5's arithmetic): action-MSE falls by >10x."""
+    tr = _trainer(16384, act="student", lr=1e-3, student_dtype="bf16")
+    for _ in range(300):
+        tr.step()
+    m = tr.metrics(300)
+    mse = m[:, 2] / (2 * m[:, 3])
+    assert mse[-10:].mean() < 0.1 * mse[:10].mean(), (mse[:10].mean(), mse[-10:].mean())
