@@ -94,6 +94,16 @@ int rdd_reset(rdd_trainer* tr);
 int rdd_rollout(rdd_trainer* tr);
 int rdd_apply(rdd_trainer* tr);
 int rdd_step(rdd_trainer* tr);
+/* Observation-batch mode: the same fused teacher relabel + student forward/backward +
+ * loss, on caller-given observation rows obs [n][11] (device) instead of the envs' state,
+ * and no env step -- the reference's training on windows drawn from its dataset buffer
+ * (mlp_train.py:146-161 over dataset.py:179-194 training_batches).  The MSE is normalised
+ * by n_global (all ranks' rows).  rdd_rollout_obs fills rdd_grad_buffer() (all-reduce it,
+ * then rdd_apply); rdd_step_obs is the single-rank rollout_obs + apply.  These advance the
+ * optimiser-step counter only; the envs' episode clocks advance with env rollouts. */
+int rdd_rollout_obs(rdd_trainer* tr, const float* obs, int64_t n, int64_t n_global);
+int rdd_step_obs(rdd_trainer* tr, const float* obs, int64_t n);
+
 /* The same work as individual launches (for per-kernel timing with events in between):
  * RDD_STAGE_ROLLOUT = the fused rollout kernel only; RDD_STAGE_REDUCE = partials -> grad;
  * RDD_STAGE_APPLY = Adam + counter; RDD_STAGE_REDUCE_APPLY = both in one launch.
@@ -116,9 +126,11 @@ int rdd_forward(rdd_trainer* tr, const float* obs, int64_t n, float* t_pdflat, f
 int rdd_get_env_state(rdd_trainer* tr, float* state);
 int rdd_set_env_state(rdd_trainer* tr, const float* state);
 
-/* Host-synchronising readers.  Metrics per completed step s (ring of metrics_len):
+/* Host-synchronising readers (they also report a timed-out producer/consumer hand-off
+ * inside a rollout as an error).  Metrics per optimiser step s (ring of metrics_len):
  * {sum reward, loss, sum (mu_s - mu_t)^2, envs}; out [count][4] for the last `count` steps. */
-int rdd_get_counter(rdd_trainer* tr, int64_t* steps);
+int rdd_get_counter(rdd_trainer* tr, int64_t* steps);              /* env steps */
+int rdd_get_counters(rdd_trainer* tr, int64_t* env_steps, int64_t* opt_steps);
 int rdd_read_metrics(rdd_trainer* tr, int64_t count, double* out);
 
 #ifdef __cplusplus

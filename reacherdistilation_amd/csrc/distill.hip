@@ -105,6 +105,7 @@ struct RolloutArgs {
     int loss, act_student, stagger;
     float inv_n_global;
     unsigned long long* dbg;               // RD_STAMPS builds: [grid*WAVES][16] stamp sums
+    const float* obs_in;                   // observation-batch mode: [n][11] rows, no env step
 };
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
@@ -501,8 +502,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         reinterpret_cast<uint32_t*>(lds + NET + NET_S + (threadIdx.x >> 2) * PSCR + P_FLAGS)[threadIdx.x & 3] = 0u;
 
     const uint32_t C = a.ctl[0];
-    // snapshot of the step words for reduce_adam_kernel, which rewrites ctl[0..3]
+    // snapshot of the step words for reduce_adam_kernel, which rewrites ctl[0..3]; ctl[12]
+    // tells it whether this launch stepped the envs (the env clock advances only then)
     if (blockIdx.x == 0 && threadIdx.x < 4) a.ctl[4 + threadIdx.x] = a.ctl[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x == 4) a.ctl[12] = a.obs_in ? 0u : 1u;
     __syncthreads();
     STAMP(1);
 
@@ -532,10 +535,15 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
             float* act = PS + P_ACT + (k & 1) * GROUP * 2;
             {
-                rd::State st{};
-                if (i < a.n) load_state(a.state, a.n, (uint32_t)i, st);
                 float ob[OBD];
-                rd::observe(st, ob);
+                if (a.obs_in) {   // observation-batch mode: rows given by the caller
+#pragma unroll
+                    for (int q = 0; q < OBD; ++q) ob[q] = i < a.n ? a.obs_in[i * OBD + q] : 0.0f;
+                } else {
+                    rd::State st{};
+                    if (i < a.n) load_state(a.state, a.n, (uint32_t)i, st);
+                    rd::observe(st, ob);
+                }
                 float* o = obs + lane * SOS;
                 st4(o, f32x4{ob[0], ob[1], ob[2], ob[3]});
                 st4(o + 4, f32x4{ob[4], ob[5], ob[6], ob[7]});
@@ -792,6 +800,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             STAMP(4);
             const uint32_t iu = (uint32_t)i;
             const bool valid = i < a.n;
+            if (a.obs_in) {   // observation-batch mode: no env to step
+                if (valid) met_n += 1.0f;
+                publish(flags + 2, k + 1);
+                continue;
+            }
             rd::State st{};
             if (valid) load_state(a.state, a.n, iu, st);
             const float act0 = act[lane * 2], act1 = act[lane * 2 + 1];
@@ -855,9 +868,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     STAMP(7);
 }
 
-// ctl words: [0] completed steps C, [2] beta1^t, [3] beta2^t (f32 bits); [4..7] the
-// rollout's snapshot of [0..3], which this kernel reads so that block 0 may rewrite
-// [0..3] without racing the other blocks (no atomics, no fences: stream order suffices).
+// ctl words: [0] env steps C (the episode clocks), [1] optimiser steps S (metrics ring),
+// [2] beta1^S, [3] beta2^S (f32 bits); [4..7] the rollout's snapshot of [0..3], which this
+// kernel reads so that block 0 may rewrite [0..3] without racing the other blocks (no
+// atomics, no fences: stream order suffices); [8] hand-off timeout; [12] 1 if the last
+// rollout stepped the envs.
 struct ReduceArgs {
     const float* ws;
     int nblk;
@@ -880,7 +895,7 @@ constexpr int RED_GRID = (P_PAD + RED_COLS - 1) / RED_COLS;
 // Sum the rollout's per-workgroup partials (fixed order: deterministic), then TF1 Adam.
 __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
     __shared__ float part[RED_ROWS][RED_COLS];
-    const uint32_t C = a.ctl[4];
+    const uint32_t C = a.ctl[4], S = a.ctl[5];
     const float b1p = __uint_as_float(a.ctl[6]), b2p = __uint_as_float(a.ctl[7]);
     const int col = threadIdx.x & (RED_COLS - 1), row = threadIdx.x / RED_COLS;
     const int p = blockIdx.x * RED_COLS + col;
@@ -909,7 +924,7 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
             for (int r = 0; r < RED_ROWS; ++r) q[r & 3] += part[r][col];
             g = (q[0] + q[1]) + (q[2] + q[3]);
             if (p < P_TOT) a.grad[p] = g;
-            else a.hist[(int64_t)(C % (uint32_t)a.hist_len) * N_MET + (p - P_TOT)] = g;
+            else a.hist[(int64_t)(S % (uint32_t)a.hist_len) * N_MET + (p - P_TOT)] = g;
         } else {
             g = p < P_TOT ? a.grad[p] : 0.f;
         }
@@ -925,7 +940,8 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
         }
     }
     if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) {
-        a.ctl[0] = C + 1u;
+        a.ctl[0] = C + a.ctl[12];   // env steps: only after a launch that stepped the envs
+        a.ctl[1] = S + 1u;          // optimiser steps
         a.ctl[2] = __float_as_uint(b1p * a.b1);
         a.ctl[3] = __float_as_uint(b2p * a.b2);
     }
@@ -947,6 +963,7 @@ __global__ __launch_bounds__(256) void init_ctl_kernel(uint32_t* ctl, float b1, 
         const int o = 4 * threadIdx.x;   // live words and their snapshot
         ctl[o] = 0u; ctl[o + 1] = 0u; ctl[o + 2] = __float_as_uint(b1); ctl[o + 3] = __float_as_uint(b2);
     }
+    if (threadIdx.x >= 8 && threadIdx.x < 16) ctl[threadIdx.x] = threadIdx.x == 12 ? 1u : 0u;
 }
 
 // policy query: obs rows -> pdflat of teacher and/or student (one 16-env tile per wave pass)
@@ -1018,14 +1035,16 @@ struct rdd_trainer {
     float* hist = nullptr;     // [hist_len][4]
     uint32_t* ctl = nullptr;   // [16]: step words, snapshot, [8] hand-off timeout flag
     unsigned long long* dbg = nullptr;   // RD_STAMPS builds only
+    int last_grid = 0;                   // workgroups of the last rollout (rows of ws to reduce)
 
 };
 
 namespace {
 
-int launch_rollout(rdd_trainer* t) {
+int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs = 0, int64_t n_obs_global = 0) {
     RolloutArgs a;
-    a.n = t->cfg.n_envs;
+    a.n = obs_in ? n_obs : t->cfg.n_envs;
+    a.obs_in = obs_in;
     a.env_base = t->cfg.env_base;
     a.seed = t->cfg.seed;
     a.state = t->state;
@@ -1037,11 +1056,17 @@ int launch_rollout(rdd_trainer* t) {
     a.act_student = t->cfg.act_with == RDD_ACT_STUDENT;
     a.stagger = t->cfg.stagger;
     a.dbg = t->dbg;
-    a.inv_n_global = 1.0f / (float)t->cfg.n_envs_global;
+    a.inv_n_global = 1.0f / (float)(obs_in ? n_obs_global : t->cfg.n_envs_global);
+    int grid = t->grid;   // the workspace holds t->grid partial rows
+    if (obs_in) {
+        const int64_t want = ((n_obs + GROUP - 1) / GROUP + PAIRS - 1) / PAIRS;
+        grid = (int)(want < t->grid ? want : t->grid);
+    }
+    t->last_grid = grid;
     if (t->cfg.student_dtype == RDD_DTYPE_BF16)
-        hipLaunchKernelGGL(rollout_kernel<true>, dim3(t->grid), dim3(BLOCK), 0, t->stream, a);
+        hipLaunchKernelGGL(rollout_kernel<true>, dim3(grid), dim3(BLOCK), 0, t->stream, a);
     else
-        hipLaunchKernelGGL(rollout_kernel<false>, dim3(t->grid), dim3(BLOCK), 0, t->stream, a);
+        hipLaunchKernelGGL(rollout_kernel<false>, dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
     return RD_OK;
 }
@@ -1049,7 +1074,7 @@ int launch_rollout(rdd_trainer* t) {
 int launch_reduce(rdd_trainer* t, int reduce, int adam, int bump) {
     ReduceArgs a;
     a.ws = t->ws;
-    a.nblk = t->grid;
+    a.nblk = t->last_grid;
     a.grad = t->grad;
     a.params = t->snet;
     a.m = t->m;
@@ -1098,9 +1123,10 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     t->device = device;
     t->stream = (hipStream_t)hip_stream;
     const int64_t ngroups = (cfg->n_envs + GROUP - 1) / GROUP;
-    const int64_t want = (ngroups + WAVES - 1) / WAVES;
+    const int64_t want = (ngroups + PAIRS - 1) / PAIRS;   // one group per producer/consumer pair
     const int cap = cfg->grid > 0 ? cfg->grid : num_cus(device);
     t->grid = (int)(want < cap ? want : cap);
+    t->last_grid = t->grid;
     const size_t netf = P_TOT + 2 * OBD;
     hipError_t e = hipSuccess;
     auto alloc = [&](void** p, size_t bytes) {
@@ -1202,6 +1228,23 @@ int rdd_step(rdd_trainer* t) {
     return launch_reduce(t, 1, 1, 1);
 }
 
+int rdd_rollout_obs(rdd_trainer* t, const float* obs, int64_t n, int64_t n_global) {
+    if (!t || !obs || n <= 0 || n > ((int64_t)1 << 31) || n_global < n)
+        return rd::set_error(RD_EINVAL, "rdd_rollout_obs: bad argument");
+    rd::DeviceGuard g(t->device);
+    RD_HIP(g.err, "rdd_rollout_obs: hipSetDevice");
+    if (int rc = launch_rollout(t, obs, n, n_global)) return rc;
+    return launch_reduce(t, 1, 0, 0);
+}
+
+int rdd_step_obs(rdd_trainer* t, const float* obs, int64_t n) {
+    if (!t || !obs || n <= 0 || n > ((int64_t)1 << 31)) return rd::set_error(RD_EINVAL, "rdd_step_obs: bad argument");
+    rd::DeviceGuard g(t->device);
+    RD_HIP(g.err, "rdd_step_obs: hipSetDevice");
+    if (int rc = launch_rollout(t, obs, n, n)) return rc;
+    return launch_reduce(t, 1, 1, 1);
+}
+
 int rdd_launch_stage(rdd_trainer* t, int stage) {
     if (!t) return rd::set_error(RD_EINVAL, "rdd_launch_stage: null handle");
     rd::DeviceGuard g(t->device);
@@ -1256,20 +1299,35 @@ int rdd_set_env_state(rdd_trainer* t, const float* state) {
     return RD_OK;
 }
 
+static int read_ctl(rdd_trainer* t, uint32_t (&c)[16], const char* what) {
+    rd::DeviceGuard g(t->device);
+    RD_HIP(hipMemcpyAsync(c, t->ctl, sizeof(c), hipMemcpyDeviceToHost, t->stream), what);
+    RD_HIP(hipStreamSynchronize(t->stream), what);
+    if (c[8]) return rd::set_error(RD_EINVAL, "%s: a rollout's producer/consumer hand-off timed out", what);
+    return RD_OK;
+}
+
 int rdd_get_counter(rdd_trainer* t, int64_t* steps) {
     if (!t || !steps) return rd::set_error(RD_EINVAL, "rdd_get_counter: null argument");
-    rd::DeviceGuard g(t->device);
-    uint32_t c = 0;
-    RD_HIP(hipMemcpyAsync(&c, t->ctl, sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream), "rdd_get_counter");
-    RD_HIP(hipStreamSynchronize(t->stream), "rdd_get_counter");
-    *steps = c;
+    uint32_t c[16];
+    if (int rc = read_ctl(t, c, "rdd_get_counter")) return rc;
+    *steps = c[0];
+    return RD_OK;
+}
+
+int rdd_get_counters(rdd_trainer* t, int64_t* env_steps, int64_t* opt_steps) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdd_get_counters: null handle");
+    uint32_t c[16];
+    if (int rc = read_ctl(t, c, "rdd_get_counters")) return rc;
+    if (env_steps) *env_steps = c[0];
+    if (opt_steps) *opt_steps = c[1];
     return RD_OK;
 }
 
 int rdd_read_metrics(rdd_trainer* t, int64_t count, double* out) {
     if (!t || !out || count < 0) return rd::set_error(RD_EINVAL, "rdd_read_metrics: bad argument");
-    int64_t steps = 0;
-    if (int rc = rdd_get_counter(t, &steps)) return rc;
+    int64_t steps = 0;   // metrics are kept per optimiser step
+    if (int rc = rdd_get_counters(t, nullptr, &steps)) return rc;
     const int64_t H = t->cfg.metrics_len;
     if (count > steps || count > H) return rd::set_error(RD_EINVAL, "rdd_read_metrics: only %lld steps kept",
                                                          (long long)(steps < H ? steps : H));

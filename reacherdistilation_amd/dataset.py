@@ -1,0 +1,103 @@
+"""Device-resident rollout -> distill buffer: the hand-off the reference's ``Dataset`` provides
+(reference dataset.py:72-296), kept in HBM instead of lists of Python dicts.
+
+Mirrored interface (reference dataset.py): ``write(ob, reward, t_pdflat, s_pdflat,
+stepped_with)`` appends one step record of the current episode (:118-143, including the
+``prev``/``prew`` fields = the previous record's teacher pdflat and reward, zeros at t = 0,
+:132-133,152-163); ``flush()`` closes the episode (:146-149); ``num_episodes()``;
+``training_batches()`` yields TRAINING_EPOCHS random windows -- LSTM_BATCH_SIZE episodes
+drawn with replacement, one common start in [0, EPISODE_STEPS - STEPS_UNROLLED] -- as
+``(ob [T,B,11], t_pdflat [T,B,4], prev_pdflat [T,B,4], prev_rew [T,B,1])`` (:179-202);
+``test_batch(ob)`` builds the [T,B,11] window ending at the current observation (:205-235).
+
+Storage: one ring of ``capacity`` complete episodes x EPISODE_STEPS records x 21 floats
+(ob 11 | rew 1 | t 4 | s 4 | with 1) plus the open episode, all on ``device``.  The
+reference's gzip-JSON pages on disk (DatasetStore, :14-65) are out of scope here
+(DESIGN.md §7); the ring replaces its paging.
+"""
+from __future__ import annotations
+
+import torch
+
+from .config import (EPISODE_STEPS, LSTM_BATCH_SIZE, OBSPACE_SHAPE, PDFLAT_SHAPE, STEPS_UNROLLED,
+                     TRAINING_EPOCHS)
+
+F_OB, F_REW, F_T, F_S, F_WITH = 0, OBSPACE_SHAPE, OBSPACE_SHAPE + 1, OBSPACE_SHAPE + 1 + PDFLAT_SHAPE, \
+    OBSPACE_SHAPE + 1 + 2 * PDFLAT_SHAPE
+REC = F_WITH + 1   # 21 floats per step record
+
+
+class DeviceDataset:
+    def __init__(self, capacity: int = 5000, device="cuda:0", seed: int = 0, batch_size: int = LSTM_BATCH_SIZE,
+                 steps_unrolled: int = STEPS_UNROLLED, epochs: int = TRAINING_EPOCHS):
+        self.device = torch.device(device)
+        self.capacity = int(capacity)
+        self.ring = torch.zeros(self.capacity, EPISODE_STEPS, REC, dtype=torch.float32, device=self.device)
+        self.curr = torch.zeros(EPISODE_STEPS, REC, dtype=torch.float32, device=self.device)
+        self.curr_len = 0
+        self.num_total_episodes = 0
+        self.B, self.T, self.epochs = int(batch_size), int(steps_unrolled), int(epochs)
+        self._gen = torch.Generator().manual_seed(int(seed))   # host RNG: indices only
+
+    # -- reference interface -------------------------------------------------------------
+    def num_episodes(self) -> int:
+        return self.num_total_episodes
+
+    def write(self, ob, reward=0.0, t_pdflat=None, s_pdflat=None, stepped_with: str = "t"):
+        if self.curr_len >= EPISODE_STEPS:
+            raise RuntimeError(f"episode already holds {EPISODE_STEPS} steps; flush() first")
+        r = self.curr[self.curr_len]
+        r[F_OB:F_REW] = torch.as_tensor(ob, dtype=torch.float32).reshape(-1)[:OBSPACE_SHAPE].to(self.device)
+        r[F_REW] = float(reward)
+        z = torch.zeros(PDFLAT_SHAPE)
+        r[F_T:F_S] = torch.as_tensor(t_pdflat if t_pdflat is not None else z, dtype=torch.float32).reshape(-1).to(
+            self.device)
+        r[F_S:F_WITH] = torch.as_tensor(s_pdflat if s_pdflat is not None else z, dtype=torch.float32).reshape(-1).to(
+            self.device)
+        r[F_WITH] = 1.0 if stepped_with == "s" else 0.0
+        self.curr_len += 1
+
+    def flush(self):
+        """Close the current episode.  Only complete episodes (EPISODE_STEPS records) enter
+        the ring: the windows of training_batches() span any start in [0, 40]."""
+        if self.curr_len == EPISODE_STEPS:
+            self.ring[self.num_total_episodes % self.capacity].copy_(self.curr)
+        self.curr.zero_()
+        self.curr_len = 0
+        self.num_total_episodes += 1
+
+    def stored(self) -> int:
+        return min(self.num_total_episodes, self.capacity)
+
+    def _prev(self, rec: torch.Tensor) -> torch.Tensor:
+        """prev pdflat / prev reward of each record: the previous record's t and rew."""
+        prev = torch.zeros(*rec.shape[:-1], PDFLAT_SHAPE + 1, dtype=rec.dtype, device=rec.device)
+        prev[..., 1:, :PDFLAT_SHAPE] = rec[..., :-1, F_T:F_S]
+        prev[..., 1:, PDFLAT_SHAPE] = rec[..., :-1, F_REW]
+        return prev
+
+    def training_batches(self):
+        n = self.stored()
+        if n == 0:
+            return
+        for _ in range(self.epochs):
+            eps = torch.randint(0, n, (self.B,), generator=self._gen)
+            start = int(torch.randint(0, EPISODE_STEPS - self.T + 1, (1,), generator=self._gen))
+            rec = self.ring[eps.to(self.device)]                      # [B, 50, REC]
+            prev = self._prev(rec)[:, start:start + self.T]           # [B, T, 5]
+            win = rec[:, start:start + self.T].transpose(0, 1)        # [T, B, REC]
+            prev = prev.transpose(0, 1)
+            yield (win[..., F_OB:F_REW].contiguous(), win[..., F_T:F_S].contiguous(),
+                   prev[..., :PDFLAT_SHAPE].contiguous(), prev[..., PDFLAT_SHAPE:].contiguous())
+
+    def test_batch(self, ob):
+        """[T, B, 11]: batch column B-1 holds the window of the current episode ending at
+        `ob` (its last T-1 observations, zero-padded at the front); the other columns are zero,
+        as in the reference's ob_batch_test_array (dataset.py:219-240)."""
+        ob = torch.as_tensor(ob, dtype=torch.float32).reshape(-1)[:OBSPACE_SHAPE].to(self.device)
+        out = torch.zeros(self.T, self.B, OBSPACE_SHAPE, device=self.device)
+        k = min(self.curr_len, self.T - 1)
+        if k > 0:
+            out[self.T - 1 - k:self.T - 1, self.B - 1] = self.curr[self.curr_len - k:self.curr_len, F_OB:F_REW]
+        out[self.T - 1, self.B - 1] = ob
+        return out

@@ -57,6 +57,9 @@ nat.register({
     "rdd_get_env_state": (INT, [P, P]),
     "rdd_set_env_state": (INT, [P, P]),
     "rdd_get_counter": (INT, [P, ctypes.POINTER(I64)]),
+    "rdd_get_counters": (INT, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+    "rdd_rollout_obs": (INT, [P, P, I64, I64]),
+    "rdd_step_obs": (INT, [P, P, I64]),
     "rdd_read_metrics": (INT, [P, I64, P]),
 })
 
@@ -148,6 +151,38 @@ class DistillTrainer:
             self.allreduce_grad()
             nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
         self.steps += 1
+
+    # -- observation-batch mode (the reference's dataset-window training) ---------------
+    def step_obs(self, obs: torch.Tensor):
+        """One distillation step on given observation rows [n, 11] (no env step): teacher
+        relabel, student forward/backward, loss, (all-reduce), TF1 Adam."""
+        obs = self._obs_arg(obs)
+        n = obs.shape[0]
+        if self.world == 1:
+            nat.check(self._lib.rdd_step_obs(self._h, nat.ptr(obs), n), "rdd_step_obs")
+        else:
+            nat.check(self._lib.rdd_rollout_obs(self._h, nat.ptr(obs), n, n * self.world), "rdd_rollout_obs")
+            self.allreduce_grad()
+            nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
+        self._keep = obs   # the launch reads it asynchronously
+
+    def rollout_obs(self, obs: torch.Tensor, n_global: int | None = None):
+        obs = self._obs_arg(obs)
+        nat.check(self._lib.rdd_rollout_obs(self._h, nat.ptr(obs), obs.shape[0], n_global or obs.shape[0]),
+                  "rdd_rollout_obs")
+        self._keep = obs
+
+    def _obs_arg(self, obs):
+        obs = torch.as_tensor(obs).to(self.device, torch.float32).contiguous()
+        if obs.dim() != 2 or obs.shape[1] != 11 or obs.shape[0] == 0:
+            raise ValueError("obs must be [n, 11]")
+        return obs
+
+    def counters(self):
+        """(env steps, optimiser steps)."""
+        e, o = ctypes.c_int64(), ctypes.c_int64()
+        nat.check(self._lib.rdd_get_counters(self._h, ctypes.byref(e), ctypes.byref(o)), "rdd_get_counters")
+        return e.value, o.value
 
     def set_stream(self, stream: torch.cuda.Stream):
         nat.check(self._lib.rdd_set_stream(self._h, ctypes.c_void_p(stream.cuda_stream)), "rdd_set_stream")

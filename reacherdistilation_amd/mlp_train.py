@@ -1,0 +1,77 @@
+"""The reference's MLP distillation driver, ``mlp_train.train(train, restore)`` (reference
+src/distilation/mlp_train.py:18-204), re-expressed over the MI355X path: the env is the HIP
+Reacher-v2 (``make_mujoco_env``), teacher queries and the student's training step are the
+fused kernels behind ``DistillTrainer`` (``rdd_forward`` / ``rdd_step_obs``), and the
+rollout -> distill buffer is the device-resident ``DeviceDataset``.
+
+Phases as in the reference:
+  1. (:120-139) the teacher steps the env until ``num_episodes() > 2 * MLP_BATCH_SIZE``,
+     every step recorded (ob, reward of the previous step, teacher pdflat, 't');
+  2. (:143-204) per env step: one optimiser step on each window from
+     ``dataset.training_batches()``, teacher relabel of the current observation, the student's
+     (deterministic mean) action, record with 's', env.step with the student action; episode
+     boundaries reset the env and flush the dataset; stop after ``episodes`` episodes.
+
+Fixes of the reference as committed: the student
+is the 2x64 MlpPolicy taking the observation (the committed graph's (10,20,.) vs (1,20,.)
+placeholder mismatch and its random-noise prev_pdflat/prev_rew inputs are not reproduced);
+every row of a [T, B] window is a training row; dropout keep_prob = 1.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .config import MLP_BATCH_SIZE, MLP_EPISODE_BUDGET, OBSPACE_SHAPE
+from .dataset import DeviceDataset
+from .distill import DistillConfig, DistillTrainer
+from .env import make_mujoco_env
+from .policy import TeacherAgent
+
+
+def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPISODE_BUDGET,
+          loss: str = "kl", lr: float = 1e-4, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
+          warmup_episodes: int = 2 * MLP_BATCH_SIZE, log=print):
+    """Returns (trainer, dataset, per-episode summed training loss)."""
+    env = make_mujoco_env("Reacher-v2", seed, device=device)
+    teacher = TeacherAgent(restore=restore, path=teacher_path)
+    tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr), device=device, teacher=teacher.pi)
+    dataset = DeviceDataset(device=device, seed=seed)
+    ob = env.reset()
+    reward = 0.0
+    losses = []
+    if not train:
+        return tr, dataset, losses
+
+    def query(o):
+        t, s = tr.forward(torch.as_tensor(np.asarray(o, np.float32)).view(1, OBSPACE_SHAPE))
+        return t[0].cpu().numpy(), s[0].cpu().numpy()
+
+    log("Begin Training! First Accumulate observation with teacher")
+    while dataset.num_episodes() <= warmup_episodes:
+        t_pdflat, _ = query(ob)
+        dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, stepped_with="t")
+        ob, reward, new, _ = env.step(t_pdflat[:2])
+        if new:
+            ob = env.reset()
+            dataset.flush()
+    log("Accumulated sufficient data points from teacher. now train")
+
+    total_loss = 0.0
+    while True:
+        for ob_batch, _t, _prev, _prew in dataset.training_batches():
+            tr.step_obs(ob_batch.reshape(-1, OBSPACE_SHAPE))
+            total_loss += float(tr.metrics(1)[0, 1])
+        t_pdflat, s_pdflat = query(ob)
+        dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, s_pdflat=s_pdflat, stepped_with="s")
+        ob, reward, new, _ = env.step(s_pdflat[:2])
+        if new:
+            log("************** Episode {0} ****************".format(dataset.num_episodes()))
+            ob = env.reset()
+            log("recent loss: %f " % total_loss)
+            losses.append(total_loss)
+            total_loss = 0.0
+            dataset.flush()
+            if dataset.num_episodes() >= episodes:
+                break
+    return tr, dataset, losses

@@ -1,0 +1,69 @@
+"""DeviceDataset (reference dataset.py Dataset) semantics on CPU tensors: record layout,
+prev/prew fields, training-window sampling and the test batch (reference
+tests/dataset_unit_test.py checks the same windowing on its fixture)."""
+import numpy as np
+import pytest
+import torch
+
+from reacherdistilation_amd.dataset import DeviceDataset
+
+
+def _fill(ds, episodes):
+    for e in range(episodes):
+        for k in range(50):
+            ob = np.full(11, 100.0 * e + k)          # encodes (episode, step)
+            t = np.array([e, k, -1, -2], float)
+            ds.write(ob=ob, reward=0.5 * k, t_pdflat=t, stepped_with="t")
+        ds.flush()
+
+
+def test_training_windows_are_contiguous_episode_slices():
+    ds = DeviceDataset(capacity=8, device="cpu", seed=1)
+    _fill(ds, 5)
+    assert ds.num_episodes() == 5 and ds.stored() == 5
+    (ob, t, prev, prew), = list(ds.training_batches())
+    assert ob.shape == (10, 20, 11) and t.shape == (10, 20, 4) and prev.shape == (10, 20, 4) and prew.shape == (10, 20, 1)
+    code = ob[..., 0].numpy()
+    ep, step = code // 100, code % 100
+    assert np.all(ep == ep[0:1])                           # one episode per batch column
+    assert np.all(np.diff(step, axis=0) == 1)              # consecutive steps in a window
+    assert np.all(step[0] == step[0, 0]) and 0 <= step[0, 0] <= 40   # one common start
+    # prev = the previous record's teacher pdflat and reward (zeros at the episode start)
+    s0 = int(step[0, 0])
+    exp_prev = np.where(step > 0, step - 1, 0)
+    assert np.array_equal(prev[..., 1].numpy(), exp_prev.astype(np.float32))
+    assert np.allclose(prew[..., 0].numpy(), np.where(step > 0, 0.5 * (step - 1), 0.0))
+    assert s0 >= 0
+
+
+def test_ring_overwrites_oldest_episode():
+    ds = DeviceDataset(capacity=3, device="cpu")
+    _fill(ds, 5)
+    eps = sorted({int(x) for x in ds.ring[:, 0, 0].numpy() // 100})
+    assert eps == [2, 3, 4]
+
+
+def test_partial_episode_not_stored():
+    ds = DeviceDataset(capacity=3, device="cpu")
+    for k in range(7):
+        ds.write(ob=np.ones(11))
+    ds.flush()
+    assert ds.num_episodes() == 1 and float(ds.ring.abs().sum()) == 0.0
+    with pytest.raises(RuntimeError):
+        for k in range(51):
+            ds.write(ob=np.ones(11))
+
+
+@pytest.mark.parametrize("length", [0, 3, 9, 12])
+def test_test_batch_window(length):
+    ds = DeviceDataset(device="cpu")
+    for k in range(length):
+        ds.write(ob=np.full(11, k + 1.0))
+    tb = ds.test_batch(np.full(11, 99.0)).numpy()
+    assert tb.shape == (10, 20, 11)
+    assert not tb[:, :19].any()                            # only the last batch column
+    col = tb[:, 19, 0]
+    assert col[-1] == 99.0
+    k = min(length, 9)
+    assert np.array_equal(col[9 - k:9], np.arange(length - k + 1, length + 1, dtype=np.float32))
+    assert not col[:9 - k].any()
