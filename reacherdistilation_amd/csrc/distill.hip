@@ -106,6 +106,8 @@ struct RolloutArgs {
     float inv_n_global;
     unsigned long long* dbg;               // RD_STAMPS builds: [grid*WAVES][16] stamp sums
     const float* obs_in;                   // observation-batch mode: [n][11] rows, no env step
+    const float* timg;                     // prepacked LDS images (pack_net_kernel)
+    const float* simg;
 };
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
@@ -415,6 +417,85 @@ __device__ void load_net_bf16(float* L, const float* g, int nthreads) {
     }
 }
 
+// ---------------------------------------------------------------- prepacked LDS images
+// The rollout's LDS images (teacher NET floats, student NET_S floats) are kept ready in
+// HBM: pack_param() writes one parameter's value into every image slot it occupies.  The
+// images are built once by pack_net_kernel (rdd_set_teacher / rdd_set_student) and the
+// student's is refreshed by reduce_adam_kernel as it updates each parameter, so a rollout's
+// prologue is a plain 16-B copy instead of a gather with index arithmetic.
+__device__ __forceinline__ void pack_param(float* img, int p, float v, bool student, bool bf16) {
+    if (!bf16) {
+        if (p < P_B1) {
+            const int k = p >> 6, f = p & 63;
+            img[N_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+        } else if (p < P_W2) {
+            const int f = p - P_B1;
+            img[N_W1 + OBD * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+        } else if (p < P_B2) {
+            const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
+            img[N_W2 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+            if (student) img[N_W2T + f * HID + (k & 15) * 4 + (k >> 4)] = v;
+        } else if (p < P_W3) {
+            img[N_B2 + (p - P_B2)] = kTanhScale * v;
+        } else if (p < P_B3) {
+            img[N_W3 + (p - P_W3)] = v;
+        } else if (p < P_LS) {
+            img[N_B3 + (p - P_B3)] = v;
+        } else if (p < P_TOT) {
+            img[N_LS + (p - P_LS)] = v;
+        }
+        return;
+    }
+    unsigned short* h = reinterpret_cast<unsigned short*>(img);
+    if (p < P_B1) {
+        const int k = p >> 6, f = p & 63;   // k = 8gg + jj
+        h[2 * NB_W1 + (((k >> 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + (k & 7)] = bf16_bits(v);
+    } else if (p < P_W2) {
+        img[NB_B1 + (p - P_B1)] = v;
+    } else if (p < P_B2) {
+        const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
+        // forward image: k (H1 feature) is the permuted K index, f the output row
+        {
+            const int s = k >> 5, r = k & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
+            h[2 * NB_W2F + (((s * 4 + gg) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + jj] = bf16_bits(v);
+        }
+        // dH1 image: f (dZ2 feature) is the permuted K index, k the output row
+        {
+            const int s = f >> 5, r = f & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
+            h[2 * NB_W2B + (((s * 4 + gg) * 4 + (k >> 4)) * 16 + (k & 15)) * 8 + jj] = bf16_bits(v);
+        }
+    } else if (p < P_W3) {
+        img[NB_B2 + (p - P_B2)] = v;
+    } else if (p < P_B3) {
+        img[NB_W3 + (p - P_W3)] = bf16_round(v);
+    } else if (p < P_LS) {
+        img[NB_B3 + (p - P_B3)] = v;
+    } else if (p < P_TOT) {
+        img[NB_LS + (p - P_LS)] = v;
+    }
+}
+
+// net = params[P] | mu[11] | sd[11] -> image (every slot, including zero padding and filter)
+__global__ __launch_bounds__(256) void pack_net_kernel(const float* net, float* img, int img_floats, int student,
+                                                       int bf16) {
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    // phase 1 (one launch): zero the image, then the filter words, then every parameter
+    for (int i = x; i < img_floats; i += gridDim.x * 256) img[i] = 0.0f;
+    __syncthreads();   // (single-block launch: see rdd host code)
+    if (x < 12) {
+        const int mu = bf16 ? NB_MU : N_MU, rs = bf16 ? NB_RS : N_RS;
+        img[mu + x] = x < OBD ? net[P_TOT + x] : 0.0f;
+        img[rs + x] = x < OBD ? 1.0f / net[P_TOT + OBD + x] : 1.0f;
+    }
+    for (int p = x; p < P_TOT; p += gridDim.x * 256) pack_param(img, p, net[p], student != 0, bf16 != 0);
+}
+
+__device__ __forceinline__ void copy_image(float* L, const float* img, int floats, int nthreads) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(img);
+    f32x4* dst = reinterpret_cast<f32x4*>(L);
+    for (int i = threadIdx.x; i < floats / 4; i += nthreads) dst[i] = src[i];
+}
+
 // bf16-student forward of a 16-env tile (same outputs/layouts as mlp_forward).
 __device__ __forceinline__ void mlp_forward_bf16(const float* L, const float* ob, int j, int g, f32x4 (&H1)[4],
                                                  f32x4 (&H2)[4], float& m0, float& m1) {
@@ -494,9 +575,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     uint32_t* err = a.ctl + 8;
 
     STAMP(0);
-    load_net(LT, a.tnet, false, BLOCK);
-    if constexpr (BS) load_net_bf16(LS, a.snet, BLOCK);
-    else load_net(LS, a.snet, true, BLOCK);
+    copy_image(LT, a.timg, NET, BLOCK);
+    copy_image(LS, a.simg, NET_S, BLOCK);
     constexpr int SW3 = BS ? NB_W3 : N_W3, SMU = BS ? NB_MU : N_MU, SRS = BS ? NB_RS : N_RS;
     if (threadIdx.x < PAIRS * 4)
         reinterpret_cast<uint32_t*>(lds + NET + NET_S + (threadIdx.x >> 2) * PSCR + P_FLAGS)[threadIdx.x & 3] = 0u;
@@ -885,6 +965,8 @@ struct ReduceArgs {
     int hist_len;
     int reduce, adam, bump;
     float lr, b1, b2, eps;
+    float* simg;       // student LDS image, refreshed with every updated parameter
+    int bf16;
 };
 
 constexpr int RED_COLS = 64;                        // params per reduce block
@@ -936,7 +1018,9 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
             v += (g * g - v) * (1.0f - a.b2);
             a.m[p] = m;
             a.v[p] = v;
-            a.params[p] -= (m * alpha) / (sqrtf(v) + a.eps);
+            const float w = a.params[p] - (m * alpha) / (sqrtf(v) + a.eps);
+            a.params[p] = w;
+            pack_param(a.simg, p, w, true, a.bf16 != 0);
         }
     }
     if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1027,6 +1111,8 @@ struct rdd_trainer {
     float* state = nullptr;    // [8][n]
     float* tnet = nullptr;     // [P + 22]
     float* snet = nullptr;     // [P + 22]
+    float* timg = nullptr;     // [NET]   teacher LDS image
+    float* simg = nullptr;     // [NET_S] student LDS image
     float* m = nullptr;
     float* v = nullptr;
     float* grad = nullptr;     // [P] (own or bound)
@@ -1045,6 +1131,8 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     RolloutArgs a;
     a.n = obs_in ? n_obs : t->cfg.n_envs;
     a.obs_in = obs_in;
+    a.timg = t->timg;
+    a.simg = t->simg;
     a.env_base = t->cfg.env_base;
     a.seed = t->cfg.seed;
     a.state = t->state;
@@ -1089,6 +1177,8 @@ int launch_reduce(rdd_trainer* t, int reduce, int adam, int bump) {
     a.b1 = t->cfg.beta1;
     a.b2 = t->cfg.beta2;
     a.eps = t->cfg.eps;
+    a.simg = t->simg;
+    a.bf16 = t->cfg.student_dtype == RDD_DTYPE_BF16;
     hipLaunchKernelGGL(reduce_adam_kernel, dim3(RED_GRID), dim3(RED_BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "reduce_adam_kernel launch");
     return RD_OK;
@@ -1136,6 +1226,8 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     alloc((void**)&t->state, sizeof(float) * 8 * cfg->n_envs);
     alloc((void**)&t->tnet, sizeof(float) * netf);
     alloc((void**)&t->snet, sizeof(float) * netf);
+    alloc((void**)&t->timg, sizeof(float) * NET);
+    alloc((void**)&t->simg, sizeof(float) * NET_S);
     alloc((void**)&t->m, sizeof(float) * P_TOT);
     alloc((void**)&t->v, sizeof(float) * P_TOT);
     alloc((void**)&t->own_grad, sizeof(float) * P_TOT);
@@ -1158,7 +1250,7 @@ int rdd_destroy(rdd_trainer* t) {
     if (!t) return RD_OK;
     rd::DeviceGuard g(t->device);
     for (void* p : {(void*)t->state, (void*)t->tnet, (void*)t->snet, (void*)t->m, (void*)t->v, (void*)t->own_grad,
-                    (void*)t->ws, (void*)t->hist, (void*)t->ctl, (void*)t->dbg})
+                    (void*)t->ws, (void*)t->hist, (void*)t->ctl, (void*)t->dbg, (void*)t->timg, (void*)t->simg})
         if (p) (void)hipFree(p);
     delete t;
     return RD_OK;
@@ -1172,6 +1264,11 @@ static int set_net(rdd_trainer* t, float* dst, const float* params, const float*
     RD_HIP(hipMemcpyAsync(dst, params, sizeof(float) * P_TOT, hipMemcpyDeviceToDevice, t->stream), what);
     RD_HIP(hipMemcpyAsync(dst + P_TOT, mu, sizeof(float) * OBD, hipMemcpyDeviceToDevice, t->stream), what);
     RD_HIP(hipMemcpyAsync(dst + P_TOT + OBD, sd, sizeof(float) * OBD, hipMemcpyDeviceToDevice, t->stream), what);
+    const bool student = dst == t->snet;
+    const bool bf16 = student && t->cfg.student_dtype == RDD_DTYPE_BF16;
+    hipLaunchKernelGGL(pack_net_kernel, dim3(1), dim3(256), 0, t->stream, dst, student ? t->simg : t->timg,
+                       student ? NET_S : NET, student ? 1 : 0, bf16 ? 1 : 0);
+    RD_HIP(hipGetLastError(), what);
     return RD_OK;
 }
 
