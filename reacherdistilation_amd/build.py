@@ -64,8 +64,18 @@ def build_stamps():
     return out
 
 
+def build_variant(name, *defines):
+    """Diagnostic/ablation build (e.g. RD_ABL_TANH) as libreacher_<name>.so; never the product."""
+    out = os.path.join(HERE, f"libreacher_{name}.so")
+    subprocess.check_call([HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-o", out, *sources()])
+    return out
+
+
 if __name__ == "__main__":
-    if "--usage" in sys.argv:
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        build_variant(sys.argv[i + 1], *sys.argv[i + 2:])
+    elif "--usage" in sys.argv:
         resource_usage()
     elif "--stamps" in sys.argv:
         build_stamps()

@@ -119,7 +119,11 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // (The backward only needs tanh's output; W2^T for dH1 keeps the unscaled weights.)
 constexpr float kTanhScale = 2.8853900817779268f;
 __device__ __forceinline__ float tanh_pre(float y) {
+#ifdef RD_ABL_TANH   // ablation build: no transcendentals (timing only, wrong results)
+    return fminf(fmaxf(0.25f * y, -1.0f), 1.0f);
+#else
     return fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(y) + 1.0f), 1.0f);
+#endif
 }
 
 // The per-wave scratch is private to its wave: LDS instructions of one wave execute in
@@ -622,7 +626,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 } else {
                     rd::State st{};
                     if (i < a.n) load_state(a.state, a.n, (uint32_t)i, st);
-                    rd::observe(st, ob);
+                    rd::observe<false>(st, ob);
                 }
                 float* o = obs + lane * SOS;
                 st4(o, f32x4{ob[0], ob[1], ob[2], ob[3]});
@@ -888,7 +892,12 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             rd::State st{};
             if (valid) load_state(a.state, a.n, iu, st);
             const float act0 = act[lane * 2], act1 = act[lane * 2 + 1];
-            const float rew = rd::env_step(st, act0, act1);
+#ifdef RD_ABL_PHYSICS   // ablation build: no dynamics (timing only)
+            const float rew = act0 + act1;
+            st.q0 += 0.01f * act0;
+#else
+            const float rew = rd::env_step<false>(st, act0, act1);
+#endif
             // episode clock of this env (RDD_STAGGER_GROUP envs share an offset)
             const int64_t gid = a.env_base + i;
             const uint32_t u = C + (a.stagger ? (uint32_t)((gid / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);

@@ -41,12 +41,14 @@ struct State {
     float q0, q1, v0, v1, tx, ty, dx, dy;   // (dx,dy) = fingertip - target at the held kinematics
 };
 
-// sin and cos together for the joint angles (|x| < 8192 rad: the arm angle resets every 50
-// steps, |q| stays < ~30).  Cody-Waite reduction by pi/2 with a 3-part constant (fma, exact
-// k*C1) and Cephes' minimax polynomials on [-pi/4, pi/4]: <= 2 ulp, ~20 VALU instead of the
-// ~45 of the libm path.  Larger arguments take the libm path (never on the hot path).
+// sin and cos together for the joint angles.  Cody-Waite reduction by pi/2 with a 3-part
+// constant (fma, exact k*C1 for |x| < 8192 rad) and Cephes' minimax polynomials on
+// [-pi/4, pi/4]: <= 2 ulp, ~20 VALU instead of the ~45 of the libm path.  With kWideRange
+// larger arguments take the libm path; the fused rollout (kWideRange = false) only sees
+// angles of episodes at most 50 steps old (|q| < ~200 rad).
+template <bool kWideRange = true>
 __device__ __forceinline__ void sincos_acc(float x, float* s, float* c) {
-    if (__builtin_expect(fabsf(x) > 8192.0f, 0)) {
+    if (kWideRange && __builtin_expect(fabsf(x) > 8192.0f, 0)) {
         sincosf(x, s, c);
         return;
     }
@@ -92,24 +94,26 @@ __device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, fl
         const float y = x <= 0.5f ? 2.0f * x * x : 1.0f - 2.0f * (1.0f - x) * (1.0f - x);
         const float d = 0.9f + y * 0.05f;
         const float aref = -(float)kBref * (J * v1) - (float)kKref * d * dist;
-        const float R = (1.0f - d) / d * (float)kInvW0;
-        const float f = fmaxf(0.0f, (aref - J * a1) / (i22 + R));
+        const float R = (1.0f - d) * __builtin_amdgcn_rcpf(d) * (float)kInvW0;
+        const float f = fmaxf(0.0f, (aref - J * a1) * __builtin_amdgcn_rcpf(i22 + R));
         a0 += i12 * J * f;
         a1 += i22 * J * f;
     }
 }
 
+template <bool kWideRange = true>
 __device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, float c1, float& a0, float& a1) {
     float s, c;
-    sincos_acc(q1, &s, &c);
+    sincos_acc<kWideRange>(q1, &s, &c);
     qacc_sc(q1, s, c, v0, v1, c0, c1, a0, a1);
 }
 
 // env.step on one env: returns the reward (computed from the held stale fingertip,
 // float32 ctrl cost of the UNCLIPPED action), advances the state by 2 RK4 substeps.
+template <bool kWideRange = true>
 __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
     const float h = 0.01f;
-    const float r = -sqrtf(st.dx * st.dx + st.dy * st.dy) - (a0 * a0 + a1 * a1);
+    const float r = -__builtin_amdgcn_sqrtf(st.dx * st.dx + st.dy * st.dy) - (a0 * a0 + a1 * a1);   // 1 ulp
     const float c0 = fminf(fmaxf(a0, -1.0f), 1.0f);   // ctrlrange +-1 (ctrllimited)
     const float c1 = fminf(fmaxf(a1, -1.0f), 1.0f);
     float q0 = st.q0, q1 = st.q1, v0 = st.v0, v1 = st.v1;
@@ -117,15 +121,15 @@ __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
         float k1a, k1b, k2a, k2b, k3a, k3b, k4a, k4b;
-        qacc(q1, v0, v1, c0, c1, k1a, k1b);
+        qacc<kWideRange>(q1, v0, v1, c0, c1, k1a, k1b);
         const float v0b = v0 + h * (0.5f * k1a), v1b = v1 + h * (0.5f * k1b);
-        qacc(q1 + h * (0.5f * v1), v0b, v1b, c0, c1, k2a, k2b);
+        qacc<kWideRange>(q1 + h * (0.5f * v1), v0b, v1b, c0, c1, k2a, k2b);
         const float v0c = v0 + h * (0.5f * k2a), v1c = v1 + h * (0.5f * k2b);
-        qacc(q1 + h * (0.5f * v1b), v0c, v1c, c0, c1, k3a, k3b);
+        qacc<kWideRange>(q1 + h * (0.5f * v1b), v0c, v1c, c0, c1, k3a, k3b);
         const float v0d = v0 + h * k3a, v1d = v1 + h * k3b;
         kq0 = q0 + h * v0c;
         kq1 = q1 + h * v1c;
-        sincos_acc(kq1, &s4, &c4);   // also the held kinematics' q1 after the 2nd substep
+        sincos_acc<kWideRange>(kq1, &s4, &c4);   // also the held kinematics' q1 after the 2nd substep
         qacc_sc(kq1, s4, c4, v0d, v1d, c0, c1, k4a, k4b);
         const float b1 = 1.0f / 6.0f, b2 = 1.0f / 3.0f;
         q0 += h * (v0 * b1 + v0b * b2 + v0c * b2 + v0d * b1);
@@ -134,7 +138,7 @@ __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
         v1 += h * (k1b * b1 + k2b * b2 + k3b * b2 + k4b * b1);
     }
     float s0, c0k;
-    sincos_acc(kq0, &s0, &c0k);
+    sincos_acc<kWideRange>(kq0, &s0, &c0k);
     const float s01 = __fmaf_rn(s0, c4, c0k * s4);    // sin(kq0 + kq1)
     const float c01 = __fmaf_rn(c0k, c4, -s0 * s4);   // cos(kq0 + kq1)
     st.q0 = q0; st.q1 = q1; st.v0 = v0; st.v1 = v1;
@@ -154,10 +158,11 @@ __device__ __forceinline__ void env_reset(State& st, const float* d /*q0 q1 v0 v
 }
 
 // gym ReacherEnv._get_obs: [cos q, sin q, target, qvel, fingertip - target (x,y,0)]
+template <bool kWideRange = true>
 __device__ __forceinline__ void observe(const State& st, float* ob) {
     float s0, c0, s1, c1;
-    sincos_acc(st.q0, &s0, &c0);
-    sincos_acc(st.q1, &s1, &c1);
+    sincos_acc<kWideRange>(st.q0, &s0, &c0);
+    sincos_acc<kWideRange>(st.q1, &s1, &c1);
     ob[0] = c0; ob[1] = c1; ob[2] = s0; ob[3] = s1;
     ob[4] = st.tx; ob[5] = st.ty; ob[6] = st.v0; ob[7] = st.v1;
     ob[8] = st.dx; ob[9] = st.dy; ob[10] = 0.0f;
