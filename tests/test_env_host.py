@@ -60,3 +60,14 @@ def test_bad_arguments_report_errors(lib):
     assert b"bad argument" in lib.rd_last_error()
     with pytest.raises(nat.NativeError):
         nat.check(rc, "rd_create")
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: pointing the loader at a missing build raises."""
+    import subprocess
+    import sys
+    code = ("import os; os.environ['RD_LIB']='libreacher_missing.so'\n"
+            "from reacherdistilation_amd import _native\n"
+            "try:\n    _native.load()\nexcept _native.NativeError as e:\n    print('raised', e)\n")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=120)
+    assert "raised" in out.stdout, out.stdout + out.stderr
