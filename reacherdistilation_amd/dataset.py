@@ -90,6 +90,16 @@ class DeviceDataset:
             yield (win[..., F_OB:F_REW].contiguous(), win[..., F_T:F_S].contiguous(),
                    prev[..., :PDFLAT_SHAPE].contiguous(), prev[..., PDFLAT_SHAPE:].contiguous())
 
+    def current_prev(self):
+        """(prev_pdflat [4], prev_rew [1]) of the record about to be written: the open
+        episode's last teacher pdflat and reward, zeros at t = 0 (reference dataset.py:
+        pdflat_at / rew_at of last_step(), as prev_pdflat_batch_array/prev_rew_batch_array
+        put them in the test batch's last row, :250-288)."""
+        if self.curr_len == 0:
+            return (torch.zeros(PDFLAT_SHAPE, device=self.device), torch.zeros(1, device=self.device))
+        r = self.curr[self.curr_len - 1]
+        return r[F_T:F_S].clone(), r[F_REW:F_REW + 1].clone()
+
     def test_batch(self, ob):
         """[T, B, 11]: batch column B-1 holds the window of the current episode ending at
         `ob` (its last T-1 observations, zero-padded at the front); the other columns are zero,

@@ -12,10 +12,15 @@ Phases as in the reference:
      (deterministic mean) action, record with 's', env.step with the student action; episode
      boundaries reset the env and flush the dataset; stop after ``episodes`` episodes.
 
-Fixes of the reference as committed: the student
-is the 2x64 MlpPolicy taking the observation (the committed graph's (10,20,.) vs (1,20,.)
-placeholder mismatch and its random-noise prev_pdflat/prev_rew inputs are not reproduced);
-every row of a [T, B] window is a training row; dropout keep_prob = 1.
+Students: ``student="policy"`` (default) is the 2x64 MlpPolicy taking the observation (the
+fused DistillTrainer path); ``student="mlp"`` is the reference's own ``student_mlp_graph``
+(student_nn.py:51-57) on rows ob | prev_pdflat | prev_rew (StudentMlpTrainer), trained on the
+recorded teacher pdflat with input dropout ``keep_prob`` (reference KEEP_PROB = 0.5).
+
+Fixes of the reference as committed: the committed
+graph's (10,20,.) vs (1,20,.) placeholder mismatch is not reproduced -- every row of a [T, B]
+window is a training row; prev_pdflat / prev_rew are the dataset's recorded fields, not the
+committed np.random.rand "TODO revert" stand-ins (mlp_train.py:151-158).
 """
 from __future__ import annotations
 
@@ -27,24 +32,35 @@ from .dataset import DeviceDataset
 from .distill import DistillConfig, DistillTrainer
 from .env import make_mujoco_env
 from .policy import TeacherAgent
+from .student_mlp import StudentMlpConfig, StudentMlpTrainer, rows
 
 
 def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPISODE_BUDGET,
           loss: str = "kl", lr: float = 1e-4, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
-          warmup_episodes: int = 2 * MLP_BATCH_SIZE, log=print):
-    """Returns (trainer, dataset, per-episode summed training loss)."""
+          warmup_episodes: int = 2 * MLP_BATCH_SIZE, student: str = "policy", keep_prob: float = 1.0,
+          log=print):
+    """Returns (trainer, dataset, per-episode summed training loss); the trainer is the
+    DistillTrainer (student="policy") or the StudentMlpTrainer (student="mlp")."""
+    if student not in ("policy", "mlp"):
+        raise ValueError(f"unknown student {student!r}")
     env = make_mujoco_env("Reacher-v2", seed, device=device)
     teacher = TeacherAgent(restore=restore, path=teacher_path)
     tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr), device=device, teacher=teacher.pi)
+    sm = StudentMlpTrainer(StudentMlpConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed),
+                           device=device) if student == "mlp" else None
     dataset = DeviceDataset(device=device, seed=seed)
     ob = env.reset()
     reward = 0.0
     losses = []
     if not train:
-        return tr, dataset, losses
+        return (sm or tr), dataset, losses
 
     def query(o):
         t, s = tr.forward(torch.as_tensor(np.asarray(o, np.float32)).view(1, OBSPACE_SHAPE))
+        if sm is not None:   # the reference student: row = ob | prev_pdflat | prev_rew
+            prev, prew = dataset.current_prev()
+            ob_t = torch.as_tensor(np.asarray(o, np.float32), device=prev.device).view(OBSPACE_SHAPE)
+            s = sm.forward(rows(ob_t, prev, prew))
         return t[0].cpu().numpy(), s[0].cpu().numpy()
 
     log("Begin Training! First Accumulate observation with teacher")
@@ -59,9 +75,13 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
 
     total_loss = 0.0
     while True:
-        for ob_batch, _t, _prev, _prew in dataset.training_batches():
-            tr.step_obs(ob_batch.reshape(-1, OBSPACE_SHAPE))
-            total_loss += float(tr.metrics(1)[0, 1])
+        for ob_batch, t_batch, prev_batch, prew_batch in dataset.training_batches():
+            if sm is not None:   # mlp_train.py:145-160 on the reference graph
+                sm.step(rows(ob_batch, prev_batch, prew_batch), t_batch.reshape(-1, 4))
+                total_loss += float(sm.metrics(1)[0, 0])
+            else:
+                tr.step_obs(ob_batch.reshape(-1, OBSPACE_SHAPE))
+                total_loss += float(tr.metrics(1)[0, 1])
         t_pdflat, s_pdflat = query(ob)
         dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, s_pdflat=s_pdflat, stepped_with="s")
         ob, reward, new, _ = env.step(s_pdflat[:2])
@@ -74,4 +94,4 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
             dataset.flush()
             if dataset.num_episodes() >= episodes:
                 break
-    return tr, dataset, losses
+    return (sm or tr), dataset, losses

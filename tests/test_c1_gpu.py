@@ -70,3 +70,15 @@ def test_reference_shaped_driver_runs():
     assert all(np.isfinite(losses))
     env_steps, opt_steps = tr.counters()
     assert env_steps == 0 and opt_steps == 2 * 50
+
+
+def test_reference_shaped_driver_with_the_reference_student():
+    """student="mlp": the reference's own student_mlp_graph on ob | prev_pdflat | prev_rew rows,
+    kl_loss on the recorded teacher pdflat, dropout keep_prob 0.5 (reference KEEP_PROB)."""
+    from reacherdistilation_amd import mlp_train
+    sm, ds, losses = mlp_train.train(episodes=4, warmup_episodes=2, loss="kl", lr=1e-3, student="mlp",
+                                     keep_prob=0.5, log=lambda *a: None)
+    assert ds.num_episodes() == 4 and len(losses) == 1 and np.isfinite(losses[0])
+    assert sm.counter() == 50
+    m = sm.metrics(50)
+    assert np.all(m[:, 2] == 200)   # one [10, 20] window = 200 rows per optimiser step

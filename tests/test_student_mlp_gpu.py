@@ -1,0 +1,147 @@
+"""GPU parity of the reference student (csrc/student_mlp.hip) against oracle/refnet_np.py.
+
+Tolerances: the kernel computes in f32 (exact f32 products, f32 sums in MFMA order) against
+the f64 oracle.  Forward: |err| <= 2e-5 + 1e-4 |ref|.  Gradient: relative L2 error < 2e-4
+and per-element |err| <= 1e-4 max|g| + 1e-6.  Adam step: parameters within 1e-6 + 1e-4
+|update| of the oracle's TF1 Adam fed the oracle gradient.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import policy_np as pn
+from oracle import refnet_np as rn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _batch(n, seed=0):
+    rs = np.random.RandomState(seed)
+    x = rs.uniform(-1, 1, (n, 16)).astype(np.float32)
+    t = np.concatenate([rs.uniform(-.5, .5, (n, 2)), rs.uniform(-1.0, -0.2, (n, 2))], 1).astype(np.float32)
+    return x, t
+
+
+def _params(seed=4):
+    p = rn.init(seed)
+    rs = np.random.RandomState(seed + 100)
+    for (_, bo, _, b) in rn.LAYOUT:
+        p[bo:bo + b] = rs.uniform(-.1, .1, b).astype(np.float32)
+    return p
+
+
+def _trainer(loss="kl", params=None, **kw):
+    from reacherdistilation_amd.student_mlp import StudentMlpConfig, StudentMlpTrainer
+    return StudentMlpTrainer(StudentMlpConfig(loss=loss, **kw), device=DEV,
+                             params=_params() if params is None else params)
+
+
+def _grad_check(g, want):
+    g = np.asarray(g, np.float64)
+    rel = np.linalg.norm(g - want) / np.linalg.norm(want)
+    assert rel < 2e-4, rel
+    assert np.abs(g - want).max() <= 1e-4 * np.abs(want).max() + 1e-6
+    return rel
+
+
+@pytest.mark.parametrize("n", [1, 17, 64, 65, 200, 1000, 4099])
+def test_forward_matches_oracle(n):
+    tr = _trainer()
+    x, _ = _batch(n, n)
+    got = tr.forward(torch.from_numpy(x)).cpu().numpy()
+    want = rn.forward(tr.params().cpu().numpy(), x)["pdflat"]
+    np.testing.assert_allclose(got, want, atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("loss", ["mse", "kl"])
+@pytest.mark.parametrize("n", [1, 20, 200, 1000, 20000])
+def test_gradient_and_metrics_match_oracle(loss, n):
+    tr = _trainer(loss)
+    x, t = _batch(n, 7 + n)
+    p = tr.params().cpu().numpy()
+    g = tr.rollout(torch.from_numpy(x), torch.from_numpy(t)).cpu().numpy()
+    fw = rn.forward(p, x)
+    lval, d, sq = rn.loss_and_dout(fw["pdflat"], t, loss, n)
+    _grad_check(g, rn.backward(p, fw, d))
+    tr.apply()
+    m = tr.metrics(1)[0]
+    assert abs(m[0] - lval) <= 1e-4 * abs(lval) + 1e-6 and abs(m[1] - sq) <= 1e-4 * sq + 1e-6 and m[2] == n
+
+
+def test_adam_step_matches_oracle():
+    tr = _trainer("kl", lr=1e-3)
+    x, t = _batch(300, 3)
+    p = tr.params().cpu().numpy().copy()
+    opt = pn.AdamTF1(rn.P_REF, lr=1e-3)
+    for k in range(3):
+        fw = rn.forward(p.astype(np.float64), x)
+        _, d, _ = rn.loss_and_dout(fw["pdflat"], t, "kl", 300)
+        g = rn.backward(p.astype(np.float64), fw, d)
+        before = p.copy()
+        p = opt.step(p, g)
+        tr.step(torch.from_numpy(x), torch.from_numpy(t))
+        got = tr.params().cpu().numpy()
+        np.testing.assert_allclose(got, p, atol=1e-6 + 1e-4 * np.abs(p - before).max())
+        p = got.copy()   # continue from the device's parameters (isolates each step)
+    assert tr.counter() == 3
+
+
+def test_dropout_matches_oracle_mask():
+    tr = _trainer("mse", keep_prob=0.5, seed=99)
+    x, t = _batch(500, 5)
+    p = tr.params().cpu().numpy()
+    for step in range(2):   # the mask is keyed by the optimiser step
+        g = tr.rollout(torch.from_numpy(x), torch.from_numpy(t)).cpu().numpy()
+        xd = rn.dropout(x, 0.5, seed=99, step=step)
+        fw = rn.forward(p, xd)
+        _, d, _ = rn.loss_and_dout(fw["pdflat"], t, "mse", 500)
+        _grad_check(g, rn.backward(p, fw, d))
+        tr.apply()
+        p = tr.params().cpu().numpy()
+
+
+def test_sharded_rows_sum_to_the_full_batch():
+    """Two trainers with contiguous halves (row_base) == one trainer on all rows (the
+    multi-GPU contract: all_reduce(SUM) of the shard gradients)."""
+    from reacherdistilation_amd.student_mlp import StudentMlpConfig, StudentMlpTrainer
+    x, t = _batch(1000, 9)
+    cfg = StudentMlpConfig(loss="mse", keep_prob=0.7, seed=5)
+    full = StudentMlpTrainer(cfg, device=DEV, params=_params()).rollout(torch.from_numpy(x), torch.from_numpy(t))
+    a = StudentMlpTrainer(cfg, device=DEV, params=_params(), row_base=0)
+    b = StudentMlpTrainer(cfg, device=DEV, params=_params(), row_base=600)
+    ga = a.rollout(torch.from_numpy(x[:600]), torch.from_numpy(t[:600]), n_global=1000).clone()
+    gb = b.rollout(torch.from_numpy(x[600:]), torch.from_numpy(t[600:]), n_global=1000).clone()
+    _grad_check((ga + gb).cpu().numpy(), full.cpu().numpy().astype(np.float64))
+
+
+def test_deterministic():
+    x, t = _batch(5000, 1)
+    g1 = _trainer().rollout(torch.from_numpy(x), torch.from_numpy(t)).clone()
+    g2 = _trainer().rollout(torch.from_numpy(x), torch.from_numpy(t)).clone()
+    assert torch.equal(g1, g2)
+
+
+def test_learns_a_fixed_teacher():
+    """KL to a fixed target policy falls by > 10x in 300 Adam steps (lr 1e-3)."""
+    teacher = rn.init(77)
+    x, _ = _batch(2000, 2)
+    t = rn.forward(teacher, x)["pdflat"].astype(np.float32)
+    tr = _trainer("kl", lr=1e-3)
+    xs, ts = torch.from_numpy(x).to(DEV), torch.from_numpy(t).to(DEV)
+    for _ in range(300):
+        tr.step(xs, ts)
+    m = tr.metrics(300)
+    assert np.all(np.isfinite(m[:, 0])) and m[-1, 0] < 0.1 * m[0, 0], (m[0, 0], m[-1, 0])
+
+
+def test_bad_arguments_raise():
+    from reacherdistilation_amd._native import NativeError
+    tr = _trainer()
+    with pytest.raises(ValueError):
+        tr.forward(torch.zeros(0, 16))
+    with pytest.raises(ValueError):
+        tr.rollout(torch.zeros(4, 16), torch.zeros(3, 4))
+    mis = torch.zeros(65, device=DEV)[1:].view(4, 16)   # 4-byte offset: not 16-B aligned
+    with pytest.raises(NativeError):
+        tr.rollout(mis, torch.zeros(4, 4, device=DEV))
