@@ -63,7 +63,27 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--accum", type=int, default=50,
+                    help="also time K env-steps per optimiser step (SURVEY §8d: K = 50 = one episode); 0 = skip")
     return ap.parse_args()
+
+
+def copy_bandwidth(dev, gib=1.0, iters=20):
+    """Measured device-to-device copy bandwidth (read + write bytes / s), the practical HBM
+    ceiling the roofline is also quoted against."""
+    import torch
+    n = int(gib * (1 << 30)) // 4
+    a = torch.empty(n, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        b.copy_(a)
+    e.record()
+    torch.cuda.synchronize(dev)
+    return 2 * 4 * n * iters / (s.elapsed_time(e) * 1e-3) / 1e9
 
 
 def cpu_baseline(workload, seconds, threads):
@@ -163,6 +183,35 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    replicas = tr.replicas_identical() if world > 1 else True   # SURVEY §8e checksum
+
+    accum = None
+    if args.accum > 1:   # secondary line: one optimiser step (+ all-reduce) per K env-steps
+        tk = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr,
+                                          student_dtype=sdt, accum_steps=args.accum),
+                            device=dev, rank=rank, world_size=world)
+        ksteps = 2 * args.accum
+        for _ in range(args.accum):
+            tk.step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(ksteps):
+            tk.step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        tt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        accum = {"accum_steps": args.accum, "steps": ksteps, "value": n * world * ksteps / float(tt.item()),
+                 "ms_per_step": float(tt.item()) * 1e3 / ksteps,
+                 "replicas_identical": tk.replicas_identical() if world > 1 else True}
+        tk.close()
+
     # student action-MSE vs teacher over the last steps (all ranks)
     met = tr.metrics(min(10, tr.counter()))
     mt = torch.tensor(met.sum(0), dtype=torch.float64, device=dev)
@@ -179,6 +228,7 @@ def main():
         if sdt == "bf16":   # mixed: the MFMA-time-weighted peak of f32 teacher + bf16 student FLOPs
             f_s = FLOP_PER_ENV_STEP - FLOP_TEACHER
             peak = FLOP_PER_ENV_STEP / (FLOP_TEACHER / PEAK_F32_TFLOPS + f_s / PEAK_BF16_TFLOPS)
+        copy_gbs = copy_bandwidth(dev)
         traffic = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}.json")
         if os.path.exists(pmc):
@@ -200,8 +250,12 @@ def main():
                          "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": traffic, "flop_per_env_step": FLOP_PER_ENV_STEP,
                          "launch_us": kern_ms * 1e3,
-                         "hbm_gbs_algorithmic": BYTES_PER_ENV_STEP * n / launch_s / 1e9},
+                         "hbm_gbs_algorithmic": BYTES_PER_ENV_STEP * n / launch_s / 1e9,
+                         "hbm_peak_gbs": PEAK_HBM_GBS, "hbm_copy_gbs_measured": copy_gbs},
+            "replicas_identical": replicas,
         }
+        if accum is not None:
+            out["accum"] = accum
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
         print(json.dumps(out), flush=True)

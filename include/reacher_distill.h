@@ -52,6 +52,9 @@ typedef struct {
                                    batch mixes all 50 episode phases (see below)          */
     int32_t student_dtype;   /* RDD_DTYPE_F32, or RDD_DTYPE_BF16 (BASELINE config 5: bf16
                                 student MLP; see below)                                  */
+    int32_t accum_steps;     /* K env steps (rollouts) per optimiser step; 0 or 1 = the
+                                reference's one Adam step per env step.  Scales the MSE
+                                normalisation to 1 / (K n_envs_global)                  */
 } rdd_config;
 
 /* Student precision.  RDD_DTYPE_F32: every product exact f32 (v_mfma_f32_16x16x4_f32).
@@ -90,7 +93,8 @@ int rdd_get_student(rdd_trainer* tr, float* params);
 int rdd_reset(rdd_trainer* tr);
 
 /* The step: rollout (env + teacher + student fwd/bwd + loss, per-workgroup gradient
- * partials) and reduction into rdd_grad_buffer(); rdd_apply(): TF1 Adam + counter++. */
+ * partials) and reduction into rdd_grad_buffer(), env-step counter++; rdd_apply(): TF1
+ * Adam, optimiser-step counter++. */
 int rdd_rollout(rdd_trainer* tr);
 int rdd_apply(rdd_trainer* tr);
 int rdd_step(rdd_trainer* tr);
@@ -104,14 +108,21 @@ int rdd_step(rdd_trainer* tr);
 int rdd_rollout_obs(rdd_trainer* tr, const float* obs, int64_t n, int64_t n_global);
 int rdd_step_obs(rdd_trainer* tr, const float* obs, int64_t n);
 
-/* The same work as individual launches (for per-kernel timing with events in between):
- * RDD_STAGE_ROLLOUT = the fused rollout kernel only; RDD_STAGE_REDUCE = partials -> grad;
- * RDD_STAGE_APPLY = Adam + counter; RDD_STAGE_REDUCE_APPLY = both in one launch.
- * rdd_step == ROLLOUT then REDUCE_APPLY. */
+/* The same work as individual launches (for per-kernel timing with events in between, and
+ * for accumulating several rollouts into one optimiser step):
+ * RDD_STAGE_ROLLOUT = the fused rollout kernel only; RDD_STAGE_REDUCE = partials -> grad
+ * (+ the env clock advances); RDD_STAGE_APPLY = Adam + optimiser step counter;
+ * RDD_STAGE_REDUCE_APPLY = both in one launch; RDD_STAGE_REDUCE_ACCUM(_APPLY) = as REDUCE
+ * (_APPLY) but grad and the step's metrics slot ADD this rollout's sums.
+ * rdd_step == ROLLOUT then REDUCE_APPLY.  One optimiser step per K env steps
+ * (rdd_config.accum_steps = K): ROLLOUT, REDUCE, then K-1 x (ROLLOUT, REDUCE_ACCUM), then
+ * APPLY (after the all-reduce when multi-GPU). */
 #define RDD_STAGE_ROLLOUT 1
 #define RDD_STAGE_REDUCE 2
 #define RDD_STAGE_APPLY 3
 #define RDD_STAGE_REDUCE_APPLY 4
+#define RDD_STAGE_REDUCE_ACCUM 5
+#define RDD_STAGE_REDUCE_ACCUM_APPLY 6
 int rdd_launch_stage(rdd_trainer* tr, int stage);
 float* rdd_grad_buffer(rdd_trainer* tr);   /* device [P], valid after rdd_rollout */
 /* Use a caller-owned device buffer [P] as the gradient buffer (e.g. a torch tensor that

@@ -972,7 +972,8 @@ struct ReduceArgs {
     uint32_t* ctl;
     float* hist;       // [hist_len][4]
     int hist_len;
-    int reduce, adam, bump;
+    int reduce, adam, accum;   // accum: grad (and the metrics slot) += this rollout's sums
+    int bump_env, bump_opt;    // advance the env clock (after a reduce) / the optimiser step
     float lr, b1, b2, eps;
     float* simg;       // student LDS image, refreshed with every updated parameter
     int bf16;
@@ -1014,8 +1015,13 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
 #pragma unroll
             for (int r = 0; r < RED_ROWS; ++r) q[r & 3] += part[r][col];
             g = (q[0] + q[1]) + (q[2] + q[3]);
-            if (p < P_TOT) a.grad[p] = g;
-            else a.hist[(int64_t)(S % (uint32_t)a.hist_len) * N_MET + (p - P_TOT)] = g;
+            if (p < P_TOT) {
+                if (a.accum) g += a.grad[p];
+                a.grad[p] = g;
+            } else {
+                float* h = a.hist + (int64_t)(S % (uint32_t)a.hist_len) * N_MET + (p - P_TOT);
+                *h = a.accum ? *h + g : g;
+            }
         } else {
             g = p < P_TOT ? a.grad[p] : 0.f;
         }
@@ -1032,11 +1038,13 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
             pack_param(a.simg, p, w, true, a.bf16 != 0);
         }
     }
-    if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) {
-        a.ctl[0] = C + a.ctl[12];   // env steps: only after a launch that stepped the envs
-        a.ctl[1] = S + 1u;          // optimiser steps
-        a.ctl[2] = __float_as_uint(b1p * a.b1);
-        a.ctl[3] = __float_as_uint(b2p * a.b2);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (a.bump_env) a.ctl[0] = C + a.ctl[12];   // env steps: only after a launch that stepped the envs
+        if (a.bump_opt) {
+            a.ctl[1] = S + 1u;                       // optimiser steps
+            a.ctl[2] = __float_as_uint(b1p * a.b1);
+            a.ctl[3] = __float_as_uint(b2p * a.b2);
+        }
     }
 }
 
@@ -1131,6 +1139,7 @@ struct rdd_trainer {
     uint32_t* ctl = nullptr;   // [16]: step words, snapshot, [8] hand-off timeout flag
     unsigned long long* dbg = nullptr;   // RD_STAMPS builds only
     int last_grid = 0;                   // workgroups of the last rollout (rows of ws to reduce)
+    int accum = 1;                       // rollouts per optimiser step (MSE normalisation)
 
 };
 
@@ -1153,7 +1162,8 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     a.act_student = t->cfg.act_with == RDD_ACT_STUDENT;
     a.stagger = t->cfg.stagger;
     a.dbg = t->dbg;
-    a.inv_n_global = 1.0f / (float)(obs_in ? n_obs_global : t->cfg.n_envs_global);
+    // MSE averages over the envs of all ranks and over the accum_steps rollouts of one optimiser step
+    a.inv_n_global = obs_in ? 1.0f / (float)n_obs_global : 1.0f / ((float)t->cfg.n_envs_global * (float)t->accum);
     int grid = t->grid;   // the workspace holds t->grid partial rows
     if (obs_in) {
         const int64_t want = ((n_obs + GROUP - 1) / GROUP + PAIRS - 1) / PAIRS;
@@ -1168,7 +1178,9 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     return RD_OK;
 }
 
-int launch_reduce(rdd_trainer* t, int reduce, int adam, int bump) {
+// reduce: partials -> grad (accum: +=) and advance the env clock; adam: TF1 Adam and
+// advance the optimiser step
+int launch_reduce(rdd_trainer* t, int reduce, int adam, int accum = 0) {
     ReduceArgs a;
     a.ws = t->ws;
     a.nblk = t->last_grid;
@@ -1181,7 +1193,9 @@ int launch_reduce(rdd_trainer* t, int reduce, int adam, int bump) {
     a.hist_len = t->cfg.metrics_len;
     a.reduce = reduce;
     a.adam = adam;
-    a.bump = bump;
+    a.accum = accum;
+    a.bump_env = reduce;
+    a.bump_opt = adam;
     a.lr = t->cfg.lr;
     a.b1 = t->cfg.beta1;
     a.b2 = t->cfg.beta2;
@@ -1211,7 +1225,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
         cfg->n_envs > ((int64_t)1 << 31) || (cfg->loss != RDD_LOSS_MSE && cfg->loss != RDD_LOSS_KL) ||
         (cfg->act_with != RDD_ACT_TEACHER && cfg->act_with != RDD_ACT_STUDENT) || !(cfg->lr > 0) ||
         cfg->grid < 0 || cfg->metrics_len < 0 || (cfg->stagger != 0 && cfg->stagger != 1) ||
-        (cfg->student_dtype != RDD_DTYPE_F32 && cfg->student_dtype != RDD_DTYPE_BF16))
+        (cfg->student_dtype != RDD_DTYPE_F32 && cfg->student_dtype != RDD_DTYPE_BF16) || cfg->accum_steps < 0)
         return rd::set_error(RD_EINVAL, "rdd_create: bad config");
     rd::DeviceGuard g(device);
     RD_HIP(g.err, "rdd_create: hipSetDevice");
@@ -1219,6 +1233,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     if (!t) return rd::set_error(RD_EINVAL, "rdd_create: out of host memory");
     t->cfg = *cfg;
     if (t->cfg.metrics_len == 0) t->cfg.metrics_len = 4096;
+    t->accum = cfg->accum_steps > 1 ? cfg->accum_steps : 1;
     t->device = device;
     t->stream = (hipStream_t)hip_stream;
     const int64_t ngroups = (cfg->n_envs + GROUP - 1) / GROUP;
@@ -1316,14 +1331,14 @@ int rdd_rollout(rdd_trainer* t) {
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_rollout: hipSetDevice");
     if (int rc = launch_rollout(t)) return rc;
-    return launch_reduce(t, 1, 0, 0);
+    return launch_reduce(t, 1, 0);
 }
 
 int rdd_apply(rdd_trainer* t) {
     if (!t) return rd::set_error(RD_EINVAL, "rdd_apply: null handle");
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_apply: hipSetDevice");
-    return launch_reduce(t, 0, 1, 1);
+    return launch_reduce(t, 0, 1);
 }
 
 int rdd_step(rdd_trainer* t) {
@@ -1331,7 +1346,7 @@ int rdd_step(rdd_trainer* t) {
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_step: hipSetDevice");
     if (int rc = launch_rollout(t)) return rc;
-    return launch_reduce(t, 1, 1, 1);
+    return launch_reduce(t, 1, 1);
 }
 
 int rdd_rollout_obs(rdd_trainer* t, const float* obs, int64_t n, int64_t n_global) {
@@ -1340,7 +1355,7 @@ int rdd_rollout_obs(rdd_trainer* t, const float* obs, int64_t n, int64_t n_globa
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_rollout_obs: hipSetDevice");
     if (int rc = launch_rollout(t, obs, n, n_global)) return rc;
-    return launch_reduce(t, 1, 0, 0);
+    return launch_reduce(t, 1, 0);
 }
 
 int rdd_step_obs(rdd_trainer* t, const float* obs, int64_t n) {
@@ -1348,7 +1363,7 @@ int rdd_step_obs(rdd_trainer* t, const float* obs, int64_t n) {
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_step_obs: hipSetDevice");
     if (int rc = launch_rollout(t, obs, n, n)) return rc;
-    return launch_reduce(t, 1, 1, 1);
+    return launch_reduce(t, 1, 1);
 }
 
 int rdd_launch_stage(rdd_trainer* t, int stage) {
@@ -1357,9 +1372,11 @@ int rdd_launch_stage(rdd_trainer* t, int stage) {
     RD_HIP(g.err, "rdd_launch_stage: hipSetDevice");
     switch (stage) {
         case RDD_STAGE_ROLLOUT: return launch_rollout(t);
-        case RDD_STAGE_REDUCE: return launch_reduce(t, 1, 0, 0);
-        case RDD_STAGE_APPLY: return launch_reduce(t, 0, 1, 1);
-        case RDD_STAGE_REDUCE_APPLY: return launch_reduce(t, 1, 1, 1);
+        case RDD_STAGE_REDUCE: return launch_reduce(t, 1, 0);
+        case RDD_STAGE_APPLY: return launch_reduce(t, 0, 1);
+        case RDD_STAGE_REDUCE_APPLY: return launch_reduce(t, 1, 1);
+        case RDD_STAGE_REDUCE_ACCUM: return launch_reduce(t, 1, 0, 1);
+        case RDD_STAGE_REDUCE_ACCUM_APPLY: return launch_reduce(t, 1, 1, 1);
         default: return rd::set_error(RD_EINVAL, "rdd_launch_stage: bad stage %d", stage);
     }
 }

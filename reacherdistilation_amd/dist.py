@@ -47,3 +47,25 @@ def allreduce_sum_(t, group=None):
     import torch.distributed as dist
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return t
+
+
+def checksum(t) -> int:
+    """Exact position-weighted checksum of a float32 tensor's bits (int64 arithmetic)."""
+    import torch
+    bits = t.detach().reshape(-1).contiguous().view(torch.int32).to(torch.int64)
+    w = torch.arange(1, bits.numel() + 1, dtype=torch.int64, device=bits.device)
+    return int(((bits & 0xFFFFFFFF) * w).sum().item())
+
+
+def replicas_identical(t, group=None) -> bool:
+    """True iff `t` is bitwise identical on every rank (MIN and MAX of the checksum agree)."""
+    import torch
+    import torch.distributed as dist
+    c = checksum(t)
+    if not dist.is_initialized():
+        return True
+    lo = torch.tensor([c], dtype=torch.int64, device=t.device)
+    hi = lo.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    return int(lo.item()) == int(hi.item())

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .dist import allreduce_sum_, shard
+from .dist import allreduce_sum_, replicas_identical, shard
 from .policy import P_TOT, MlpPolicyParams, student_init, synthetic_teacher
 
 P = nat.P
@@ -35,7 +35,7 @@ class RddConfig(ctypes.Structure):
     _fields_ = [("n_envs", I64), ("n_envs_global", I64), ("env_base", I64), ("seed", U64),
                 ("loss", I32), ("act_with", I32), ("lr", F32), ("beta1", F32), ("beta2", F32),
                 ("eps", F32), ("grid", I32), ("metrics_len", I32), ("stagger", I32),
-                ("student_dtype", I32)]
+                ("student_dtype", I32), ("accum_steps", I32)]
 
 
 nat.register({
@@ -81,6 +81,7 @@ class DistillConfig:
     metrics_len: int = 4096
     stagger: bool = True               # spread episode phases over the batch (reacher_distill.h)
     student_dtype: str = "f32"         # "f32" | "bf16" (BASELINE config 5: bf16 student MLP)
+    accum_steps: int = 1               # env steps per optimiser step (1 = the reference)
 
 
 class DistillTrainer:
@@ -104,7 +105,8 @@ class DistillTrainer:
         c = RddConfig(n_envs=self.n_local, n_envs_global=self.n_global, env_base=self.env_base,
                       seed=cfg.seed % 2 ** 64, loss=LOSSES[cfg.loss], act_with=ACTORS[cfg.act_with], lr=cfg.lr,
                       beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps, grid=cfg.grid, metrics_len=cfg.metrics_len,
-                      stagger=int(bool(cfg.stagger)), student_dtype=DTYPES[cfg.student_dtype])
+                      stagger=int(bool(cfg.stagger)), student_dtype=DTYPES[cfg.student_dtype],
+                      accum_steps=max(1, int(cfg.accum_steps)))
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             nat.check(self._lib.rdd_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,
@@ -120,6 +122,7 @@ class DistillTrainer:
         self._grad = torch.zeros(P_TOT, dtype=torch.float32, device=self.device)
         nat.check(self._lib.rdd_bind_grad_buffer(self._h, nat.ptr(self._grad)), "rdd_bind_grad_buffer")
         self.steps = 0
+        self._k = 0   # rollouts accumulated into the current optimiser step (accum_steps > 1)
 
     # -- parameters ------------------------------------------------------------------
     def set_teacher(self, p: MlpPolicyParams):
@@ -143,13 +146,29 @@ class DistillTrainer:
 
     # -- the step ----------------------------------------------------------------------
     def step(self):
-        """One rollout + distill step over this rank's envs (+ gradient all-reduce)."""
-        if self.world == 1:
-            nat.check(self._lib.rdd_step(self._h), "rdd_step")
+        """One env step of this rank's envs: rollout + distill.  With accum_steps = K the
+        gradients of K consecutive env steps are summed and one (all-reduce +) Adam step is
+        taken every K-th call."""
+        K = max(1, int(self.cfg.accum_steps))
+        if K == 1:
+            if self.world == 1:
+                nat.check(self._lib.rdd_step(self._h), "rdd_step")
+            else:
+                nat.check(self._lib.rdd_rollout(self._h), "rdd_rollout")
+                self.allreduce_grad()
+                nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
         else:
-            nat.check(self._lib.rdd_rollout(self._h), "rdd_rollout")
-            self.allreduce_grad()
-            nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
+            k = self._k
+            last = k == K - 1
+            self.launch(self.STAGE_ROLLOUT)
+            if last and self.world == 1:
+                self.launch(self.STAGE_REDUCE_ACCUM_APPLY if k else self.STAGE_REDUCE_APPLY)
+            else:
+                self.launch(self.STAGE_REDUCE_ACCUM if k else self.STAGE_REDUCE)
+                if last:
+                    self.allreduce_grad()
+                    self.launch(self.STAGE_APPLY)
+            self._k = 0 if last else k + 1
         self.steps += 1
 
     # -- observation-batch mode (the reference's dataset-window training) ---------------
@@ -195,14 +214,18 @@ class DistillTrainer:
         g = torch.cuda.CUDAGraph()
         prev = torch.cuda.current_stream(self.device)
         torch.cuda.synchronize(self.device)
+        if max(1, int(self.cfg.accum_steps)) > 1 and steps % self.cfg.accum_steps:
+            raise ValueError("capture whole optimiser steps: steps must be a multiple of accum_steps")
         with torch.cuda.graph(g):
             self.set_stream(torch.cuda.current_stream(self.device))
             for _ in range(steps):
-                nat.check(self._lib.rdd_step(self._h), "rdd_step")
+                self.step()
+        self.steps -= steps   # capture only records launches
         self.set_stream(prev)
         return g
 
     STAGE_ROLLOUT, STAGE_REDUCE, STAGE_APPLY, STAGE_REDUCE_APPLY = 1, 2, 3, 4
+    STAGE_REDUCE_ACCUM, STAGE_REDUCE_ACCUM_APPLY = 5, 6
 
     def launch(self, stage: int):
         nat.check(self._lib.rdd_launch_stage(self._h, stage), "rdd_launch_stage")
@@ -220,6 +243,11 @@ class DistillTrainer:
 
     def allreduce_grad(self):
         allreduce_sum_(self._grad, self.pg)
+
+    def replicas_identical(self) -> bool:
+        """student weights stay bit-identical across ranks (same init, same
+        all-reduced gradient); checked with an exact integer checksum (all ranks agree)."""
+        return replicas_identical(self.student_params(), self.pg)
 
     # -- queries -----------------------------------------------------------------------
     def forward(self, obs: torch.Tensor, teacher=True, student=True):

@@ -97,3 +97,26 @@ def test_two_rank_allreduce_equals_full_batch(oracle_c):
     n0 = shard(N_GLOBAL, 0, world)[0]
     np.testing.assert_allclose(np.concatenate([st0, st1], axis=1), state, atol=2e-5)
     assert st0.shape[1] == n0
+
+
+def _run_checksum(rank, world, port, out):
+    from reacherdistilation_amd.dist import checksum, replicas_identical
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    same = torch.arange(5060, dtype=torch.float32) * 1e-3
+    diff = same.clone()
+    if rank == 1:
+        diff[1234] = torch.nextafter(diff[1234], torch.tensor(1e9))   # one ulp on one rank
+    out[rank] = (replicas_identical(same), replicas_identical(diff), checksum(same))
+    dist.destroy_process_group()
+
+
+def test_replica_checksum_detects_one_ulp():
+    """student weights are asserted identical across ranks by a checksum."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_run_checksum, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r][0] is True and out[r][1] is False
+    assert out[0][2] == out[1][2]

@@ -57,6 +57,7 @@ def test_forward_matches_oracle(n):
 def _grad_check(tr, loss, act):
     st0 = tr.env_state().cpu().numpy()
     sp = tr.student_params().cpu().numpy()
+    c0 = tr.counter()   # env clock of this rollout (rdd_rollout advances it)
     tr.rollout()
     g = tr.grad().cpu().numpy()
     st1 = tr.env_state().cpu().numpy()
@@ -74,7 +75,7 @@ def _grad_check(tr, loss, act):
     rn_ob, _ = __import__("oracle.ref_c", fromlist=["x"]).step(ref, a, np.float64)
     n = st0.shape[1]
     off = (np.arange(n) // 32) % 50 if tr.cfg.stagger else np.zeros(n, np.int64)
-    reset = (tr.counter() + off) % 50 == 49
+    reset = (c0 + off) % 50 == 49
     near = (np.abs(st0[1]) > 2.8) | reset
     bad = ~np.isclose(st1.T, ref.T, atol=3e-4, rtol=1e-4).all(axis=1)
     assert not (bad & ~near).any()
@@ -258,3 +259,35 @@ def test_bf16_dagger_student_learns():
     m = tr.metrics(300)
     mse = m[:, 2] / (2 * m[:, 3])
     assert mse[-10:].mean() < 0.1 * mse[:10].mean(), (mse[:10].mean(), mse[-10:].mean())
+
+
+def test_accumulated_steps_sum_rollout_gradients():
+    """accum_steps = K: the gradient of one optimiser step is the sum of K rollouts' gradients
+    at frozen weights (KL: no normalisation, so bit-exact vs separate rollouts), the env clock
+    advances every rollout, and Adam runs once per K env steps."""
+    K = 3
+    a = _trainer(2048, loss="kl", accum_steps=K)
+    b = _trainer(2048, loss="kl")
+    gs = []
+    for k in range(K - 1):
+        a.step()
+        b.launch(b.STAGE_ROLLOUT)
+        b.launch(b.STAGE_REDUCE)
+        gs.append(b.grad().clone())
+    assert torch.equal(a.grad(), gs[0] + gs[1])
+    assert a.counters() == (K - 1, 0) and torch.equal(a.env_state(), b.env_state())
+    p0 = a.student_params().clone()
+    a.step()
+    assert a.counters() == (K, 1) and not torch.equal(a.student_params(), p0)
+    m = a.metrics(1)[0]
+    assert m[3] == K * 2048   # the step's metrics slot sums its K rollouts
+
+
+def test_accumulated_mse_normalises_over_k_rollouts():
+    K = 2
+    a = _trainer(1024, loss="mse", accum_steps=K)
+    b = _trainer(1024, loss="mse")
+    a.step()
+    b.launch(b.STAGE_ROLLOUT)
+    b.launch(b.STAGE_REDUCE)
+    torch.testing.assert_close(a.grad() * K, b.grad(), rtol=1e-6, atol=1e-9)
