@@ -1,0 +1,87 @@
+/* reacher_student_lstm.h -- C ABI of the reference's LSTM student: forward over unrolled
+ * windows and one truncated-BPTT distillation training step (libreacher.so).
+ *
+ * Graph: student_lstm_graph (reference src/distilation/student_nn.py:21-49), T unrolled steps
+ * (STEPS_UNROLLED = 10, config.py:25) over B windows (LSTM_BATCH_SIZE = 20, config.py:26):
+ *     p_t = dense(prev_pdflat_t, 32)                         linear
+ *     x_t = [dropout(ob_t)[11], p_t[32]]
+ *     (c_t, h_t) = LSTMCell(200)(x_t, (c_{t-1}, h_{t-1}))     TF1: gates i, j, f, o of
+ *                                                             [x_t, h_{t-1}] . Wl + bl,
+ *                                                             forget_bias 1, tanh
+ *     pdflat_t = dense(tanh dense 32(tanh dense 64(tanh dense 128(tanh dense 64(h_t))))), 4)
+ * Flat parameters (RDL_PARAMS = 227,012 floats) in variable-creation order, each kernel
+ * W[in][out] row-major then its bias:
+ *     Wp[4][32] bp | Wl[243][800] bl | W1[200][64] b1 | W2[64][128] b2 | W3[128][64] b3 |
+ *     W4[64][32] b4 | W5[32][4] b5
+ * Tensors: ob [T][B][11], prev_pdflat [T][B][4], t_pdflat / pdflat [T][B][4], LSTM state
+ * [2][B][200] = (c, m) as the reference's initial_state_batch_ph (lstm_train.py:51).
+ * Loss: kl_loss summed over T and B (loss.py:3-13), or action-MSE over T x rows_global.
+ * Optimiser: TF1 Adam (reference lr 1e-3, lstm_train.py:73-79).
+ *
+ * Conventions as in reacher.h: device pointers, asynchronous on the handle's stream,
+ * 0 = OK, RD_EINVAL, -(hipError_t).  Multi-GPU: windows sharded by the caller (row_base =
+ * this rank's first global window); rdl_rollout, all-reduce(SUM) rdl_grad_buffer(), rdl_apply.
+ */
+#ifndef REACHER_STUDENT_LSTM_H
+#define REACHER_STUDENT_LSTM_H
+#include <stdint.h>
+
+#include "reacher.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RDL_PARAMS 227012
+#define RDL_UNITS 200
+#define RDL_LOSS_MSE 0
+#define RDL_LOSS_KL 1
+
+typedef struct {
+    int32_t loss;                  /* RDL_LOSS_*                                             */
+    float lr, beta1, beta2, eps;   /* Adam (reference: 1e-3, .9, .999, 1e-8)                 */
+    int32_t steps;                 /* T, unrolled steps per window (reference 10)            */
+    int32_t max_windows;           /* capacity: largest B passed to any call                 */
+    int32_t metrics_len;           /* per-step metrics ring length; 0 = 4096                 */
+    float keep_prob;               /* dropout on ob while training (reference KEEP_PROB 0.5);
+                                      mask of ob[t][b][k] at optimiser step S: keep iff
+                                      u < keep_prob, u = word k%4 of Philox4x32-10(ctr =
+                                      {w lo, w hi, S, 4t + k/4}, key = seed), w = row_base + b */
+    uint64_t seed;
+    int64_t row_base;              /* global index of this rank's window 0                  */
+} rdl_config;
+
+typedef struct rdl_trainer rdl_trainer;
+
+int rdl_param_count(void);
+/* the 'LSTM' scope: graph, kl_loss and Adam (lstm_train.py:35-79) */
+int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_stream);
+int rdl_destroy(rdl_trainer* t);
+int rdl_set_stream(rdl_trainer* t, void* hip_stream);
+/* initialisation / saver.restore (lstm_train.py:82-107): params [RDL_PARAMS] */
+int rdl_set_params(rdl_trainer* t, const float* params);
+int rdl_get_params(rdl_trainer* t, float* params);
+/* Adam slots, beta powers, step counter to zero (lstm_train.py:99) */
+int rdl_reset(rdl_trainer* t);
+/* sess.run((s_action, s_pdflat_slice, final_state)) (lstm_train.py:171-183), all T x B outputs:
+ * state0 may be null (zero state); state_out may be null */
+int rdl_forward(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* state0, int64_t windows,
+                float* pdflat, float* state_out);
+/* forward + loss + BPTT of B windows (of windows_global over all ranks) from state0 (null =
+ * zeros, as lstm_train.py:159): gradient into rdl_grad_buffer() */
+int rdl_rollout(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* t_pdflat,
+                const float* state0, int64_t windows, int64_t windows_global);
+int rdl_apply(rdl_trainer* t);
+/* sess.run([loss, minimize_adam]) (lstm_train.py:145-160) == rollout + apply */
+int rdl_step(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* t_pdflat,
+             const float* state0, int64_t windows);
+float* rdl_grad_buffer(rdl_trainer* t);
+int rdl_bind_grad_buffer(rdl_trainer* t, float* grad);
+int rdl_get_counter(rdl_trainer* t, int64_t* opt_steps);
+/* [count][4] = loss, sum |mu_s - mu_t|^2, rows (T x B), 0 */
+int rdl_read_metrics(rdl_trainer* t, int64_t count, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,166 @@
+"""ORACLE (test infrastructure only) -- numpy f64 restatement of the reference's LSTM student
+and its truncated-BPTT training step.
+
+  student_lstm_graph (reference student_nn.py:21-49), unrolled over T = STEPS_UNROLLED:
+      p_t = prev_pdflat_t . Wp + bp                              (dense 4 -> 32, linear)
+      x_t = [dropout(ob_t) (11), p_t (32)]                       (43)
+      z_t = [x_t, h_{t-1}] . Wl + bl  -> i, j, f, o              (TF1 LSTMCell, 200 units,
+      c_t = sig(f + 1) c_{t-1} + sig(i) tanh(j)                   forget_bias 1, no peepholes,
+      h_t = sig(o) tanh(c_t)                                      no projection)
+      y_t = dense(tanh dense 32 (tanh dense 64 (tanh dense 128 (tanh dense 64 (h_t))))) (4)
+  loss: kl_loss (loss.py:3-13, summed over T and B) or MSE; Adam lr 1e-3 (lstm_train.py:75-80).
+  Flat parameters in the variables' creation order (lstm_train.py:53 builds the graph):
+      Wp[4][32] bp[32] | Wl[243][800] bl[800] | W1[200][64] b1 | W2[64][128] b2 |
+      W3[128][64] b3 | W4[64][32] b4 | W5[32][4] b5          = 227,012 floats
+  Dropout mask on ob (tf.nn.dropout, keep_prob): Philox4x32-10 keyed like the MLP student's
+  (refnet_np.dropout) with counter word 3 = 4 t + q, so the oracle reproduces it exactly.
+
+Parity status: UNPINNED beyond the formulas (TensorFlow absent; no reference test covers the
+LSTM); checked by finite differences in tests/test_lstm_oracle.py.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle.refnet_np import M32, philox4x32_10
+
+UNITS = 200
+IN_X = 11 + 32
+HEAD = (UNITS, 64, 128, 64, 32, 4)
+
+
+def layout():
+    """name -> (offset, shape) in the flat vector."""
+    shapes = [("Wp", (4, 32)), ("bp", (32,)), ("Wl", (IN_X + UNITS, 4 * UNITS)), ("bl", (4 * UNITS,))]
+    for k, (a, b) in enumerate(zip(HEAD[:-1], HEAD[1:])):
+        shapes += [(f"W{k + 1}", (a, b)), (f"b{k + 1}", (b,))]
+    out, off = {}, 0
+    for name, shp in shapes:
+        out[name] = (off, shp)
+        off += int(np.prod(shp))
+    return out, off
+
+
+LAYOUT, P_LSTM = layout()   # 227,012
+
+
+def unpack(p):
+    p = np.asarray(p, np.float64)
+    return {k: p[o:o + int(np.prod(s))].reshape(s) for k, (o, s) in LAYOUT.items()}
+
+
+def init(seed=3):
+    """glorot_uniform kernels (tf.layers.dense / LSTMCell defaults), zero biases."""
+    rng = np.random.RandomState(seed)
+    p = np.zeros(P_LSTM, np.float32)
+    for k, (o, s) in LAYOUT.items():
+        if len(s) == 2:
+            lim = np.sqrt(6.0 / (s[0] + s[1]))
+            p[o:o + s[0] * s[1]] = rng.uniform(-lim, lim, s[0] * s[1]).astype(np.float32)
+    return p
+
+
+def dropout(ob, keep_prob, seed, step, row_base=0):
+    """ob [T, B, 11] f32 -> dropped f32 (mask word k%4 of Philox(ctr = {b lo, b hi, step,
+    4 t + k/4}, key = seed), keep iff u < keep_prob, kept values / keep_prob)."""
+    ob = np.array(ob, np.float32)
+    if keep_prob >= 1.0:
+        return ob
+    T, B, _ = ob.shape
+    rows = np.arange(B, dtype=np.uint64) + np.uint64(row_base)
+    kp = np.float32(keep_prob)
+    for t in range(T):
+        for q in range(3):
+            w = philox4x32_10([rows & M32, rows >> np.uint64(32), np.full(B, step, np.uint64),
+                               np.full(B, 4 * t + q, np.uint64)], seed & 0xFFFFFFFF, seed >> 32)
+            u = (w >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+            for k in range(4):
+                col = 4 * q + k
+                if col < 11:
+                    ob[t, :, col] = np.where(u[k] < kp, ob[t, :, col] / kp, np.float32(0.0))
+    return ob
+
+
+def sig(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def forward(p, ob, prev, state0=None):
+    """ob [T,B,11] (already dropped), prev [T,B,4] -> dict with pdflat [T,B,4] and caches."""
+    W = unpack(p)
+    ob = np.asarray(ob, np.float64)
+    prev = np.asarray(prev, np.float64)
+    T, B, _ = ob.shape
+    c = np.zeros((B, UNITS)) if state0 is None else np.asarray(state0[0], np.float64)
+    h = np.zeros((B, UNITS)) if state0 is None else np.asarray(state0[1], np.float64)
+    cache = dict(x=[], hprev=[], cprev=[], gi=[], gj=[], gf=[], go=[], c=[], h=[], acts=[])
+    ys = []
+    for t in range(T):
+        pt = prev[t] @ W["Wp"] + W["bp"]
+        x = np.concatenate([ob[t], pt], 1)
+        z = np.concatenate([x, h], 1) @ W["Wl"] + W["bl"]
+        i, j, f, o = np.split(z, 4, axis=1)
+        gi, gj, gf, go = sig(i), np.tanh(j), sig(f + 1.0), sig(o)
+        cache["x"].append(x); cache["hprev"].append(h); cache["cprev"].append(c)
+        c = gf * c + gi * gj
+        h = go * np.tanh(c)
+        for k, v in (("gi", gi), ("gj", gj), ("gf", gf), ("go", go), ("c", c), ("h", h)):
+            cache[k].append(v)
+        a = [h]
+        for k in range(1, 5):
+            a.append(np.tanh(a[-1] @ W[f"W{k}"] + W[f"b{k}"]))
+        ys.append(a[-1] @ W["W5"] + W["b5"])
+        cache["acts"].append(a)
+    return dict(pdflat=np.stack(ys), state=(c, h), cache=cache, prev=prev)
+
+
+def loss_and_dout(pdflat, t_pdflat, loss, n_global):
+    """Summed over T and B (KL) or MSE over n_global rows; pdflat [T,B,4]."""
+    from oracle.refnet_np import loss_and_dout as lo
+    T, B, _ = pdflat.shape
+    L, d, sq = lo(pdflat.reshape(T * B, 4), np.asarray(t_pdflat).reshape(T * B, 4), loss, n_global)
+    return L, d.reshape(T, B, 4), sq
+
+
+def backward(p, fw, dout):
+    W = unpack(p)
+    g = {k: np.zeros(s) for k, (_, s) in LAYOUT.items()}
+    C = fw["cache"]
+    T = len(C["x"])
+    B = dout.shape[1]
+    dh_next = np.zeros((B, UNITS))
+    dc_next = np.zeros((B, UNITS))
+    for t in range(T - 1, -1, -1):
+        a = C["acts"][t]
+        dz = dout[t]
+        g["W5"] += a[4].T @ dz
+        g["b5"] += dz.sum(0)
+        da = dz @ W["W5"].T
+        for k in range(4, 0, -1):
+            dz = da * (1 - a[k] ** 2)
+            g[f"W{k}"] += a[k - 1].T @ dz
+            g[f"b{k}"] += dz.sum(0)
+            da = dz @ W[f"W{k}"].T
+        dh = da + dh_next
+        gi, gj, gf, go, c = C["gi"][t], C["gj"][t], C["gf"][t], C["go"][t], C["c"][t]
+        tc = np.tanh(c)
+        dc = dh * go * (1 - tc ** 2) + dc_next
+        dzo = dh * tc * go * (1 - go)
+        dzi = dc * gj * gi * (1 - gi)
+        dzj = dc * gi * (1 - gj ** 2)
+        dzf = dc * C["cprev"][t] * gf * (1 - gf)
+        dc_next = dc * gf
+        dzl = np.concatenate([dzi, dzj, dzf, dzo], 1)
+        xin = np.concatenate([C["x"][t], C["hprev"][t]], 1)
+        g["Wl"] += xin.T @ dzl
+        g["bl"] += dzl.sum(0)
+        dxin = dzl @ W["Wl"].T
+        dh_next = dxin[:, IN_X:]
+        dp = dxin[:, 11:IN_X]
+        g["Wp"] += fw["prev"][t].T @ dp
+        g["bp"] += dp.sum(0)
+    return np.concatenate([g[k].ravel() for k in LAYOUT])
+
+
+def loss_fn(p, ob, prev, t_pdflat, loss, n_global):
+    return loss_and_dout(forward(p, ob, prev)["pdflat"], t_pdflat, loss, n_global)[0]

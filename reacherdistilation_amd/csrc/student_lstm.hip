@@ -1,0 +1,618 @@
+// The reference's LSTM student (include/reacher_student_lstm.h): forward over T unrolled
+// steps of B windows and one truncated-BPTT distillation step, for gfx950.
+//
+// Graph (reference student_nn.py:21-49): x_t = [dropout(ob_t), dense32(prev_pdflat_t)];
+// TF1 LSTMCell(200) (gates i, j, f, o; forget_bias 1); head 200-64-128-64-32-4 (tanh).
+//
+// MI355X mapping.  Rows = (t, window) pairs, t-major, so every per-step slice is contiguous.
+// All GEMM-shaped work runs on one MFMA GEMM (csrc/rd_gemm.h) with fused epilogues:
+//  * the input half of the gate GEMM, [x_t] . Wl[0:43], is ONE GEMM over all T x B rows
+//    (bias fused); only the recurrent half h_{t-1} . Wl[43:243] is per step (accumulating
+//    into the same gate buffer), followed by the elementwise cell kernel;
+//  * the head runs once over all T x B rows after the recurrence (bias + tanh fused);
+//  * backward: the head's data gradients fuse the tanh derivative of the stored activation
+//    into the GEMM epilogue; BPTT is per step (cell kernel, then dh_{t-1} = dz_t Wr^T); the
+//    LSTM weight gradients are two GEMMs over all T x B rows at the end ([x | h_prev]^T dz),
+//    split-K with a fixed-order reduction when the output tile grid is small;
+//  * bias gradients are deterministic two-level column sums; no atomics anywhere.
+// Activations of all steps stay resident in HBM (sized at create for max_windows).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <new>
+
+#include "../../include/reacher_student_lstm.h"
+#include "rd_common.h"
+#include "rd_gemm.h"
+#include "rd_physics.h"
+
+namespace {
+
+constexpr int U = RDL_UNITS;             // 200
+constexpr int G4 = 4 * U;                // 800 gates
+constexpr int XI = 11 + 32;              // 43 cell inputs
+constexpr int XLD = 44;                  // X row stride (16-B rows)
+constexpr int H1 = 64, H2 = 128, H3 = 64, H4 = 32;
+
+// flat parameter offsets (variable-creation order)
+constexpr int OFF_WP = 0;
+constexpr int OFF_BP = OFF_WP + 4 * 32;
+constexpr int OFF_WL = OFF_BP + 32;
+constexpr int OFF_BL = OFF_WL + (XI + U) * G4;
+constexpr int OFF_W1 = OFF_BL + G4;
+constexpr int OFF_B1 = OFF_W1 + U * H1;
+constexpr int OFF_W2 = OFF_B1 + H1;
+constexpr int OFF_B2 = OFF_W2 + H1 * H2;
+constexpr int OFF_W3 = OFF_B2 + H2;
+constexpr int OFF_B3 = OFF_W3 + H2 * H3;
+constexpr int OFF_W4 = OFF_B3 + H3;
+constexpr int OFF_B4 = OFF_W4 + H3 * H4;
+constexpr int OFF_W5 = OFF_B4 + H4;
+constexpr int OFF_B5 = OFF_W5 + H4 * 4;
+constexpr int P_LSTM = OFF_B5 + 4;
+static_assert(P_LSTM == RDL_PARAMS, "flat layout");
+static_assert(OFF_WL % 4 == 0 && OFF_W1 % 4 == 0 && OFF_W2 % 4 == 0 && OFF_W3 % 4 == 0 && OFF_W4 % 4 == 0 &&
+                  OFF_W5 % 4 == 0 && (OFF_WL + XI * G4) % 4 == 0,
+              "16-B aligned weight matrices");
+
+constexpr int N_MET = 4;
+constexpr int LOSS_BLOCK = 256;
+constexpr int COLSUM_CHUNK = 2048;        // rows per first-level column-sum block
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// X[r] = [dropout(ob[r]) (11) | prev[r] . Wp + bp (32) | 0]; r = t B + b
+__global__ __launch_bounds__(256) void inputs_kernel(const float* ob, const float* prev, const float* params,
+                                                     float* X, int64_t R, int64_t B, float keep_prob, uint64_t seed,
+                                                     int64_t row_base, const uint32_t* ctl) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= R * XLD) return;
+    const int64_t r = idx / XLD;
+    const int col = (int)(idx % XLD);
+    float v = 0.0f;
+    if (col < 11) {
+        v = ob[r * 11 + col];
+        if (keep_prob < 1.0f) {   // tf.nn.dropout (student_nn.py:24)
+            const int64_t t = r / B, b = r % B;
+            const uint64_t w = (uint64_t)(row_base + b);
+            uint32_t o[4];
+            rd::philox((uint32_t)w, (uint32_t)(w >> 32), ctl[0], (uint32_t)(4 * t + col / 4), (uint32_t)seed,
+                       (uint32_t)(seed >> 32), o);
+            v = rd::u01(o[col & 3]) < keep_prob ? v / keep_prob : 0.0f;
+        }
+    } else if (col < XI) {        // hid_prev_pdflat = dense(prev_pdflat, 32) (student_nn.py:26)
+        const int c = col - 11;
+        const float* p = prev + r * 4;
+        v = params[OFF_BP + c];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) v = fmaf(p[a], params[OFF_WP + a * 32 + c], v);
+    }
+    X[idx] = v;
+}
+
+// TF1 LSTMCell: z = [i | j | f | o]; c = sig(f + 1) c_prev + sig(i) tanh(j); h = sig(o) tanh(c)
+__global__ __launch_bounds__(256) void cell_fwd_kernel(const float* Z, const float* c_prev, float* G, float* c_out,
+                                                       float* h_out, int64_t B) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= B * U) return;
+    const int64_t b = idx / U;
+    const int u = (int)(idx % U);
+    const float* z = Z + b * G4;
+    const float gi = sigm(z[u]), gj = tanhf(z[U + u]), gf = sigm(z[2 * U + u] + 1.0f), go = sigm(z[3 * U + u]);
+    const float c = fmaf(gf, c_prev[idx], gi * gj);
+    float* g = G + b * G4;
+    g[u] = gi; g[U + u] = gj; g[2 * U + u] = gf; g[3 * U + u] = go;
+    c_out[idx] = c;
+    h_out[idx] = go * tanhf(c);
+}
+
+// BPTT through one cell: dh = dh_head + dh_next; dc carried in place
+__global__ __launch_bounds__(256) void cell_bwd_kernel(const float* dh_head, const float* dh_next, int add_next,
+                                                       const float* G, const float* c_t, const float* c_prev,
+                                                       float* dc, float* dZ, int64_t B) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= B * U) return;
+    const int64_t b = idx / U;
+    const int u = (int)(idx % U);
+    const float* g = G + b * G4;
+    const float gi = g[u], gj = g[U + u], gf = g[2 * U + u], go = g[3 * U + u];
+    const float dh = add_next ? dh_head[idx] + dh_next[idx] : dh_head[idx];
+    const float tc = tanhf(c_t[idx]);
+    const float dcv = fmaf(dh * go, fmaf(-tc, tc, 1.0f), dc[idx]);
+    float* dz = dZ + b * G4;
+    dz[u] = dcv * gj * gi * (1.0f - gi);
+    dz[U + u] = dcv * gi * fmaf(-gj, gj, 1.0f);
+    dz[2 * U + u] = dcv * c_prev[idx] * gf * (1.0f - gf);
+    dz[3 * U + u] = dh * tc * go * (1.0f - go);
+    dc[idx] = dcv * gf;
+}
+
+// loss (reference loss.py:3-13 / action-MSE) and dY; per-block partials (fixed-order tree)
+__global__ __launch_bounds__(LOSS_BLOCK) void loss_kernel(const float* Y, const float* tgt, float* dY, int64_t R,
+                                                          int loss, float inv_n, float* part) {
+    __shared__ float sl[LOSS_BLOCK], ss[LOSS_BLOCK];
+    const int64_t r = (int64_t)blockIdx.x * LOSS_BLOCK + threadIdx.x;
+    float lv = 0.f, sq = 0.f;
+    if (r < R) {
+        const float* o = Y + r * 4;
+        const float* t = tgt + r * 4;
+        const float e0 = o[0] - t[0], e1 = o[1] - t[1];
+        sq = fmaf(e0, e0, e1 * e1);
+        float d0, d1, d2 = 0.f, d3 = 0.f;
+        if (loss == RDL_LOSS_MSE) {
+            d0 = e0 * inv_n;
+            d1 = e1 * inv_n;
+            lv = 0.5f * inv_n * sq;
+        } else {
+            const float ivt0 = expf(-2.0f * t[2]), ivt1 = expf(-2.0f * t[3]);
+            const float vs0 = expf(2.0f * o[2]), vs1 = expf(2.0f * o[3]);
+            lv = ((t[2] - o[2]) + 0.5f * (vs0 + e0 * e0) * ivt0 - 0.5f) +
+                 ((t[3] - o[3]) + 0.5f * (vs1 + e1 * e1) * ivt1 - 0.5f);
+            d0 = e0 * ivt0;
+            d1 = e1 * ivt1;
+            d2 = fmaf(vs0, ivt0, -1.0f);
+            d3 = fmaf(vs1, ivt1, -1.0f);
+        }
+        float* d = dY + r * 4;
+        d[0] = d0; d[1] = d1; d[2] = d2; d[3] = d3;
+    }
+    sl[threadIdx.x] = lv;
+    ss[threadIdx.x] = sq;
+    __syncthreads();
+    for (int s = LOSS_BLOCK / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            sl[threadIdx.x] += sl[threadIdx.x + s];
+            ss[threadIdx.x] += ss[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = sl[0];
+        part[2 * blockIdx.x + 1] = ss[0];
+    }
+}
+
+// metrics of this rollout into the ring slot of the current optimiser step; snapshot of the
+// step words for the Adam kernel (whose block 0 rewrites them)
+__global__ void metrics_kernel(const float* part, int nblk, float rows, uint32_t* ctl, float* hist, int hist_len) {
+    __shared__ float sl[256], ss[256];
+    float a = 0.f, b = 0.f;
+    for (int k = threadIdx.x; k < nblk; k += 256) {
+        a += part[2 * k];
+        b += part[2 * k + 1];
+    }
+    sl[threadIdx.x] = a;
+    ss[threadIdx.x] = b;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            sl[threadIdx.x] += sl[threadIdx.x + s];
+            ss[threadIdx.x] += ss[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        float* h = hist + (int64_t)(ctl[0] % (uint32_t)hist_len) * N_MET;
+        h[0] = sl[0];
+        h[1] = ss[0];
+        h[2] = rows;
+        h[3] = 0.f;
+    }
+    if (threadIdx.x < 4) ctl[4 + threadIdx.x] = ctl[threadIdx.x];
+}
+
+// deterministic column sums: out[c] (+ blockIdx.y * ld_out) = sum over rows [y*chunk, ...)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* src, int64_t M, int N, int64_t ld, int64_t chunk,
+                                                     float* out, int64_t ld_out) {
+    __shared__ float s[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = min(M, r0 + chunk);
+    float a = 0.f;
+    if (c < N)
+        for (int64_t r = r0 + ph; r < r1; r += 4) a += src[r * ld + c];
+    s[ph][threadIdx.x & 63] = a;
+    __syncthreads();
+    if (ph == 0 && c < N) out[(int64_t)blockIdx.y * ld_out + c] = (s[0][threadIdx.x] + s[1][threadIdx.x]) +
+                                                                 (s[2][threadIdx.x] + s[3][threadIdx.x]);
+}
+
+struct AdamArgs {
+    const float* grad;
+    float* params;
+    float* m;
+    float* v;
+    uint32_t* ctl;
+    float lr, b1, b2, eps;
+};
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t S = a.ctl[4];
+    const float b1p = __uint_as_float(a.ctl[5]), b2p = __uint_as_float(a.ctl[6]);
+    if (p < P_LSTM) {   // TF1 ApplyAdam (lstm_train.py:73-79)
+        const float g = a.grad[p];
+        const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+        float m = a.m[p], v = a.v[p];
+        m += (g - m) * (1.0f - a.b1);
+        v += (g * g - v) * (1.0f - a.b2);
+        a.m[p] = m;
+        a.v[p] = v;
+        a.params[p] -= (m * alpha) / (sqrtf(v) + a.eps);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ctl[0] = S + 1u;
+        a.ctl[1] = __float_as_uint(b1p * a.b1);
+        a.ctl[2] = __float_as_uint(b2p * a.b2);
+    }
+}
+
+__global__ void init_ctl_kernel(uint32_t* ctl, float b1, float b2) {
+    if (threadIdx.x < 2) {
+        const int o = 4 * threadIdx.x;
+        ctl[o] = 0u; ctl[o + 1] = __float_as_uint(b1); ctl[o + 2] = __float_as_uint(b2); ctl[o + 3] = 0u;
+    }
+}
+
+int cu_count(int device) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 256;
+    return prop.multiProcessorCount;
+}
+
+constexpr int64_t SPLIT_FLOATS = 4 << 20;   // split-K partials (16 MB)
+
+}  // namespace
+
+struct rdl_trainer {
+    rdl_config cfg{};
+    int device = 0, cus = 256;
+    hipStream_t stream = nullptr;
+    int T = 0;
+    int64_t Bmax = 0;
+    float *params = nullptr, *m = nullptr, *v = nullptr, *grad = nullptr, *own_grad = nullptr;
+    float *X = nullptr, *H = nullptr, *Cs = nullptr, *Z = nullptr, *G = nullptr;
+    float *A1 = nullptr, *A2 = nullptr, *A3 = nullptr, *A4 = nullptr, *Y = nullptr, *dY = nullptr;
+    float *D32 = nullptr, *D64a = nullptr, *D128 = nullptr, *D64b = nullptr, *dHh = nullptr, *dP = nullptr;
+    float *dhn = nullptr, *dc = nullptr;
+    float *split = nullptr, *colws = nullptr, *lpart = nullptr, *hist = nullptr;
+    int64_t colws_floats = 0;
+    uint32_t* ctl = nullptr;
+};
+
+namespace {
+
+hipError_t mm(rdl_trainer* t, int M, int N, int K, const float* A, int64_t lda, int ta, const float* B, int64_t ldb,
+              int tb, float* C, int64_t ldc, const float* bias = nullptr, int epi = rdg::EPI_NONE,
+              const float* aux = nullptr, int64_t ldaux = 0, int accum = 0) {
+    rdg::GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.lda = lda; g.ta = ta;
+    g.B = B; g.ldb = ldb; g.tb = tb;
+    g.C = C; g.ldc = ldc;
+    g.bias = bias; g.epi = epi; g.aux = aux; g.ldaux = ldaux; g.accum = accum;
+    return rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus);
+}
+
+hipError_t colsum(rdl_trainer* t, const float* src, int64_t M, int N, int64_t ld, float* out) {
+    const unsigned gx = (unsigned)((N + 63) / 64);
+    if (M <= COLSUM_CHUNK) {
+        hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, t->stream, src, M, N, ld, (int64_t)COLSUM_CHUNK,
+                           out, (int64_t)0);
+        return hipGetLastError();
+    }
+    const int64_t nch = (M + COLSUM_CHUNK - 1) / COLSUM_CHUNK;
+    hipLaunchKernelGGL(colsum_kernel, dim3(gx, (unsigned)nch), dim3(256), 0, t->stream, src, M, N, ld,
+                       (int64_t)COLSUM_CHUNK, t->colws, (int64_t)N);
+    hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, t->stream, (const float*)t->colws, nch, N,
+                       (int64_t)N, nch, out, (int64_t)0);
+    return hipGetLastError();
+}
+
+#define RDL_CK(call, what) RD_HIP((call), what)
+
+// forward over all T steps of B windows.  out_pdflat: where the head's output goes (the
+// internal Y when training).
+int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float* state0, int64_t B, float* out_pdflat,
+                bool train) {
+    const int T = t->T;
+    const int64_t R = (int64_t)T * B;
+    const float* P = t->params;
+    hipLaunchKernelGGL(inputs_kernel, dim3((unsigned)((R * XLD + 255) / 256)), dim3(256), 0, t->stream, ob, prev, P,
+                       t->X, R, B, train ? t->cfg.keep_prob : 1.0f, t->cfg.seed, t->cfg.row_base,
+                       (const uint32_t*)t->ctl);
+    RDL_CK(hipGetLastError(), "rdl inputs_kernel");
+    if (state0) {
+        RDL_CK(hipMemcpyAsync(t->Cs, state0, sizeof(float) * B * U, hipMemcpyDeviceToDevice, t->stream), "rdl state");
+        RDL_CK(hipMemcpyAsync(t->H, state0 + B * U, sizeof(float) * B * U, hipMemcpyDeviceToDevice, t->stream),
+               "rdl state");
+    } else {
+        RDL_CK(hipMemsetAsync(t->Cs, 0, sizeof(float) * B * U, t->stream), "rdl state");
+        RDL_CK(hipMemsetAsync(t->H, 0, sizeof(float) * B * U, t->stream), "rdl state");
+    }
+    // input half of the gate pre-activations for all steps: Z = X[:, :43] Wl[0:43] + bl
+    RDL_CK(mm(t, (int)R, G4, XI, t->X, XLD, 0, P + OFF_WL, G4, 0, t->Z, G4, P + OFF_BL), "rdl gemm Zx");
+    const unsigned cb = (unsigned)((B * U + 255) / 256);
+    for (int s = 0; s < T; ++s) {
+        float* Zs = t->Z + (int64_t)s * B * G4;
+        RDL_CK(mm(t, (int)B, G4, U, t->H + (int64_t)s * B * U, U, 0, P + OFF_WL + XI * G4, G4, 0, Zs, G4, nullptr,
+                  rdg::EPI_NONE, nullptr, 0, 1),
+               "rdl gemm recurrent");
+        hipLaunchKernelGGL(cell_fwd_kernel, dim3(cb), dim3(256), 0, t->stream, (const float*)Zs,
+                           (const float*)(t->Cs + (int64_t)s * B * U), t->G + (int64_t)s * B * G4,
+                           t->Cs + (int64_t)(s + 1) * B * U, t->H + (int64_t)(s + 1) * B * U, B);
+        RDL_CK(hipGetLastError(), "rdl cell_fwd_kernel");
+    }
+    // head over all T x B rows (student_nn.py:42-46)
+    const float* Hc = t->H + B * U;
+    RDL_CK(mm(t, (int)R, H1, U, Hc, U, 0, P + OFF_W1, H1, 0, t->A1, H1, P + OFF_B1, rdg::EPI_TANH), "rdl head1");
+    RDL_CK(mm(t, (int)R, H2, H1, t->A1, H1, 0, P + OFF_W2, H2, 0, t->A2, H2, P + OFF_B2, rdg::EPI_TANH), "rdl head2");
+    RDL_CK(mm(t, (int)R, H3, H2, t->A2, H2, 0, P + OFF_W3, H3, 0, t->A3, H3, P + OFF_B3, rdg::EPI_TANH), "rdl head3");
+    RDL_CK(mm(t, (int)R, H4, H3, t->A3, H3, 0, P + OFF_W4, H4, 0, t->A4, H4, P + OFF_B4, rdg::EPI_TANH), "rdl head4");
+    RDL_CK(mm(t, (int)R, 4, H4, t->A4, H4, 0, P + OFF_W5, 4, 0, out_pdflat, 4, P + OFF_B5), "rdl head5");
+    return RD_OK;
+}
+
+int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B, int64_t B_global) {
+    const int T = t->T;
+    const int64_t R = (int64_t)T * B;
+    const int Ri = (int)R;
+    const float* P = t->params;
+    float* g = t->grad;
+    const int lblk = (int)((R + LOSS_BLOCK - 1) / LOSS_BLOCK);
+    hipLaunchKernelGGL(loss_kernel, dim3(lblk), dim3(LOSS_BLOCK), 0, t->stream, (const float*)t->Y, tgt, t->dY, R,
+                       t->cfg.loss, 1.0f / ((float)T * (float)B_global), t->lpart);
+    RDL_CK(hipGetLastError(), "rdl loss_kernel");
+    hipLaunchKernelGGL(metrics_kernel, dim3(1), dim3(256), 0, t->stream, (const float*)t->lpart, lblk, (float)R,
+                       t->ctl, t->hist, t->cfg.metrics_len);
+    RDL_CK(hipGetLastError(), "rdl metrics_kernel");
+    // head backward (weight gradients over all rows; data gradients with the tanh derivative fused)
+    RDL_CK(mm(t, H4, 4, Ri, t->A4, H4, 1, t->dY, 4, 0, g + OFF_W5, 4), "rdl dW5");
+    RDL_CK(colsum(t, t->dY, R, 4, 4, g + OFF_B5), "rdl db5");
+    RDL_CK(mm(t, Ri, H4, 4, t->dY, 4, 0, P + OFF_W5, 4, 1, t->D32, H4, nullptr, rdg::EPI_DTANH, t->A4, H4), "rdl dZ4");
+    RDL_CK(mm(t, H3, H4, Ri, t->A3, H3, 1, t->D32, H4, 0, g + OFF_W4, H4), "rdl dW4");
+    RDL_CK(colsum(t, t->D32, R, H4, H4, g + OFF_B4), "rdl db4");
+    RDL_CK(mm(t, Ri, H3, H4, t->D32, H4, 0, P + OFF_W4, H4, 1, t->D64a, H3, nullptr, rdg::EPI_DTANH, t->A3, H3),
+           "rdl dZ3");
+    RDL_CK(mm(t, H2, H3, Ri, t->A2, H2, 1, t->D64a, H3, 0, g + OFF_W3, H3), "rdl dW3");
+    RDL_CK(colsum(t, t->D64a, R, H3, H3, g + OFF_B3), "rdl db3");
+    RDL_CK(mm(t, Ri, H2, H3, t->D64a, H3, 0, P + OFF_W3, H3, 1, t->D128, H2, nullptr, rdg::EPI_DTANH, t->A2, H2),
+           "rdl dZ2");
+    RDL_CK(mm(t, H1, H2, Ri, t->A1, H1, 1, t->D128, H2, 0, g + OFF_W2, H2), "rdl dW2");
+    RDL_CK(colsum(t, t->D128, R, H2, H2, g + OFF_B2), "rdl db2");
+    RDL_CK(mm(t, Ri, H1, H2, t->D128, H2, 0, P + OFF_W2, H2, 1, t->D64b, H1, nullptr, rdg::EPI_DTANH, t->A1, H1),
+           "rdl dZ1");
+    const float* Hc = t->H + B * U;
+    RDL_CK(mm(t, U, H1, Ri, Hc, U, 1, t->D64b, H1, 0, g + OFF_W1, H1), "rdl dW1");
+    RDL_CK(colsum(t, t->D64b, R, H1, H1, g + OFF_B1), "rdl db1");
+    RDL_CK(mm(t, Ri, U, H1, t->D64b, H1, 0, P + OFF_W1, H1, 1, t->dHh, U), "rdl dHhead");
+    // BPTT (the gate buffer Z is reused for dz: the forward keeps activations in G)
+    float* dZl = t->Z;
+    RDL_CK(hipMemsetAsync(t->dc, 0, sizeof(float) * B * U, t->stream), "rdl bptt");
+    const unsigned cb = (unsigned)((B * U + 255) / 256);
+    for (int s = T - 1; s >= 0; --s) {
+        hipLaunchKernelGGL(cell_bwd_kernel, dim3(cb), dim3(256), 0, t->stream, (const float*)(t->dHh + (int64_t)s * B * U),
+                           (const float*)t->dhn, s < T - 1 ? 1 : 0, (const float*)(t->G + (int64_t)s * B * G4),
+                           (const float*)(t->Cs + (int64_t)(s + 1) * B * U), (const float*)(t->Cs + (int64_t)s * B * U),
+                           t->dc, dZl + (int64_t)s * B * G4, B);
+        RDL_CK(hipGetLastError(), "rdl cell_bwd_kernel");
+        if (s > 0)   // dh_{s-1} = dz_s . Wr^T
+            RDL_CK(mm(t, (int)B, U, G4, dZl + (int64_t)s * B * G4, G4, 0, P + OFF_WL + XI * G4, G4, 1, t->dhn, U),
+                   "rdl gemm dh");
+    }
+    // LSTM weights: dWl = [x | h_prev]^T dz over all rows; dbl; then dp -> dWp, dbp
+    RDL_CK(mm(t, XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4), "rdl dWl x");
+    RDL_CK(mm(t, U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4), "rdl dWl h");
+    RDL_CK(colsum(t, dZl, R, G4, G4, g + OFF_BL), "rdl dbl");
+    RDL_CK(mm(t, Ri, 32, G4, dZl, G4, 0, P + OFF_WL + 11 * G4, G4, 1, t->dP, 32), "rdl dP");
+    RDL_CK(mm(t, 4, 32, Ri, prev, 4, 1, t->dP, 32, 0, g + OFF_WP, 32), "rdl dWp");
+    RDL_CK(colsum(t, t->dP, R, 32, 32, g + OFF_BP), "rdl dbp");
+    return RD_OK;
+}
+
+int launch_adam(rdl_trainer* t) {
+    AdamArgs a{t->grad, t->params, t->m, t->v, t->ctl, t->cfg.lr, t->cfg.beta1, t->cfg.beta2, t->cfg.eps};
+    hipLaunchKernelGGL(adam_kernel, dim3((P_LSTM + 255) / 256), dim3(256), 0, t->stream, a);
+    RD_HIP(hipGetLastError(), "rdl adam_kernel");
+    return RD_OK;
+}
+
+bool bad_windows(const rdl_trainer* t, int64_t B) { return B <= 0 || B > t->Bmax; }
+
+}  // namespace
+
+extern "C" {
+
+int rdl_param_count(void) { return P_LSTM; }
+
+int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_stream) {
+    if (!out || !cfg) return rd::set_error(RD_EINVAL, "rdl_create: null argument");
+    if ((cfg->loss != RDL_LOSS_MSE && cfg->loss != RDL_LOSS_KL) || !(cfg->lr > 0) || cfg->steps <= 0 ||
+        cfg->max_windows <= 0 || (int64_t)cfg->steps * cfg->max_windows > ((int64_t)1 << 22) || cfg->metrics_len < 0 ||
+        !(cfg->keep_prob > 0.0f && cfg->keep_prob <= 1.0f) || cfg->row_base < 0)
+        return rd::set_error(RD_EINVAL, "rdl_create: bad config");
+    rd::DeviceGuard dg(device);
+    RD_HIP(dg.err, "rdl_create: hipSetDevice");
+    rdl_trainer* t = new (std::nothrow) rdl_trainer();
+    if (!t) return rd::set_error(RD_EINVAL, "rdl_create: out of host memory");
+    t->cfg = *cfg;
+    if (t->cfg.metrics_len == 0) t->cfg.metrics_len = 4096;
+    t->device = device;
+    t->cus = cu_count(device);
+    t->stream = (hipStream_t)hip_stream;
+    t->T = cfg->steps;
+    t->Bmax = cfg->max_windows;
+    const int64_t R = (int64_t)t->T * t->Bmax, B = t->Bmax;
+    const int64_t nch = (R + COLSUM_CHUNK - 1) / COLSUM_CHUNK;
+    t->colws_floats = nch * G4;
+    hipError_t e = hipSuccess;
+    auto alloc = [&](float** p, int64_t floats) {
+        if (e == hipSuccess) e = hipMalloc((void**)p, sizeof(float) * (size_t)floats);
+        if (e == hipSuccess) e = hipMemsetAsync(*p, 0, sizeof(float) * (size_t)floats, t->stream);
+    };
+    alloc(&t->params, P_LSTM);
+    alloc(&t->m, P_LSTM);
+    alloc(&t->v, P_LSTM);
+    alloc(&t->own_grad, P_LSTM);
+    alloc(&t->X, R * XLD);
+    alloc(&t->H, (R + B) * U);
+    alloc(&t->Cs, (R + B) * U);
+    alloc(&t->Z, R * G4);
+    alloc(&t->G, R * G4);
+    alloc(&t->A1, R * H1);
+    alloc(&t->A2, R * H2);
+    alloc(&t->A3, R * H3);
+    alloc(&t->A4, R * H4);
+    alloc(&t->Y, R * 4);
+    alloc(&t->dY, R * 4);
+    alloc(&t->D32, R * H4);
+    alloc(&t->D64a, R * H3);
+    alloc(&t->D128, R * H2);
+    alloc(&t->D64b, R * H1);
+    alloc(&t->dHh, R * U);
+    alloc(&t->dP, R * 32);
+    alloc(&t->dhn, B * U);
+    alloc(&t->dc, B * U);
+    alloc(&t->split, SPLIT_FLOATS);
+    alloc(&t->colws, t->colws_floats);
+    alloc(&t->lpart, 2 * ((R + LOSS_BLOCK - 1) / LOSS_BLOCK));
+    alloc(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
+    if (e == hipSuccess) e = hipMalloc((void**)&t->ctl, sizeof(uint32_t) * 8);
+    t->grad = t->own_grad;
+    if (e != hipSuccess) {
+        rdl_destroy(t);
+        return rd::hip_fail(e, "rdl_create: allocation");
+    }
+    if (int rc = rdl_reset(t)) {
+        rdl_destroy(t);
+        return rc;
+    }
+    *out = t;
+    return RD_OK;
+}
+
+int rdl_destroy(rdl_trainer* t) {
+    if (!t) return RD_OK;
+    rd::DeviceGuard dg(t->device);
+    float* bufs[] = {t->params, t->m, t->v, t->own_grad, t->X, t->H, t->Cs, t->Z, t->G, t->A1, t->A2, t->A3, t->A4,
+                     t->Y, t->dY, t->D32, t->D64a, t->D128, t->D64b, t->dHh, t->dP, t->dhn, t->dc, t->split,
+                     t->colws, t->lpart, t->hist};
+    for (float* p : bufs)
+        if (p) (void)hipFree(p);
+    if (t->ctl) (void)hipFree(t->ctl);
+    delete t;
+    return RD_OK;
+}
+
+int rdl_set_stream(rdl_trainer* t, void* hip_stream) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdl_set_stream: null handle");
+    t->stream = (hipStream_t)hip_stream;
+    return RD_OK;
+}
+
+int rdl_set_params(rdl_trainer* t, const float* params) {
+    if (!t || !params) return rd::set_error(RD_EINVAL, "rdl_set_params: null argument");
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(hipMemcpyAsync(t->params, params, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream),
+           "rdl_set_params");
+    return RD_OK;
+}
+
+int rdl_get_params(rdl_trainer* t, float* params) {
+    if (!t || !params) return rd::set_error(RD_EINVAL, "rdl_get_params: null argument");
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(hipMemcpyAsync(params, t->params, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream),
+           "rdl_get_params");
+    return RD_OK;
+}
+
+int rdl_reset(rdl_trainer* t) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdl_reset: null handle");
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(hipMemsetAsync(t->m, 0, sizeof(float) * P_LSTM, t->stream), "rdl_reset");
+    RD_HIP(hipMemsetAsync(t->v, 0, sizeof(float) * P_LSTM, t->stream), "rdl_reset");
+    hipLaunchKernelGGL(init_ctl_kernel, dim3(1), dim3(64), 0, t->stream, t->ctl, t->cfg.beta1, t->cfg.beta2);
+    RD_HIP(hipGetLastError(), "rdl_reset");
+    return RD_OK;
+}
+
+int rdl_forward(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* state0, int64_t windows,
+                float* pdflat, float* state_out) {
+    if (!t || !ob || !prev_pdflat || !pdflat || bad_windows(t, windows))
+        return rd::set_error(RD_EINVAL, "rdl_forward: bad argument");
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(dg.err, "rdl_forward");
+    if (int rc = run_forward(t, ob, prev_pdflat, state0, windows, pdflat, false)) return rc;
+    if (state_out) {
+        const int64_t last = (int64_t)t->T * windows * U;
+        RD_HIP(hipMemcpyAsync(state_out, t->Cs + last, sizeof(float) * windows * U, hipMemcpyDeviceToDevice,
+                              t->stream), "rdl_forward: state");
+        RD_HIP(hipMemcpyAsync(state_out + windows * U, t->H + last, sizeof(float) * windows * U,
+                              hipMemcpyDeviceToDevice, t->stream), "rdl_forward: state");
+    }
+    return RD_OK;
+}
+
+int rdl_rollout(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* t_pdflat,
+                const float* state0, int64_t windows, int64_t windows_global) {
+    if (!t || !ob || !prev_pdflat || !t_pdflat || bad_windows(t, windows) || windows_global < windows)
+        return rd::set_error(RD_EINVAL, "rdl_rollout: bad argument");
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(dg.err, "rdl_rollout");
+    if (int rc = run_forward(t, ob, prev_pdflat, state0, windows, t->Y, true)) return rc;
+    return run_backward(t, prev_pdflat, t_pdflat, windows, windows_global);
+}
+
+int rdl_apply(rdl_trainer* t) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdl_apply: null handle");
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(dg.err, "rdl_apply");
+    return launch_adam(t);
+}
+
+int rdl_step(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* t_pdflat, const float* state0,
+             int64_t windows) {
+    if (int rc = rdl_rollout(t, ob, prev_pdflat, t_pdflat, state0, windows, windows)) return rc;
+    return launch_adam(t);
+}
+
+float* rdl_grad_buffer(rdl_trainer* t) { return t ? t->grad : nullptr; }
+
+int rdl_bind_grad_buffer(rdl_trainer* t, float* grad) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdl_bind_grad_buffer: null handle");
+    t->grad = grad ? grad : t->own_grad;
+    return RD_OK;
+}
+
+int rdl_get_counter(rdl_trainer* t, int64_t* opt_steps) {
+    if (!t || !opt_steps) return rd::set_error(RD_EINVAL, "rdl_get_counter: null argument");
+    rd::DeviceGuard dg(t->device);
+    uint32_t c[8];
+    RD_HIP(hipMemcpyAsync(c, t->ctl, sizeof(c), hipMemcpyDeviceToHost, t->stream), "rdl_get_counter");
+    RD_HIP(hipStreamSynchronize(t->stream), "rdl_get_counter");
+    *opt_steps = c[0];
+    return RD_OK;
+}
+
+int rdl_read_metrics(rdl_trainer* t, int64_t count, double* out) {
+    if (!t || !out || count < 0) return rd::set_error(RD_EINVAL, "rdl_read_metrics: bad argument");
+    int64_t steps = 0;
+    if (int rc = rdl_get_counter(t, &steps)) return rc;
+    const int64_t Hn = t->cfg.metrics_len;
+    if (count > steps || count > Hn)
+        return rd::set_error(RD_EINVAL, "rdl_read_metrics: only %lld steps kept", (long long)(steps < Hn ? steps : Hn));
+    float* host = new (std::nothrow) float[(size_t)Hn * N_MET];
+    if (!host) return rd::set_error(RD_EINVAL, "rdl_read_metrics: out of host memory");
+    hipError_t e = hipMemcpy(host, t->hist, sizeof(float) * Hn * N_MET, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        delete[] host;
+        return rd::hip_fail(e, "rdl_read_metrics");
+    }
+    for (int64_t k = 0; k < count; ++k) {
+        const int64_t s = (steps - count + k) % Hn;
+        for (int j = 0; j < N_MET; ++j) out[k * N_MET + j] = host[s * N_MET + j];
+    }
+    delete[] host;
+    return RD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,217 @@
+"""Host layer of the reference's LSTM student (include/reacher_student_lstm.h).
+
+``StudentLstmTrainer`` is the 'LSTM' scope of the reference's lstm_train.py (:35-79): the
+graph ``student_lstm_graph`` (student_nn.py:21-49: dense prev-pdflat embedding, TF1
+LSTMCell(200), 200-64-128-64-32-4 head), ``kl_loss`` (loss.py:3-13) and TF1 Adam, run by
+csrc/student_lstm.hip.  Tensors are the reference's window layout: ob [T, B, 11],
+prev_pdflat [T, B, 4], t_pdflat / pdflat [T, B, 4], state [2, B, 200] = (c, m).
+
+Multi-GPU: windows sharded contiguously (row_base = first global window), one
+all_reduce(SUM) of the flat 227,012-float gradient per optimiser step.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .config import LSTM_BATCH_SIZE, NUM_UNITS, OBSPACE_SHAPE, PDFLAT_SHAPE, STEPS_UNROLLED
+from .dist import allreduce_sum_
+
+P = nat.P
+I32, I64, U64, F32, INT = nat.I32, nat.I64, nat.U64, nat.F32, nat.INT
+
+HEAD = (NUM_UNITS, 64, 128, 64, 32, 4)
+SHAPES = [("Wp", (4, 32)), ("bp", (32,)), ("Wl", (OBSPACE_SHAPE + 32 + NUM_UNITS, 4 * NUM_UNITS)),
+          ("bl", (4 * NUM_UNITS,))] + [x for k, (a, b) in enumerate(zip(HEAD[:-1], HEAD[1:]))
+                                        for x in ((f"W{k + 1}", (a, b)), (f"b{k + 1}", (b,)))]
+N_PARAMS = sum(int(np.prod(s)) for _, s in SHAPES)   # 227,012
+LOSSES = {"mse": 0, "kl": 1}
+
+
+class RdlConfig(ctypes.Structure):
+    _fields_ = [("loss", I32), ("lr", F32), ("beta1", F32), ("beta2", F32), ("eps", F32), ("steps", I32),
+                ("max_windows", I32), ("metrics_len", I32), ("keep_prob", F32), ("seed", U64), ("row_base", I64)]
+
+
+nat.register({
+    "rdl_param_count": (INT, []),
+    "rdl_create": (INT, [ctypes.POINTER(P), ctypes.POINTER(RdlConfig), INT, P]),
+    "rdl_destroy": (INT, [P]),
+    "rdl_set_stream": (INT, [P, P]),
+    "rdl_set_params": (INT, [P, P]),
+    "rdl_get_params": (INT, [P, P]),
+    "rdl_reset": (INT, [P]),
+    "rdl_forward": (INT, [P, P, P, P, I64, P, P]),
+    "rdl_rollout": (INT, [P, P, P, P, P, I64, I64]),
+    "rdl_apply": (INT, [P]),
+    "rdl_step": (INT, [P, P, P, P, P, I64]),
+    "rdl_grad_buffer": (P, [P]),
+    "rdl_bind_grad_buffer": (INT, [P, P]),
+    "rdl_get_counter": (INT, [P, ctypes.POINTER(I64)]),
+    "rdl_read_metrics": (INT, [P, I64, P]),
+})
+
+
+def glorot_init(seed: int = 3) -> np.ndarray:
+    """glorot_uniform kernels (tf.layers.dense and LSTMCell defaults), zero biases."""
+    rng = np.random.RandomState(seed)
+    out = []
+    for _, s in SHAPES:
+        if len(s) == 2:
+            lim = math.sqrt(6.0 / (s[0] + s[1]))
+            out.append(rng.uniform(-lim, lim, s[0] * s[1]).astype(np.float32))
+        else:
+            out.append(np.zeros(s, np.float32))
+    return np.concatenate(out)
+
+
+@dataclass
+class StudentLstmConfig:
+    loss: str = "kl"                  # lstm_train.py:71
+    lr: float = 1e-3                  # lstm_train.py:74
+    beta1: float = 0.9
+    beta2: float = 0.999
+    eps: float = 1e-8
+    steps: int = STEPS_UNROLLED       # T
+    max_windows: int = LSTM_BATCH_SIZE
+    keep_prob: float = 1.0            # reference trains with KEEP_PROB = 0.5
+    seed: int = 0
+    init_seed: int = 3
+    metrics_len: int = 4096
+
+
+class StudentLstmTrainer:
+    def __init__(self, cfg: StudentLstmConfig | None = None, device="cuda:0", rank: int = 0, world_size: int = 1,
+                 process_group=None, params=None, row_base: int = 0):
+        self.cfg = cfg or StudentLstmConfig()
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("StudentLstmTrainer runs on a GPU (HIP) device only; there is no CPU path")
+        self.rank, self.world, self.pg = rank, world_size, process_group
+        self.T = int(self.cfg.steps)
+        self._lib = nat.load()
+        assert self._lib.rdl_param_count() == N_PARAMS
+        c = RdlConfig(loss=LOSSES[self.cfg.loss], lr=self.cfg.lr, beta1=self.cfg.beta1, beta2=self.cfg.beta2,
+                      eps=self.cfg.eps, steps=self.T, max_windows=int(self.cfg.max_windows),
+                      metrics_len=self.cfg.metrics_len, keep_prob=self.cfg.keep_prob,
+                      seed=self.cfg.seed % 2 ** 64, row_base=int(row_base))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            nat.check(self._lib.rdl_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,
+                                           nat.stream_handle(self.device)), "rdl_create")
+        self._h = h
+        self._grad = torch.zeros(N_PARAMS, dtype=torch.float32, device=self.device)
+        nat.check(self._lib.rdl_bind_grad_buffer(self._h, nat.ptr(self._grad)), "rdl_bind_grad_buffer")
+        self.set_params(glorot_init(self.cfg.init_seed) if params is None else params)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rdl_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _sync_stream(self):
+        nat.check(self._lib.rdl_set_stream(self._h, nat.stream_handle(self.device)), "rdl_set_stream")
+
+    # -- parameters ------------------------------------------------------------------
+    def set_params(self, params):
+        p = (params if torch.is_tensor(params) else torch.from_numpy(np.asarray(params, np.float32)))
+        p = p.to(self.device, torch.float32).reshape(-1).contiguous()
+        if p.numel() != N_PARAMS:
+            raise ValueError(f"expected {N_PARAMS} parameters, got {p.numel()}")
+        self._sync_stream()
+        nat.check(self._lib.rdl_set_params(self._h, nat.ptr(p)), "rdl_set_params")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def params(self) -> torch.Tensor:
+        out = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
+        self._sync_stream()
+        nat.check(self._lib.rdl_get_params(self._h, nat.ptr(out)), "rdl_get_params")
+        return out
+
+    def reset_optimizer(self):
+        self._sync_stream()
+        nat.check(self._lib.rdl_reset(self._h), "rdl_reset")
+
+    # -- compute -----------------------------------------------------------------------
+    def _t(self, x, last):
+        x = torch.as_tensor(x, dtype=torch.float32, device=self.device).contiguous()
+        if x.dim() != 3 or x.shape[0] != self.T or x.shape[2] != last:
+            raise ValueError(f"expected [T={self.T}, B, {last}], got {tuple(x.shape)}")
+        return x
+
+    def _windows(self, ob, prev, tgt=None, state0=None):
+        ob, prev = self._t(ob, OBSPACE_SHAPE), self._t(prev, PDFLAT_SHAPE)
+        B = ob.shape[1]
+        if B == 0 or prev.shape[1] != B or B > self.cfg.max_windows:
+            raise ValueError(f"bad window count {B} (max_windows {self.cfg.max_windows})")
+        if tgt is not None:
+            tgt = self._t(tgt, PDFLAT_SHAPE)
+            if tgt.shape[1] != B:
+                raise ValueError("t_pdflat window count differs")
+        if state0 is not None:
+            state0 = torch.as_tensor(state0, dtype=torch.float32, device=self.device).contiguous()
+            if tuple(state0.shape) != (2, B, NUM_UNITS):
+                raise ValueError(f"state must be [2, {B}, {NUM_UNITS}]")
+        return ob, prev, tgt, state0, B
+
+    def forward(self, ob, prev_pdflat, state0=None):
+        """(pdflat [T, B, 4], final state [2, B, 200]) with dropout off (lstm_train.py:171-183)."""
+        ob, prev, _, st, B = self._windows(ob, prev_pdflat, None, state0)
+        out = torch.empty(self.T, B, PDFLAT_SHAPE, dtype=torch.float32, device=self.device)
+        fin = torch.empty(2, B, NUM_UNITS, dtype=torch.float32, device=self.device)
+        self._sync_stream()
+        nat.check(self._lib.rdl_forward(self._h, nat.ptr(ob), nat.ptr(prev), nat.ptr(st) if st is not None else None,
+                                        B, nat.ptr(out), nat.ptr(fin)), "rdl_forward")
+        return out, fin
+
+    def rollout(self, ob, prev_pdflat, t_pdflat, state0=None, windows_global: int | None = None):
+        ob, prev, tgt, st, B = self._windows(ob, prev_pdflat, t_pdflat, state0)
+        self._sync_stream()
+        nat.check(self._lib.rdl_rollout(self._h, nat.ptr(ob), nat.ptr(prev), nat.ptr(tgt),
+                                        nat.ptr(st) if st is not None else None, B, int(windows_global or B)),
+                  "rdl_rollout")
+        self._keep = (ob, prev, tgt, st)
+        return self._grad
+
+    def apply(self):
+        self._sync_stream()
+        nat.check(self._lib.rdl_apply(self._h), "rdl_apply")
+
+    def step(self, ob, prev_pdflat, t_pdflat, state0=None, windows_global: int | None = None):
+        """sess.run([loss, minimize_adam]) (lstm_train.py:145-160)."""
+        if self.world == 1:
+            ob, prev, tgt, st, B = self._windows(ob, prev_pdflat, t_pdflat, state0)
+            self._sync_stream()
+            nat.check(self._lib.rdl_step(self._h, nat.ptr(ob), nat.ptr(prev), nat.ptr(tgt),
+                                         nat.ptr(st) if st is not None else None, B), "rdl_step")
+            self._keep = (ob, prev, tgt, st)
+            return
+        self.rollout(ob, prev_pdflat, t_pdflat, state0, windows_global)
+        allreduce_sum_(self._grad, self.pg)
+        self.apply()
+
+    def grad(self) -> torch.Tensor:
+        return self._grad
+
+    def counter(self) -> int:
+        v = ctypes.c_int64()
+        nat.check(self._lib.rdl_get_counter(self._h, ctypes.byref(v)), "rdl_get_counter")
+        return v.value
+
+    def metrics(self, count: int = 1) -> np.ndarray:
+        """[count, 4]: loss, sum |mu_s - mu_t|^2, rows (T x B), 0."""
+        out = np.zeros((count, 4), np.float64)
+        nat.check(self._lib.rdl_read_metrics(self._h, count, out.ctypes.data_as(ctypes.c_void_p)),
+                  "rdl_read_metrics")
+        return out

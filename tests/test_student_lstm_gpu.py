@@ -1,0 +1,174 @@
+"""GPU parity of the LSTM student (csrc/student_lstm.hip + csrc/rd_gemm.h) against
+oracle/lstm_np.py (f64).
+
+Tolerances (f32 kernels through T recurrent steps vs the f64 oracle): pdflat and final
+state |err| <= 5e-5 + 1e-4 |ref|; gradient relative L2 error < 5e-4 and per element
+<= 1e-3 max|g| + 1e-6; Adam step within 1e-6 + 1e-3 |update| where |g| > 1e-4 max|g|
+(elsewhere Adam's ~lr sign(g) step is bounded by 2 lr).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import lstm_np as ln
+from oracle import policy_np as pn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _batch(T, B, seed=0):
+    rs = np.random.RandomState(seed)
+    ob = rs.uniform(-1, 1, (T, B, 11)).astype(np.float32)
+    prev = np.concatenate([rs.uniform(-.5, .5, (T, B, 2)), rs.uniform(-1, 0, (T, B, 2))], 2).astype(np.float32)
+    t = np.concatenate([rs.uniform(-.5, .5, (T, B, 2)), rs.uniform(-1.0, -0.2, (T, B, 2))], 2).astype(np.float32)
+    return ob, prev, t
+
+
+def _params(seed=6):
+    p = ln.init(seed)
+    rs = np.random.RandomState(seed + 1)
+    for k, (o, s) in ln.LAYOUT.items():
+        if len(s) == 1:
+            p[o:o + s[0]] = rs.uniform(-.1, .1, s[0]).astype(np.float32)
+    return p
+
+
+def _trainer(T=10, B=20, loss="kl", params=None, **kw):
+    from reacherdistilation_amd.student_lstm import StudentLstmConfig, StudentLstmTrainer
+    return StudentLstmTrainer(StudentLstmConfig(loss=loss, steps=T, max_windows=B, **kw), device=DEV,
+                              params=_params() if params is None else params)
+
+
+def _t(x):
+    return torch.from_numpy(np.ascontiguousarray(x))
+
+
+def _grad_check(g, want):
+    g = np.asarray(g, np.float64)
+    rel = np.linalg.norm(g - want) / np.linalg.norm(want)
+    assert rel < 5e-4, rel
+    assert np.abs(g - want).max() <= 1e-3 * np.abs(want).max() + 1e-6
+    return rel
+
+
+@pytest.mark.parametrize("T,B,with_state", [(10, 1, False), (10, 20, False), (10, 20, True), (3, 130, True)])
+def test_forward_matches_oracle(T, B, with_state):
+    tr = _trainer(T, B)
+    ob, prev, _ = _batch(T, B, B)
+    st = None
+    if with_state:
+        rs = np.random.RandomState(5)
+        st = rs.uniform(-.5, .5, (2, B, 200)).astype(np.float32)
+    y, fin = tr.forward(_t(ob), _t(prev), None if st is None else _t(st))
+    want = ln.forward(tr.params().cpu().numpy(), ob, prev, st)
+    np.testing.assert_allclose(y.cpu().numpy(), want["pdflat"], atol=5e-5, rtol=1e-4)
+    np.testing.assert_allclose(fin[0].cpu().numpy(), want["state"][0], atol=5e-5, rtol=1e-4)
+    np.testing.assert_allclose(fin[1].cpu().numpy(), want["state"][1], atol=5e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("loss", ["mse", "kl"])
+@pytest.mark.parametrize("T,B", [(10, 20), (10, 300), (4, 2000)])
+def test_bptt_gradient_and_metrics_match_oracle(loss, T, B):
+    tr = _trainer(T, B, loss)
+    ob, prev, t = _batch(T, B, 3 + B)
+    p = tr.params().cpu().numpy()
+    g = tr.rollout(_t(ob), _t(prev), _t(t)).cpu().numpy()
+    fw = ln.forward(p, ob, prev)
+    L, d, sq = ln.loss_and_dout(fw["pdflat"], t, loss, T * B)
+    _grad_check(g, ln.backward(p, fw, d))
+    tr.apply()
+    m = tr.metrics(1)[0]
+    assert abs(m[0] - L) <= 2e-4 * abs(L) + 1e-6 and abs(m[1] - sq) <= 2e-4 * sq + 1e-6 and m[2] == T * B
+
+
+def test_gradient_from_a_given_initial_state():
+    T, B = 5, 40
+    tr = _trainer(T, B, "kl")
+    ob, prev, t = _batch(T, B, 1)
+    st = np.random.RandomState(2).uniform(-.5, .5, (2, B, 200)).astype(np.float32)
+    p = tr.params().cpu().numpy()
+    g = tr.rollout(_t(ob), _t(prev), _t(t), _t(st)).cpu().numpy()
+    fw = ln.forward(p, ob, prev, st)
+    _, d, _ = ln.loss_and_dout(fw["pdflat"], t, "kl", T * B)
+    _grad_check(g, ln.backward(p, fw, d))
+
+
+def test_adam_steps_match_oracle():
+    T, B = 10, 20
+    tr = _trainer(T, B, "kl")
+    ob, prev, t = _batch(T, B, 8)
+    p = tr.params().cpu().numpy().copy()
+    opt = pn.AdamTF1(ln.P_LSTM, lr=1e-3)
+    for k in range(3):
+        fw = ln.forward(p, ob, prev)
+        _, d, _ = ln.loss_and_dout(fw["pdflat"], t, "kl", T * B)
+        g = ln.backward(p, fw, d)
+        before = p.copy()
+        p = opt.step(p, g)
+        tr.step(_t(ob), _t(prev), _t(t))
+        got = tr.params().cpu().numpy()
+        # Adam's update is ~lr * sign(g) where |g| is tiny, so f32 rounding of a near-zero
+        # gradient can move it by up to 2 lr: compare tightly where the gradient is resolved
+        strong = np.abs(g) > 1e-4 * np.abs(g).max()
+        np.testing.assert_allclose(got[strong], p[strong], atol=1e-6 + 1e-3 * np.abs(p - before).max())
+        assert np.abs(got - p).max() <= 2e-3 + 1e-6
+        p = got.copy()
+    assert tr.counter() == 3
+
+
+def test_dropout_matches_oracle_mask():
+    T, B = 10, 50
+    tr = _trainer(T, B, "mse", keep_prob=0.5, seed=77)
+    ob, prev, t = _batch(T, B, 4)
+    for step in range(2):
+        p = tr.params().cpu().numpy()
+        g = tr.rollout(_t(ob), _t(prev), _t(t)).cpu().numpy()
+        fw = ln.forward(p, ln.dropout(ob, 0.5, 77, step), prev)
+        _, d, _ = ln.loss_and_dout(fw["pdflat"], t, "mse", T * B)
+        _grad_check(g, ln.backward(p, fw, d))
+        tr.apply()
+
+
+def test_sharded_windows_sum_to_the_full_batch():
+    from reacherdistilation_amd.student_lstm import StudentLstmConfig, StudentLstmTrainer
+    T, B = 10, 60
+    ob, prev, t = _batch(T, B, 9)
+    cfg = dict(loss="mse", steps=T, keep_prob=0.8, seed=3)
+    full = StudentLstmTrainer(StudentLstmConfig(max_windows=B, **cfg), device=DEV, params=_params())
+    gf = full.rollout(_t(ob), _t(prev), _t(t)).clone()
+    a = StudentLstmTrainer(StudentLstmConfig(max_windows=25, **cfg), device=DEV, params=_params(), row_base=0)
+    b = StudentLstmTrainer(StudentLstmConfig(max_windows=35, **cfg), device=DEV, params=_params(), row_base=25)
+    ga = a.rollout(_t(ob[:, :25]), _t(prev[:, :25]), _t(t[:, :25]), windows_global=B).clone()
+    gb = b.rollout(_t(ob[:, 25:]), _t(prev[:, 25:]), _t(t[:, 25:]), windows_global=B).clone()
+    _grad_check((ga + gb).cpu().numpy(), gf.cpu().numpy().astype(np.float64))
+
+
+def test_deterministic():
+    T, B = 10, 500
+    ob, prev, t = _batch(T, B, 2)
+    g1 = _trainer(T, B).rollout(_t(ob), _t(prev), _t(t)).clone()
+    g2 = _trainer(T, B).rollout(_t(ob), _t(prev), _t(t)).clone()
+    assert torch.equal(g1, g2)
+
+
+def test_learns_a_fixed_teacher_sequence():
+    """KL to fixed target windows falls by > 5x in 150 Adam steps (lr 1e-3)."""
+    T, B = 10, 64
+    ob, prev, _ = _batch(T, B, 11)
+    target = ln.forward(ln.init(99), ob, prev)["pdflat"].astype(np.float32)
+    tr = _trainer(T, B, "kl")
+    obt, prt, tgt = _t(ob).to(DEV), _t(prev).to(DEV), _t(target).to(DEV)
+    for _ in range(150):
+        tr.step(obt, prt, tgt)
+    m = tr.metrics(150)
+    assert np.all(np.isfinite(m[:, 0])) and m[-1, 0] < 0.2 * m[0, 0], (m[0, 0], m[-1, 0])
+
+
+def test_bad_arguments_raise():
+    tr = _trainer(10, 20)
+    ob, prev, t = _batch(10, 21)
+    with pytest.raises(ValueError):
+        tr.forward(_t(ob), _t(prev))           # 21 windows > max_windows 20
+    with pytest.raises(ValueError):
+        tr.forward(_t(ob[:5, :4]), _t(prev[:5, :4]))   # T = 5 != 10
