@@ -100,6 +100,29 @@ class DeviceDataset:
         r = self.curr[self.curr_len - 1]
         return r[F_T:F_S].clone(), r[F_REW:F_REW + 1].clone()
 
+    def test_windows(self, ob):
+        """(ob [T,B,11], prev_pdflat [T,B,4], prev_rew [T,B,1]) for the LSTM student's query:
+        column B-1 holds the current episode's last T-1 records and the current step (zero-
+        padded at the front), each with its prev fields; other columns are zero.  This is the
+        reference's intended test batch (dataset.py:205-288 with the per-step "prev" series its
+        commented-out lines build): as committed, prev_pdflat_batch_array holds a single
+        element that only broadcasts when the episode has 0 or >= T-1 records."""
+        ob_w = self.test_batch(ob)
+        prev_w = torch.zeros(self.T, self.B, PDFLAT_SHAPE, device=self.device)
+        prew_w = torch.zeros(self.T, self.B, 1, device=self.device)
+        n = self.curr_len
+        k = min(n, self.T - 1)
+        if n > 0:
+            rec = self.curr[:n]
+            prev_all = self._prev(rec)                               # [n, 5] prev fields of the records
+            if k > 0:
+                prev_w[self.T - 1 - k:self.T - 1, self.B - 1] = prev_all[n - k:, :PDFLAT_SHAPE]
+                prew_w[self.T - 1 - k:self.T - 1, self.B - 1] = prev_all[n - k:, PDFLAT_SHAPE:]
+            cp, cr = self.current_prev()
+            prev_w[self.T - 1, self.B - 1] = cp
+            prew_w[self.T - 1, self.B - 1] = cr
+        return ob_w, prev_w, prew_w
+
     def test_batch(self, ob):
         """[T, B, 11]: batch column B-1 holds the window of the current episode ending at
         `ob` (its last T-1 observations, zero-padded at the front); the other columns are zero,

@@ -1,0 +1,83 @@
+"""The reference's LSTM distillation driver, ``lstm_train.train(train, restore)`` (reference
+src/distilation/lstm_train.py:18-201), re-expressed over the MI355X path: the env is the HIP
+Reacher-v2 (``make_mujoco_env``), the teacher query is ``rdd_forward``, and the student is
+the reference's ``student_lstm_graph`` trained by the kernels behind ``StudentLstmTrainer``
+on windows from the device-resident ``DeviceDataset``.
+
+Phases as in the reference:
+  1. (:114-135) the teacher steps the env until ``num_episodes() > 2 * LSTM_BATCH_SIZE``;
+  2. (:139-201) per env step: one optimiser step on each [T, B] window from
+     ``training_batches()`` (zero initial LSTM state, :159), teacher relabel of the current
+     observation, the student's mean action from the test window's last output with the
+     previous query's final state as initial state (:166-183), record with 's', env.step
+     with the student action; episode boundaries reset the env and flush the dataset.
+
+Fixes of the reference as committed: the test window's prev_pdflat column is
+the per-step series (``DeviceDataset.test_windows``), not the single element that only
+broadcasts at 0 or >= T-1 records.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .config import LSTM_BATCH_SIZE, OBSPACE_SHAPE, STEPS_UNROLLED, TOTAL_EPISODES
+from .dataset import DeviceDataset
+from .distill import DistillConfig, DistillTrainer
+from .env import make_mujoco_env
+from .policy import TeacherAgent
+from .student_lstm import StudentLstmConfig, StudentLstmTrainer
+
+
+def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EPISODES, loss: str = "kl",
+          lr: float = 1e-3, keep_prob: float = 1.0, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
+          warmup_episodes: int = 2 * LSTM_BATCH_SIZE, log=print):
+    """Returns (student trainer, dataset, per-episode summed training loss)."""
+    env = make_mujoco_env("Reacher-v2", seed, device=device)
+    teacher = TeacherAgent(restore=restore, path=teacher_path)
+    tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
+    st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
+                                              steps=STEPS_UNROLLED, max_windows=LSTM_BATCH_SIZE), device=device)
+    dataset = DeviceDataset(device=device, seed=seed, batch_size=LSTM_BATCH_SIZE, steps_unrolled=STEPS_UNROLLED)
+    losses = []
+    if not train:
+        return st, dataset, losses
+    ob = env.reset()
+    reward = 0.0
+
+    def teacher_query(o):
+        t, _ = tq.forward(torch.as_tensor(np.asarray(o, np.float32)).view(1, OBSPACE_SHAPE), student=False)
+        return t[0].cpu().numpy()
+
+    log("Begin Training! First Accumulate observation with teacher")
+    while dataset.num_episodes() <= warmup_episodes:
+        t_pdflat = teacher_query(ob)
+        dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, stepped_with="t")
+        ob, reward, new, _ = env.step(t_pdflat[:2])
+        if new:
+            ob = env.reset()
+            dataset.flush()
+    log("Accumulated sufficient data points from teacher. now train")
+
+    state = None   # curr_state_batch: zero at the start (lstm_train.py:88-89)
+    total_loss = 0.0
+    while True:
+        for ob_b, t_b, prev_b, _prew_b in dataset.training_batches():
+            st.step(ob_b, prev_b, t_b)          # zero initial state (lstm_train.py:159)
+            total_loss += float(st.metrics(1)[0, 0])
+        t_pdflat = teacher_query(ob)
+        ob_w, prev_w, _ = dataset.test_windows(ob)
+        out, state = st.forward(ob_w, prev_w, state)
+        s_pdflat = out[STEPS_UNROLLED - 1, LSTM_BATCH_SIZE - 1].cpu().numpy()
+        dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, s_pdflat=s_pdflat, stepped_with="s")
+        ob, reward, new, _ = env.step(s_pdflat[:2])
+        if new:
+            log("************** Episode {0} ****************".format(dataset.num_episodes()))
+            ob = env.reset()
+            log("recent loss: %f " % total_loss)
+            losses.append(total_loss)
+            total_loss = 0.0
+            dataset.flush()
+            if dataset.num_episodes() >= episodes:
+                break
+    return st, dataset, losses

@@ -82,3 +82,14 @@ def test_reference_shaped_driver_with_the_reference_student():
     assert sm.counter() == 50
     m = sm.metrics(50)
     assert np.all(m[:, 2] == 200)   # one [10, 20] window = 200 rows per optimiser step
+
+
+def test_reference_shaped_lstm_driver_runs():
+    """lstm_train.train: teacher warm-up, then per env step one truncated-BPTT Adam step on a
+    [10, 20] window and the student's query with the carried LSTM state."""
+    from reacherdistilation_amd import lstm_train
+    st, ds, losses = lstm_train.train(episodes=4, warmup_episodes=2, keep_prob=0.5, log=lambda *a: None)
+    assert ds.num_episodes() == 4 and len(losses) == 1 and np.isfinite(losses[0])
+    assert st.counter() == 50
+    m = st.metrics(50)
+    assert np.all(m[:, 2] == 200) and np.all(np.isfinite(m[:, 0]))

@@ -67,3 +67,30 @@ def test_test_batch_window(length):
     k = min(length, 9)
     assert np.array_equal(col[9 - k:9], np.arange(length - k + 1, length + 1, dtype=np.float32))
     assert not col[:9 - k].any()
+
+
+@pytest.mark.parametrize("length", [0, 1, 5, 9, 30])
+def test_test_windows_carry_the_prev_series(length):
+    """LSTM query window: column B-1 = last T-1 records + the current step, with each step's
+    prev fields (previous record's teacher pdflat / reward; the current step's = the last
+    record's), zero-padded at the front; the other columns are zero."""
+    ds = DeviceDataset(capacity=4, device="cpu", seed=0)
+    for k in range(length):
+        ds.write(ob=np.full(11, float(k)), reward=0.5 * k, t_pdflat=np.array([k, 10 + k, -1, -2], float))
+    ob_w, prev_w, prew_w = ds.test_windows(np.full(11, 99.0))
+    assert ob_w.shape == (10, 20, 11) and prev_w.shape == (10, 20, 4) and prew_w.shape == (10, 20, 1)
+    assert not ob_w[:, :19].any() and not prev_w[:, :19].any() and not prew_w[:, :19].any()
+    assert ob_w[9, 19, 0] == 99.0
+    for row in range(10):
+        j = length - (9 - row)          # record index of this row (j == length: the current step)
+        if j < 0:
+            assert not ob_w[row, 19].any() and not prev_w[row, 19].any()
+            continue
+        if j < length:
+            assert ob_w[row, 19, 0] == j
+        want_prev = j - 1               # prev = previous record's t (zeros at j = 0)
+        if want_prev >= 0:
+            assert prev_w[row, 19, 0] == want_prev and prev_w[row, 19, 1] == 10 + want_prev
+            assert prew_w[row, 19, 0] == 0.5 * want_prev
+        else:
+            assert not prev_w[row, 19].any() and prew_w[row, 19, 0] == 0
