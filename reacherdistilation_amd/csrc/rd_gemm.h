@@ -5,12 +5,12 @@
 // optional accumulate into C.  Deterministic: fixed tiling, split-K partials summed in a
 // fixed order by a second kernel (no atomics).
 //
-// Tiling: 256-thread workgroups own a 64 x 64 C tile; 4 waves each 32 x 32 = 2 x 2 blocks of
-// v_mfma_f32_16x16x4_f32 (exact f32 products).  K advances 16 at a time through double-
-// buffered LDS tiles stored [k][m] / [k][n] with row stride 80 floats, so the 64 lanes of an
-// MFMA operand read (16 consecutive m or n) x (4 k rows) hit 64 distinct banks; the next
-// tile's global loads (one 16-B load per thread per operand when aligned) are in flight
-// while the current tile's 16 MFMAs per wave issue.
+// Tiling: 256-thread workgroups own a 128 x 128 (or, for thin problems, 64 x 64) C tile; 4
+// waves in 2 x 2, each 4 x 4 (2 x 2) blocks of v_mfma_f32_16x16x4_f32 (exact f32 products).
+// K advances 16 at a time through double-buffered LDS tiles stored [k][m] / [k][n] with row
+// stride BT + 16 floats, so the 64 lanes of an MFMA operand read (16 consecutive m or n) x
+// (4 k rows) hit 64 distinct banks; the next tile's global loads (16-B loads when aligned)
+// are in flight while the current tile's MFMAs issue.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -41,7 +41,7 @@ struct GemmArgs {
     int kchunk;           // K range per split (multiple of 16)
 };
 
-constexpr int TM = 64, TN = 64, TK = 16, GEMM_THREADS = 256, LDS_STRIDE = 80;
+constexpr int TK = 16, GEMM_THREADS = 256;
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, int row, int col, float v) {
     if (g.bias) v += g.bias[col];
@@ -67,102 +67,117 @@ __device__ __forceinline__ f32x4 load4(const float* p, int valid) {
     return v;
 }
 
-template <bool TA, bool TB, bool VEC>
+// BT x BT C tile per workgroup (BT = 64 or 128); 4 waves in 2 x 2, each (BT/2)^2 =
+// (BT/32)^2 16x16 blocks.  LDS rows are BT + 16 floats: the 4 k-rows of one MFMA operand
+// start 16 banks apart, so 16 consecutive m (or n) x 4 k hit 64 distinct banks.
+template <int BT, bool TA, bool TB, bool VEC>
 __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
-    __shared__ __attribute__((aligned(16))) float As[2][TK][LDS_STRIDE];
-    __shared__ __attribute__((aligned(16))) float Bs[2][TK][LDS_STRIDE];
+    constexpr int LS = BT + 16, FB = BT / 32, NQ = BT / 64;   // blocks per wave dim, loads per thread
+    __shared__ __attribute__((aligned(16))) float As[2][TK][LS];
+    __shared__ __attribute__((aligned(16))) float Bs[2][TK][LS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int wm = wave >> 1, wn = wave & 1;
-    const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+    const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT;
     const int kbeg = blockIdx.z * g.kchunk;
     const int kend = min(g.K, kbeg + g.kchunk);
-    // loader coordinates: [contiguous-dim quad][other dim]
-    const int a_r = TA ? tid >> 4 : tid >> 2, a_q = TA ? tid & 15 : tid & 3;
-    const int b_r = TB ? tid >> 2 : tid >> 4, b_q = TB ? tid & 3 : tid & 15;
 
-    auto load_a = [&](int k0) -> f32x4 {
-        if (!TA) {   // A[m][k]: row m0 + a_r, k = k0 + 4 a_q ..
-            const int m = m0 + a_r, k = k0 + 4 * a_q;
+    // quad q of a tile: [row][4 quads of k] (k-contiguous) or [k][BT/4 quads] (k-strided)
+    auto load_a = [&](int k0, int q) -> f32x4 {
+        if (!TA) {
+            const int m = m0 + (q >> 2), k = k0 + 4 * (q & 3);
             const int valid = m < g.M ? min(4, kend - k) : 0;
             return load4<VEC>(g.A + (int64_t)m * g.lda + k, valid);
-        } else {     // A^T stored [k][m]: row k0 + a_r, m = m0 + 4 a_q ..
-            const int k = k0 + a_r, m = m0 + 4 * a_q;
+        } else {
+            const int k = k0 + q / (BT / 4), m = m0 + 4 * (q % (BT / 4));
             const int valid = k < kend ? min(4, g.M - m) : 0;
             return load4<VEC>(g.A + (int64_t)k * g.lda + m, valid);
         }
     };
-    auto load_b = [&](int k0) -> f32x4 {
-        if (!TB) {   // B[k][n]
-            const int k = k0 + b_r, n = n0 + 4 * b_q;
+    auto load_b = [&](int k0, int q) -> f32x4 {
+        if (!TB) {
+            const int k = k0 + q / (BT / 4), n = n0 + 4 * (q % (BT / 4));
             const int valid = k < kend ? min(4, g.N - n) : 0;
             return load4<VEC>(g.B + (int64_t)k * g.ldb + n, valid);
-        } else {     // B^T stored [n][k]
-            const int n = n0 + b_r, k = k0 + 4 * b_q;
+        } else {
+            const int n = n0 + (q >> 2), k = k0 + 4 * (q & 3);
             const int valid = n < g.N ? min(4, kend - k) : 0;
             return load4<VEC>(g.B + (int64_t)n * g.ldb + k, valid);
         }
     };
-    auto store_a = [&](int buf, f32x4 v) {
+    auto store_a = [&](int buf, int q, f32x4 v) {
         if (!TA) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) As[buf][4 * a_q + e][a_r] = v[e];
+            for (int e = 0; e < 4; ++e) As[buf][4 * (q & 3) + e][q >> 2] = v[e];
         } else {
-            *reinterpret_cast<f32x4*>(&As[buf][a_r][4 * a_q]) = v;
+            *reinterpret_cast<f32x4*>(&As[buf][q / (BT / 4)][4 * (q % (BT / 4))]) = v;
         }
     };
-    auto store_b = [&](int buf, f32x4 v) {
+    auto store_b = [&](int buf, int q, f32x4 v) {
         if (!TB) {
-            *reinterpret_cast<f32x4*>(&Bs[buf][b_r][4 * b_q]) = v;
+            *reinterpret_cast<f32x4*>(&Bs[buf][q / (BT / 4)][4 * (q % (BT / 4))]) = v;
         } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) Bs[buf][4 * b_q + e][b_r] = v[e];
+            for (int e = 0; e < 4; ++e) Bs[buf][4 * (q & 3) + e][q >> 2] = v[e];
         }
     };
 
-    f32x4 acc[2][2];
+    f32x4 acc[FB][FB];
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < FB; ++x)
 #pragma unroll
-        for (int y = 0; y < 2; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int y = 0; y < FB; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int ntiles = kend > kbeg ? (kend - kbeg + TK - 1) / TK : 0;
     if (ntiles > 0) {
-        store_a(0, load_a(kbeg));
-        store_b(0, load_b(kbeg));
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+            store_a(0, tid + GEMM_THREADS * u, load_a(kbeg, tid + GEMM_THREADS * u));
+            store_b(0, tid + GEMM_THREADS * u, load_b(kbeg, tid + GEMM_THREADS * u));
+        }
     }
     __syncthreads();
     for (int kt = 0; kt < ntiles; ++kt) {
         const int buf = kt & 1;
-        f32x4 na, nb;
+        f32x4 na[NQ], nb[NQ];
         const bool more = kt + 1 < ntiles;
         if (more) {
-            na = load_a(kbeg + (kt + 1) * TK);
-            nb = load_b(kbeg + (kt + 1) * TK);
+#pragma unroll
+            for (int u = 0; u < NQ; ++u) {
+                na[u] = load_a(kbeg + (kt + 1) * TK, tid + GEMM_THREADS * u);
+                nb[u] = load_b(kbeg + (kt + 1) * TK, tid + GEMM_THREADS * u);
+            }
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int kk = 4 * s + gq;
-            const float a0 = As[buf][kk][32 * wm + i], a1 = As[buf][kk][32 * wm + 16 + i];
-            const float b0 = Bs[buf][kk][32 * wn + i], b1 = Bs[buf][kk][32 * wn + 16 + i];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+            float a[FB], b[FB];
+#pragma unroll
+            for (int x = 0; x < FB; ++x) a[x] = As[buf][kk][(BT / 2) * wm + 16 * x + i];
+#pragma unroll
+            for (int y = 0; y < FB; ++y) b[y] = Bs[buf][kk][(BT / 2) * wn + 16 * y + i];
+#pragma unroll
+            for (int x = 0; x < FB; ++x)
+#pragma unroll
+                for (int y = 0; y < FB; ++y)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x], b[y], acc[x][y], 0, 0, 0);
         }
         if (more) {
-            store_a(buf ^ 1, na);
-            store_b(buf ^ 1, nb);
+#pragma unroll
+            for (int u = 0; u < NQ; ++u) {
+                store_a(buf ^ 1, tid + GEMM_THREADS * u, na[u]);
+                store_b(buf ^ 1, tid + GEMM_THREADS * u, nb[u]);
+            }
         }
         __syncthreads();
     }
 
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < FB; ++x)
 #pragma unroll
-        for (int y = 0; y < 2; ++y)
+        for (int y = 0; y < FB; ++y)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = m0 + 32 * wm + 16 * x + 4 * gq + r, col = n0 + 32 * wn + 16 * y + i;
+                const int row = m0 + (BT / 2) * wm + 16 * x + 4 * gq + r, col = n0 + (BT / 2) * wn + 16 * y + i;
                 if (row >= g.M || col >= g.N) continue;
                 if (g.splits > 1)
                     g.part[((int64_t)blockIdx.z * g.M + row) * g.N + col] = acc[x][y][r];
@@ -171,27 +186,49 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
             }
 }
 
-// split-K: C = epi(sum_z part[z]) in a fixed order
+// split-K: C = epi(sum_z part[z]) in a fixed order.  64 outputs per block, 4 interleaved
+// split phases per output (summed in a fixed order at the end).
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ float s[4][64];
     const int64_t MN = (int64_t)g.M * g.N;
-    if (idx >= MN) return;
-    float s = 0.f;
-    for (int z = 0; z < g.splits; ++z) s += g.part[z * MN + idx];
-    const int row = (int)(idx / g.N), col = (int)(idx % g.N);
-    g.C[(int64_t)row * g.ldc + col] = apply_epi(g, row, col, s);
+    const int64_t idx = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int ph = threadIdx.x >> 6;
+    float a = 0.f, b = 0.f;
+    if (idx < MN) {
+        int z = ph;
+        for (; z + 4 < g.splits; z += 8) {
+            a += g.part[z * MN + idx];
+            b += g.part[(z + 4) * MN + idx];
+        }
+        if (z < g.splits) a += g.part[z * MN + idx];
+    }
+    s[ph][threadIdx.x & 63] = a + b;
+    __syncthreads();
+    if (ph == 0 && idx < MN) {
+        const float v = (s[0][threadIdx.x] + s[1][threadIdx.x]) + (s[2][threadIdx.x] + s[3][threadIdx.x]);
+        const int row = (int)(idx / g.N), col = (int)(idx % g.N);
+        g.C[(int64_t)row * g.ldc + col] = apply_epi(g, row, col, v);
+    }
 }
 
 // Launch; `part`/`part_floats` = split-K workspace (may be null: no split).  Returns a hip error.
 inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_floats, int cus) {
     if (g.M <= 0 || g.N <= 0) return hipSuccess;
-    const int tm = (g.M + TM - 1) / TM, tn = (g.N + TN - 1) / TN;
+    // 128 x 128 tiles (half the operand re-reads, 4x the MFMAs per LDS read) when both
+    // dimensions fill them; 64 x 64 otherwise
+#ifdef RD_GEMM_BT   // diagnostic builds (build.py --variant): force one tile size
+    const int BT = RD_GEMM_BT;
+#else
+    const int BT = 64;   // measured (scripts/gemm_tile_compare.sh): 64 beats 128 on every LSTM shape
+#endif
+    const int tm = (g.M + BT - 1) / BT, tn = (g.N + BT - 1) / BT;
     const int tiles = tm * tn;
-    // split K when the tile grid cannot fill the chip and K is long
+    // split K when the tile grid cannot fill the chip (~8 workgroups per CU, so the loads of
+    // one tile's K-loop hide behind the others' MFMAs) and K is long
     int splits = 1;
-    if (part && tiles < 2 * cus && g.K >= 512) {
-        splits = (2 * cus + tiles - 1) / tiles;
-        const int maxs = g.K / 256;
+    if (part && tiles < 8 * cus && g.K >= 512) {
+        splits = (8 * cus + tiles - 1) / tiles;
+        const int maxs = g.K / 256 < 256 ? g.K / 256 : 256;   // >= 16 k-tiles per split, <= 256 partials
         if (splits > maxs) splits = maxs;
         while (splits > 1 && (int64_t)splits * g.M * g.N > part_floats) --splits;
     }
@@ -201,23 +238,31 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
     if (splits > 1) g.splits = (g.K + g.kchunk - 1) / g.kchunk;
     const bool vec = ((uintptr_t)g.A % 16 == 0) && ((uintptr_t)g.B % 16 == 0) && g.lda % 4 == 0 && g.ldb % 4 == 0;
     dim3 grid(tn, tm, g.splits);
-#define RDG_LAUNCH(TA_, TB_, V_) hipLaunchKernelGGL((gemm_kernel<TA_, TB_, V_>), grid, dim3(GEMM_THREADS), 0, st, g)
-    if (vec) {
-        if (!g.ta && !g.tb) RDG_LAUNCH(false, false, true);
-        else if (!g.ta && g.tb) RDG_LAUNCH(false, true, true);
-        else if (g.ta && !g.tb) RDG_LAUNCH(true, false, true);
-        else RDG_LAUNCH(true, true, true);
-    } else {
-        if (!g.ta && !g.tb) RDG_LAUNCH(false, false, false);
-        else if (!g.ta && g.tb) RDG_LAUNCH(false, true, false);
-        else if (g.ta && !g.tb) RDG_LAUNCH(true, false, false);
-        else RDG_LAUNCH(true, true, false);
+#define RDG_LAUNCH(BT_, TA_, TB_, V_) \
+    hipLaunchKernelGGL((gemm_kernel<BT_, TA_, TB_, V_>), grid, dim3(GEMM_THREADS), 0, st, g)
+#define RDG_DISPATCH(BT_)                                                   \
+    if (vec) {                                                              \
+        if (!g.ta && !g.tb) RDG_LAUNCH(BT_, false, false, true);           \
+        else if (!g.ta && g.tb) RDG_LAUNCH(BT_, false, true, true);        \
+        else if (g.ta && !g.tb) RDG_LAUNCH(BT_, true, false, true);        \
+        else RDG_LAUNCH(BT_, true, true, true);                             \
+    } else {                                                                \
+        if (!g.ta && !g.tb) RDG_LAUNCH(BT_, false, false, false);          \
+        else if (!g.ta && g.tb) RDG_LAUNCH(BT_, false, true, false);       \
+        else if (g.ta && !g.tb) RDG_LAUNCH(BT_, true, false, false);       \
+        else RDG_LAUNCH(BT_, true, true, false);                            \
     }
+    if (BT == 128) {
+        RDG_DISPATCH(128)
+    } else {
+        RDG_DISPATCH(64)
+    }
+#undef RDG_DISPATCH
 #undef RDG_LAUNCH
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || g.splits <= 1) return e;
     const int64_t MN = (int64_t)g.M * g.N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, g);
     return hipGetLastError();
 }
 

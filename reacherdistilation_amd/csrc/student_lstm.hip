@@ -57,7 +57,7 @@ static_assert(OFF_WL % 4 == 0 && OFF_W1 % 4 == 0 && OFF_W2 % 4 == 0 && OFF_W3 % 
 
 constexpr int N_MET = 4;
 constexpr int LOSS_BLOCK = 256;
-constexpr int COLSUM_CHUNK = 2048;        // rows per first-level column-sum block
+constexpr int COLSUM_CHUNK = 512;         // rows per first-level column-sum block
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
@@ -207,10 +207,16 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* src, int64_t M
     __shared__ float s[4][64];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
     const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = min(M, r0 + chunk);
-    float a = 0.f;
-    if (c < N)
-        for (int64_t r = r0 + ph; r < r1; r += 4) a += src[r * ld + c];
-    s[ph][threadIdx.x & 63] = a;
+    float a = 0.f, b = 0.f;
+    if (c < N) {
+        int64_t r = r0 + ph;
+        for (; r + 4 < r1; r += 8) {   // two chains: loads of 2 rows in flight per step
+            a += src[r * ld + c];
+            b += src[(r + 4) * ld + c];
+        }
+        if (r < r1) a += src[r * ld + c];
+    }
+    s[ph][threadIdx.x & 63] = a + b;
     __syncthreads();
     if (ph == 0 && c < N) out[(int64_t)blockIdx.y * ld_out + c] = (s[0][threadIdx.x] + s[1][threadIdx.x]) +
                                                                  (s[2][threadIdx.x] + s[3][threadIdx.x]);
@@ -259,7 +265,7 @@ int cu_count(int device) {
     return prop.multiProcessorCount;
 }
 
-constexpr int64_t SPLIT_FLOATS = 4 << 20;   // split-K partials (16 MB)
+constexpr int64_t SPLIT_FLOATS = 16 << 20;  // split-K partials (64 MB)
 
 }  // namespace
 
