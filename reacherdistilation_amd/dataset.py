@@ -8,7 +8,9 @@ stepped_with)`` appends one step record of the current episode (:118-143, includ
 ``training_batches()`` yields TRAINING_EPOCHS random windows -- LSTM_BATCH_SIZE episodes
 drawn with replacement, one common start in [0, EPISODE_STEPS - STEPS_UNROLLED] -- as
 ``(ob [T,B,11], t_pdflat [T,B,4], prev_pdflat [T,B,4], prev_rew [T,B,1])`` (:179-202);
-``test_batch(ob)`` builds the [T,B,11] window ending at the current observation (:205-235).
+``test_batch(ob)`` builds the [T,B,11] window ending at the current observation (:205-235);
+``dump(store)`` / ``load_page(path)`` move episodes to / from pages in the reference's
+on-disk format (``pages.PageStore``, :14-65,72-96).
 
 Storage: one ring of ``capacity`` complete episodes x EPISODE_STEPS records x 21 floats
 (ob 11 | rew 1 | t 4 | s 4 | with 1) plus the open episode, all on ``device``.  The
@@ -38,6 +40,7 @@ class DeviceDataset:
         self.num_total_episodes = 0
         self.B, self.T, self.epochs = int(batch_size), int(steps_unrolled), int(epochs)
         self._gen = torch.Generator().manual_seed(int(seed))   # host RNG: indices only
+        self._mem_slots = []   # ring slots flushed since the last full page (reference data_in_memory)
 
     # -- reference interface -------------------------------------------------------------
     def num_episodes(self) -> int:
@@ -62,9 +65,27 @@ class DeviceDataset:
         the ring: the windows of training_batches() span any start in [0, 40]."""
         if self.curr_len == EPISODE_STEPS:
             self.ring[self.num_total_episodes % self.capacity].copy_(self.curr)
+            self._mem_slots.append(self.num_total_episodes % self.capacity)
         self.curr.zero_()
         self.curr_len = 0
         self.num_total_episodes += 1
+
+    def dump(self, store):
+        """Dataset.dump (reference dataset.py:78-83): write the episodes flushed since the last
+        full page to the store's current page (a new page starts once MAX_CAPACITY are in)."""
+        from .pages import records_to_episodes
+        eps = records_to_episodes(self.ring[self._mem_slots].double().cpu().numpy()) if self._mem_slots else []
+        if not store.store(eps):
+            self._mem_slots = []
+
+    def load_page(self, path: str) -> int:
+        """Append a page's complete episodes to the ring (oldest overwritten); returns how many."""
+        from .pages import episodes_to_records, read_page
+        rec = torch.as_tensor(episodes_to_records(read_page(path)), dtype=torch.float32)
+        for ep in rec:
+            self.ring[self.num_total_episodes % self.capacity].copy_(ep.to(self.device))
+            self.num_total_episodes += 1
+        return rec.shape[0]
 
     def stored(self) -> int:
         return min(self.num_total_episodes, self.capacity)
