@@ -188,6 +188,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
 
 // split-K: C = epi(sum_z part[z]) in a fixed order.  64 outputs per block, 4 interleaved
 // split phases per output (summed in a fixed order at the end).
+template <int = 0>   // a template: one definition per translation unit that includes this header
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
     __shared__ float s[4][64];
     const int64_t MN = (int64_t)g.M * g.N;
@@ -262,7 +263,7 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || g.splits <= 1) return e;
     const int64_t MN = (int64_t)g.M * g.N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(splitk_reduce_kernel<0>, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, g);
     return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@ from tests.conftest import ROOT
 def _declared(header):
     txt = open(os.path.join(ROOT, "include", header)).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(rd[dml]?_[a-z0-9_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(rd[dmlp]?_[a-z0-9_]+)\s*\(", txt)))
 
 
 @pytest.fixture(scope="module")
