@@ -68,6 +68,93 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_ref_loop(seconds):
+    """BASELINE.md §2 "CPU-ref-loop (C1)": the reference's single-env loop structure on one
+    core -- per env step: teacher query (B=1), one distillation Adam step on a window batch
+    of 20 episodes x 10 steps (200 rows, f64 policy math), the student's query (B=1), f64
+    env.step -- with the oracle's CPU restatement (numpy policy, C f64 env)."""
+    import numpy as np
+
+    from oracle import policy_np as pn
+    from oracle import ref_c
+    from reacherdistilation_amd.policy import student_init, synthetic_teacher
+    t, s = synthetic_teacher(1), student_init(2)
+    tp, tmu, tsd = t.flat.astype(np.float64), t.ob_mean.astype(np.float64), t.ob_std.astype(np.float64)
+    sp = s.flat.copy()
+    smu, ssd = s.ob_mean.astype(np.float64), s.ob_std.astype(np.float64)
+    opt = pn.AdamTF1(pn.P_TOT)
+    state = ref_c.philox_reset(1, 0, 0, 0).astype(np.float64)
+    rng = np.random.RandomState(0)
+    buf = np.zeros((40, 50, 11))                       # a filled dataset of 40 episodes
+    buf[:] = rng.uniform(-1, 1, buf.shape)
+    ob, _ = ref_c.step(state, np.zeros((1, 2), np.float32), np.float64)
+    import threadpoolctl
+    limit = threadpoolctl.threadpool_limits(1)         # one core: BLAS single-threaded
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        ft1 = pn.forward(tp, tmu, tsd, ob)                              # teacher query
+        eps, st = rng.randint(0, 40, 20), rng.randint(0, 41)
+        win = buf[eps, st:st + 10].reshape(200, 11)                     # training window
+        fs = pn.forward(sp.astype(np.float64), smu, ssd, win)
+        ft = pn.forward(tp, tmu, tsd, win)
+        _, dmean, dls, _ = pn.loss_and_dmean(fs, ft, "mse", 200)
+        sp = opt.step(sp, pn.backward(sp.astype(np.float64), fs, dmean, dls))
+        fa = pn.forward(sp.astype(np.float64), smu, ssd, ob)           # student acts
+        ob, _ = ref_c.step(state, fa["mean"].astype(np.float32), np.float64)
+        del ft1
+        steps += 1
+    el = time.perf_counter() - t0
+    limit.restore_original_limits()
+    return dict(value=steps / el, unit="env-steps/s", cores=1, kind="port",
+                sample=f"{steps} env steps ({el:.1f} s) of the reference-shaped single-env loop")
+
+
+def cpu_batched_env(seconds, n=65536):
+    """BASELINE.md §2 "CPU-batched-env": the C restatement's OpenMP reacher_step, f32 and f64."""
+    import numpy as np
+
+    from oracle import ref_c
+    out = {}
+    for dt, name in ((np.float32, "f32"), (np.float64, "f64")):
+        state = ref_c.philox_reset(n, 0, 0, 0).astype(dt)
+        act = np.random.RandomState(1).uniform(-1, 1, (n, 2)).astype(np.float32)
+        steps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds / 2:
+            ref_c.step(state, act, dt)
+            steps += 1
+        el = time.perf_counter() - t0
+        out[name] = dict(value=n * steps / el, unit="env-steps/s",
+                         cores=int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                         sample=f"{n} envs x {steps} steps ({el:.1f} s)")
+    return out
+
+
+def env_roofline(dev, n=1 << 24, iters=30):
+    """The standalone env.step kernel (rd_step) at 16.8M envs: algorithmic 113 B per
+    env-step (read act 8 + q,v 16 + target 8 + held offset 8; write q,v 16 + offset 8 +
+    obs 44 + rew 4 + done 1) over its launch time, vs the 8 TB/s HBM peak."""
+    import torch
+
+    from reacherdistilation_amd.env import BatchedReacher
+    env = BatchedReacher(n, seed=0, device=dev)
+    env.reset()
+    a = (torch.rand(n, 2, device=dev) * 2 - 1).contiguous()
+    for _ in range(5):
+        env.step(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    s.record()
+    for _ in range(iters):
+        env.step(a)
+    e.record()
+    torch.cuda.synchronize(dev)
+    sec = s.elapsed_time(e) * 1e-3 / iters
+    env.close()
+    gbs = 113 * n / sec / 1e9
+    return {"kernel": "rd_step_kernel", "bound": "hbm", "envs": n, "env_steps_per_s": n / sec,
+            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
+
+
 def copy_bandwidth(dev, gib=1.0, iters=20):
     """Measured device-to-device copy bandwidth (read + write bytes / s), the practical HBM
     ceiling the roofline is also quoted against."""
@@ -256,8 +343,12 @@ def main():
         }
         if accum is not None:
             out["accum"] = accum
+        out["roofline_env"] = env_roofline(dev)
+        out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / copy_gbs
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
+            out["cpu_baseline"]["ref_loop"] = cpu_ref_loop(min(4.0, args.cpu_seconds))
+            out["cpu_baseline"]["batched_env"] = cpu_batched_env(min(4.0, args.cpu_seconds))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

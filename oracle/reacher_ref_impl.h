@@ -99,7 +99,7 @@ static inline void FN(env_reset_)(REAL* s, const REAL* draw, REAL* obs) {
 
 /* Batched, SoA state [8][n]; act [n][2] float32; obs [n][11]; rew [n]. */
 void FN(rdo_step_)(int64_t n, REAL* state, const float* act, REAL* obs, REAL* rew) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (n >= 1024)
     for (int64_t i = 0; i < n; ++i) {
         REAL s[8];
         for (int k = 0; k < 8; ++k) s[k] = state[k * n + i];
@@ -110,7 +110,7 @@ void FN(rdo_step_)(int64_t n, REAL* state, const float* act, REAL* obs, REAL* re
 
 /* draws [n][6] = (q0,q1,v0,v1,tx,ty) */
 void FN(rdo_reset_)(int64_t n, REAL* state, const REAL* draws, REAL* obs) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (n >= 1024)
     for (int64_t i = 0; i < n; ++i) {
         REAL s[8];
         FN(env_reset_)(s, draws + 6 * i, obs + 11 * i);
