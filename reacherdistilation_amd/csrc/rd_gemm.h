@@ -38,7 +38,7 @@ struct GemmArgs {
     int accum;            // C += result
     float* part;          // split-K partials [splits][M][N] (splits > 1)
     int splits;
-    int kchunk;           // K range per split (multiple of 16)
+    int kchunk;           // K range per split (multiple of 32)
 };
 
 constexpr int TK = 16, GEMM_THREADS = 256;
@@ -52,6 +52,15 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, int row, int col, 
         v *= fmaf(-a, a, 1.0f);
     }
     if (g.accum) v += g.C[(int64_t)row * g.ldc + col];
+    return v;
+}
+
+// the epilogue on preloaded operands: bias b, stored activation a (EPI_DTANH), prior C c
+__device__ __forceinline__ float epi_value(const GemmArgs& g, float v, float b, float a, float c) {
+    v += b;
+    if (g.epi == EPI_TANH) v = tanhf(v);
+    else if (g.epi == EPI_DTANH) v *= fmaf(-a, a, 1.0f);
+    if (g.accum) v += c;
     return v;
 }
 
@@ -171,6 +180,23 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
         __syncthreads();
     }
 
+    // epilogue in two passes: every operand load (C when accumulating, the tanh' activation,
+    // the bias) is issued before any result is formed, so their latencies overlap
+    float in_c[FB][FB][4], in_a[FB][FB][4], in_b[FB][FB];
+#pragma unroll
+    for (int x = 0; x < FB; ++x)
+#pragma unroll
+        for (int y = 0; y < FB; ++y) {
+            const int col = n0 + (BT / 2) * wn + 16 * y + i;
+            in_b[x][y] = (g.splits <= 1 && g.bias && col < g.N) ? g.bias[col] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + (BT / 2) * wm + 16 * x + 4 * gq + r;
+                const bool ok = g.splits <= 1 && row < g.M && col < g.N;
+                in_c[x][y][r] = (ok && g.accum) ? g.C[(int64_t)row * g.ldc + col] : 0.0f;
+                in_a[x][y][r] = (ok && g.epi == EPI_DTANH) ? g.aux[(int64_t)row * g.ldaux + col] : 0.0f;
+            }
+        }
 #pragma unroll
     for (int x = 0; x < FB; ++x)
 #pragma unroll
@@ -182,8 +208,135 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
                 if (g.splits > 1)
                     g.part[((int64_t)blockIdx.z * g.M + row) * g.N + col] = acc[x][y][r];
                 else
-                    g.C[(int64_t)row * g.ldc + col] = apply_epi(g, row, col, acc[x][y][r]);
+                    g.C[(int64_t)row * g.ldc + col] = epi_value(g, acc[x][y][r], in_b[x][y], in_a[x][y][r],
+                                                               in_c[x][y][r]);
             }
+}
+
+// 128 x 128 C tile, K advancing 32 at a time, on v_mfma_f32_32x32x2_f32: 4 waves in 2 x 2,
+// each 64 x 64 = 2 x 2 blocks of 32 x 32 (64 accumulator registers).  Per k-step (K = 2) a
+// wave reads 2 A + 2 B operands from LDS for 4 MFMAs of 64 cycles each, 4x the MFMA work per
+// LDS read of the 64-tile kernel, and one barrier covers 64 MFMAs per wave.  LDS rows are
+// 128 + 32 floats: the two k-rows of an operand (lanes 0-31 / 32-63) start 32 banks apart.
+// Operand layouts (per lane l): A[i = l % 32][k = l / 32], B[k = l / 32][j = l % 32];
+// D register r of lane l = C[8 (r / 4) + 4 (l / 32) + r % 4][l % 32].
+template <bool TA, bool TB, bool VEC>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel_big(GemmArgs g) {
+    constexpr int BT = 128, BK = 32, LS = BT + 32, NQ = BT * BK / 4 / GEMM_THREADS;   // 4 quads per thread
+    __shared__ __attribute__((aligned(16))) float As[2][BK][LS];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BK][LS];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, kh = lane >> 5;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT;
+    const int kbeg = blockIdx.z * g.kchunk;
+    const int kend = min(g.K, kbeg + g.kchunk);
+    // quad q: k-contiguous operands are [row][8 quads], k-strided ones [k][32 quads]
+    auto load_a = [&](int k0, int q) -> f32x4 {
+        if (!TA) {
+            const int m = m0 + (q >> 3), k = k0 + 4 * (q & 7);
+            return load4<VEC>(g.A + (int64_t)m * g.lda + k, m < g.M ? min(4, kend - k) : 0);
+        } else {
+            const int k = k0 + (q >> 5), m = m0 + 4 * (q & 31);
+            return load4<VEC>(g.A + (int64_t)k * g.lda + m, k < kend ? min(4, g.M - m) : 0);
+        }
+    };
+    auto load_b = [&](int k0, int q) -> f32x4 {
+        if (!TB) {
+            const int k = k0 + (q >> 5), n = n0 + 4 * (q & 31);
+            return load4<VEC>(g.B + (int64_t)k * g.ldb + n, k < kend ? min(4, g.N - n) : 0);
+        } else {
+            const int n = n0 + (q >> 3), k = k0 + 4 * (q & 7);
+            return load4<VEC>(g.B + (int64_t)n * g.ldb + k, n < g.N ? min(4, kend - k) : 0);
+        }
+    };
+    auto store_a = [&](int buf, int q, f32x4 v) {
+        if (!TA) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) As[buf][4 * (q & 7) + e][q >> 3] = v[e];
+        } else {
+            *reinterpret_cast<f32x4*>(&As[buf][q >> 5][4 * (q & 31)]) = v;
+        }
+    };
+    auto store_b = [&](int buf, int q, f32x4 v) {
+        if (!TB) {
+            *reinterpret_cast<f32x4*>(&Bs[buf][q >> 5][4 * (q & 31)]) = v;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Bs[buf][4 * (q & 7) + e][q >> 3] = v[e];
+        }
+    };
+    typedef float f32x16 __attribute__((ext_vector_type(16)));
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[x][y][r] = 0.0f;
+    const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    if (ntiles > 0) {
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+            store_a(0, tid + GEMM_THREADS * u, load_a(kbeg, tid + GEMM_THREADS * u));
+            store_b(0, tid + GEMM_THREADS * u, load_b(kbeg, tid + GEMM_THREADS * u));
+        }
+    }
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+        const int buf = kt & 1;
+        f32x4 na[NQ], nb[NQ];
+        const bool more = kt + 1 < ntiles;
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < NQ; ++u) {
+                na[u] = load_a(kbeg + (kt + 1) * BK, tid + GEMM_THREADS * u);
+                nb[u] = load_b(kbeg + (kt + 1) * BK, tid + GEMM_THREADS * u);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < BK / 2; ++s) {
+            const int kk = 2 * s + kh;
+            const float a0 = As[buf][kk][64 * wm + i], a1 = As[buf][kk][64 * wm + 32 + i];
+            const float b0 = Bs[buf][kk][64 * wn + i], b1 = Bs[buf][kk][64 * wn + 32 + i];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < NQ; ++u) {
+                store_a(buf ^ 1, tid + GEMM_THREADS * u, na[u]);
+                store_b(buf ^ 1, tid + GEMM_THREADS * u, nb[u]);
+            }
+        }
+        __syncthreads();
+    }
+    // two-pass epilogue (operand loads first, as in gemm_kernel), one 32 x 32 block at a time
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int col = n0 + 64 * wn + 32 * y + i;
+            const float bv = (g.splits <= 1 && g.bias && col < g.N) ? g.bias[col] : 0.0f;
+            float in_c[16], in_a[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + 64 * wm + 32 * x + 8 * (r >> 2) + 4 * kh + (r & 3);
+                const bool ok = g.splits <= 1 && row < g.M && col < g.N;
+                in_c[r] = (ok && g.accum) ? g.C[(int64_t)row * g.ldc + col] : 0.0f;
+                in_a[r] = (ok && g.epi == EPI_DTANH) ? g.aux[(int64_t)row * g.ldaux + col] : 0.0f;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + 64 * wm + 32 * x + 8 * (r >> 2) + 4 * kh + (r & 3);
+                if (row >= g.M || col >= g.N) continue;
+                if (g.splits > 1)
+                    g.part[((int64_t)blockIdx.z * g.M + row) * g.N + col] = acc[x][y][r];
+                else
+                    g.C[(int64_t)row * g.ldc + col] = epi_value(g, acc[x][y][r], bv, in_a[r], in_c[r]);
+            }
+        }
 }
 
 // split-K: C = epi(sum_z part[z]) in a fixed order.  64 outputs per block, 4 interleaved
@@ -217,25 +370,32 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
     if (g.M <= 0 || g.N <= 0) return hipSuccess;
     // 128 x 128 tiles (half the operand re-reads, 4x the MFMAs per LDS read) when both
     // dimensions fill them; 64 x 64 otherwise
-#ifdef RD_GEMM_BT   // diagnostic builds (build.py --variant): force one tile size
+#ifdef RD_GEMM_BT   // diagnostic builds (build.py --variant): force one tile size / kernel
     const int BT = RD_GEMM_BT;
 #else
-    const int BT = 64;   // measured (scripts/gemm_tile_compare.sh): 64 beats 128 on every LSTM shape
+    // the 16x16x4 64 x 64 kernel everywhere: on every LSTM / PPO shape it beats both the
+    // 16x16x4 128-tile variant and the 32x32x2 128 x 128 x 32 kernel (BT 129), which are kept
+    // for diagnostic builds (scripts/gemm_tile_compare.sh): the LSTM's GEMMs
+    // are short-K (recurrent, K = 200) or weight gradients whose operands stream from HBM,
+    // where 8 resident 64-tile workgroups per CU keep more loads in flight than 2 big ones
+    const int BT = 64;
 #endif
-    const int tm = (g.M + BT - 1) / BT, tn = (g.N + BT - 1) / BT;
+    const int TILE = BT == 129 ? 128 : BT;
+    const int tm = (g.M + TILE - 1) / TILE, tn = (g.N + TILE - 1) / TILE;
     const int tiles = tm * tn;
     // split K when the tile grid cannot fill the chip (~8 workgroups per CU, so the loads of
     // one tile's K-loop hide behind the others' MFMAs) and K is long
     int splits = 1;
-    if (part && tiles < 8 * cus && g.K >= 512) {
-        splits = (8 * cus + tiles - 1) / tiles;
+    const int target = (BT == 129 ? 2 : 8) * cus;   // the big kernel's 80 KB of LDS: 2 per CU
+    if (part && tiles < target && g.K >= 512) {
+        splits = (target + tiles - 1) / tiles;
         const int maxs = g.K / 256 < 256 ? g.K / 256 : 256;   // >= 16 k-tiles per split, <= 256 partials
         if (splits > maxs) splits = maxs;
         while (splits > 1 && (int64_t)splits * g.M * g.N > part_floats) --splits;
     }
     g.splits = splits;
     g.part = part;
-    g.kchunk = splits > 1 ? (((g.K + splits - 1) / splits + TK - 1) / TK) * TK : g.K;
+    g.kchunk = splits > 1 ? (((g.K + splits - 1) / splits + 31) / 32) * 32 : g.K;   // multiple of both K tiles
     if (splits > 1) g.splits = (g.K + g.kchunk - 1) / g.kchunk;
     const bool vec = ((uintptr_t)g.A % 16 == 0) && ((uintptr_t)g.B % 16 == 0) && g.lda % 4 == 0 && g.ldb % 4 == 0;
     dim3 grid(tn, tm, g.splits);
@@ -253,11 +413,26 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
         else if (g.ta && !g.tb) RDG_LAUNCH(BT_, true, false, false);       \
         else RDG_LAUNCH(BT_, true, true, false);                            \
     }
-    if (BT == 128) {
+#define RDG_LAUNCH_BIG(TA_, TB_, V_) \
+    hipLaunchKernelGGL((gemm_kernel_big<TA_, TB_, V_>), grid, dim3(GEMM_THREADS), 0, st, g)
+    if (BT == 129) {
+        if (vec) {
+            if (!g.ta && !g.tb) RDG_LAUNCH_BIG(false, false, true);
+            else if (!g.ta && g.tb) RDG_LAUNCH_BIG(false, true, true);
+            else if (g.ta && !g.tb) RDG_LAUNCH_BIG(true, false, true);
+            else RDG_LAUNCH_BIG(true, true, true);
+        } else {
+            if (!g.ta && !g.tb) RDG_LAUNCH_BIG(false, false, false);
+            else if (!g.ta && g.tb) RDG_LAUNCH_BIG(false, true, false);
+            else if (g.ta && !g.tb) RDG_LAUNCH_BIG(true, false, false);
+            else RDG_LAUNCH_BIG(true, true, false);
+        }
+    } else if (BT == 128) {
         RDG_DISPATCH(128)
     } else {
         RDG_DISPATCH(64)
     }
+#undef RDG_LAUNCH_BIG
 #undef RDG_DISPATCH
 #undef RDG_LAUNCH
     hipError_t e = hipGetLastError();
