@@ -201,6 +201,35 @@ class StudentLstmTrainer:
         allreduce_sum_(self._grad, self.pg)
         self.apply()
 
+    def graph_step(self, windows: int):
+        """One training step (rdl_step, zero initial state) for `windows` windows captured
+        into a HIP graph: returns step(ob, prev_pdflat, t_pdflat), which copies the inputs
+        into the graph's static buffers and replays (no host launches; the reference's
+        20-window step is launch-bound).  Replays are the same computation as step()."""
+        if self.world != 1:
+            raise RuntimeError("graph capture is for the single-rank step")
+        T, B = self.T, int(windows)
+        if not 0 < B <= self.cfg.max_windows:
+            raise ValueError(f"bad window count {B}")
+        ob = torch.zeros(T, B, OBSPACE_SHAPE, device=self.device)
+        prev = torch.zeros(T, B, PDFLAT_SHAPE, device=self.device)
+        tgt = torch.zeros(T, B, PDFLAT_SHAPE, device=self.device)
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g):
+            self._sync_stream()
+            nat.check(self._lib.rdl_step(self._h, nat.ptr(ob), nat.ptr(prev), nat.ptr(tgt), None, B), "rdl_step")
+        self._sync_stream()
+
+        def step(o, p, t):
+            ob.copy_(torch.as_tensor(o, dtype=torch.float32).reshape(ob.shape))
+            prev.copy_(torch.as_tensor(p, dtype=torch.float32).reshape(prev.shape))
+            tgt.copy_(torch.as_tensor(t, dtype=torch.float32).reshape(tgt.shape))
+            g.replay()
+
+        step.graph, step.inputs = g, (ob, prev, tgt)
+        return step
+
     def grad(self) -> torch.Tensor:
         return self._grad
 

@@ -192,6 +192,28 @@ class StudentMlpTrainer:
         allreduce_sum_(self._grad, self.pg)
         self.apply()
 
+    def graph_step(self, n: int):
+        """One training step (rdm_step) on n rows captured into a HIP graph: returns
+        step(x, t_pdflat), which copies into the graph's static buffers and replays."""
+        if self.world != 1:
+            raise RuntimeError("graph capture is for the single-rank step")
+        x = torch.zeros(int(n), IN_DIM, device=self.device)
+        t = torch.zeros(int(n), PDFLAT_SHAPE, device=self.device)
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g):
+            self._sync_stream()
+            nat.check(self._lib.rdm_step(self._h, nat.ptr(x), nat.ptr(t), int(n)), "rdm_step")
+        self._sync_stream()
+
+        def step(xv, tv):
+            x.copy_(torch.as_tensor(xv, dtype=torch.float32).reshape(x.shape))
+            t.copy_(torch.as_tensor(tv, dtype=torch.float32).reshape(t.shape))
+            g.replay()
+
+        step.graph, step.inputs = g, (x, t)
+        return step
+
     def grad(self) -> torch.Tensor:
         return self._grad
 

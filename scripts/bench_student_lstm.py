@@ -39,8 +39,11 @@ def main():
         tgt = torch.rand(T, B, 4, device="cuda:0") - 0.5
         iters = max(3, min(50, int(5e5 // (B * T + 1000))))
         ts = timeit(lambda: tr.step(ob, prev, tgt), iters)
+        gstep = tr.graph_step(B)
+        tg = timeit(lambda: gstep(ob, prev, tgt), iters)
         tf = timeit(lambda: tr.forward(ob, prev), iters)
         print(json.dumps({"windows": B, "T": T, "step_ms": ts * 1e3, "window_steps_per_s": B * T / ts,
+                          "graph_step_ms": tg * 1e3,
                           "fwd_ms": tf * 1e3, "tflops": FLOP * B * T / ts / 1e12,
                           "mfma_frac": FLOP * B * T / ts / PEAK}), flush=True)
         tr.close()

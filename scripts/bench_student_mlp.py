@@ -39,8 +39,10 @@ def main():
         t = torch.rand(n, 4, device="cuda:0") - 0.5
         iters = max(5, min(200, int(2e8 // (n * 100 + 1e5))))
         ts = timeit(lambda: tr.step(x, t), iters)
+        gstep = tr.graph_step(n)
+        tg = timeit(lambda: gstep(x, t), iters)
         tf = timeit(lambda: tr.forward(x), iters)
-        print(json.dumps({"rows": n, "step_us": ts * 1e6, "rows_per_s": n / ts, "fwd_us": tf * 1e6,
+        print(json.dumps({"rows": n, "step_us": ts * 1e6, "rows_per_s": n / ts, "graph_step_us": tg * 1e6, "fwd_us": tf * 1e6,
                           "fwd_rows_per_s": n / tf, "tflops": FLOP_TRAIN * n / ts / 1e12,
                           "mfma_frac_step": FLOP_TRAIN * n / ts / PEAK_F32_MFMA}), flush=True)
 

@@ -172,3 +172,17 @@ def test_bad_arguments_raise():
         tr.forward(_t(ob), _t(prev))           # 21 windows > max_windows 20
     with pytest.raises(ValueError):
         tr.forward(_t(ob[:5, :4]), _t(prev[:5, :4]))   # T = 5 != 10
+
+
+def test_graph_step_equals_eager():
+    T, B = 10, 20
+    ob, prev, t = _batch(T, B, 21)
+    eager, graphed = _trainer(T, B, keep_prob=0.5, seed=4), _trainer(T, B, keep_prob=0.5, seed=4)
+    step = graphed.graph_step(B)
+    for _ in range(3):
+        eager.step(_t(ob), _t(prev), _t(t))
+        step(_t(ob).to(DEV), _t(prev).to(DEV), _t(t).to(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(eager.params(), graphed.params())
+    assert eager.counter() == graphed.counter() == 3
+    np.testing.assert_array_equal(eager.metrics(3), graphed.metrics(3))

@@ -145,3 +145,15 @@ def test_bad_arguments_raise():
     mis = torch.zeros(65, device=DEV)[1:].view(4, 16)   # 4-byte offset: not 16-B aligned
     with pytest.raises(NativeError):
         tr.rollout(mis, torch.zeros(4, 4, device=DEV))
+
+
+def test_graph_step_equals_eager():
+    x, t = _batch(200, 13)
+    eager, graphed = _trainer("kl", keep_prob=0.5, seed=3), _trainer("kl", keep_prob=0.5, seed=3)
+    step = graphed.graph_step(200)
+    for _ in range(3):
+        eager.step(torch.from_numpy(x), torch.from_numpy(t))
+        step(torch.from_numpy(x).to(DEV), torch.from_numpy(t).to(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(eager.params(), graphed.params())
+    np.testing.assert_array_equal(eager.metrics(3), graphed.metrics(3))
