@@ -4,6 +4,7 @@ algorithmic FLOPs (1,337,472 per window-step: forward 451,776 + data grads 433,9
 grads 451,776), forward-only rate."""
 import json
 import sys
+import time
 
 import torch
 
@@ -30,8 +31,34 @@ def timeit(fn, iters, warm=3):
     return s.elapsed_time(e) / 1e3 / iters
 
 
+def cpu_baseline(B=20, seconds=3.0):
+    """The oracle (numpy f64, one core): the same truncated-BPTT step on [T, B] windows."""
+    import threadpoolctl
+    import numpy as np
+
+    from oracle import lstm_np as ln
+    from oracle import policy_np as pn
+    rs = np.random.RandomState(0)
+    ob, prev = rs.uniform(-1, 1, (T, B, 11)), rs.uniform(-1, 0, (T, B, 4))
+    tgt = np.concatenate([rs.uniform(-.5, .5, (T, B, 2)), rs.uniform(-1, -.2, (T, B, 2))], 2)
+    p = ln.init(3)
+    opt = pn.AdamTF1(ln.P_LSTM, lr=1e-3)
+    with threadpoolctl.threadpool_limits(1):
+        k, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            fw = ln.forward(p, ob, prev)
+            _, d, _ = ln.loss_and_dout(fw["pdflat"], tgt, "kl", T * B)
+            p = opt.step(p, ln.backward(p, fw, d))
+            k += 1
+        el = time.perf_counter() - t0
+    return {"cpu_window_steps_per_s": B * T * k / el, "cpu_step_ms": el / k * 1e3, "cpu_windows": B,
+            "cpu_cores": 1, "cpu_kind": "oracle/lstm_np.py (numpy f64)"}
+
+
 def main():
     sizes = [int(a) for a in sys.argv[1:]] or [20, 1024, 16384]
+    if not sys.argv[1:]:
+        print(json.dumps(cpu_baseline()), flush=True)
     for B in sizes:
         tr = StudentLstmTrainer(StudentLstmConfig(loss="kl", steps=T, max_windows=B), device="cuda:0")
         ob = torch.rand(T, B, 11, device="cuda:0") * 2 - 1

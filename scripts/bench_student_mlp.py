@@ -6,6 +6,7 @@ forward-only rows/s.
 """
 import json
 import sys
+import time
 
 import torch
 
@@ -31,8 +32,34 @@ def timeit(fn, iters, warm=5):
     return s.elapsed_time(e) / 1e3 / iters
 
 
+def cpu_baseline(n=200, seconds=3.0):
+    """The oracle (numpy f64, one core) doing the same training step on n rows."""
+    import threadpoolctl
+    import numpy as np
+
+    from oracle import policy_np as pn
+    from oracle import refnet_np as rn
+    rs = np.random.RandomState(0)
+    x = rs.uniform(-1, 1, (n, 16))
+    t = np.concatenate([rs.uniform(-.5, .5, (n, 2)), rs.uniform(-1, -.2, (n, 2))], 1)
+    p = rn.init(2).astype(np.float32)
+    opt = pn.AdamTF1(rn.P_REF)
+    with threadpoolctl.threadpool_limits(1):
+        k, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            fw = rn.forward(p, x)
+            _, d, _ = rn.loss_and_dout(fw["pdflat"], t, "kl", n)
+            p = opt.step(p, rn.backward(p, fw, d))
+            k += 1
+        el = time.perf_counter() - t0
+    return {"cpu_rows_per_s": n * k / el, "cpu_step_us": el / k * 1e6, "cpu_rows": n, "cpu_cores": 1,
+            "cpu_kind": "oracle/refnet_np.py (numpy f64)"}
+
+
 def main():
     sizes = [int(a) for a in sys.argv[1:]] or [200, 4096, 65536, 262144, 1048576]
+    if not sys.argv[1:]:
+        print(json.dumps(cpu_baseline()), flush=True)
     tr = StudentMlpTrainer(StudentMlpConfig(loss="kl"), device="cuda:0")
     for n in sizes:
         x = torch.rand(n, 16, device="cuda:0") * 2 - 1
