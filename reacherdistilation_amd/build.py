@@ -65,9 +65,11 @@ def build_stamps():
 
 
 def build_variant(name, *defines):
-    """Diagnostic/ablation build (e.g. RD_ABL_TANH) as libreacher_<name>.so; never the product."""
+    """Diagnostic/ablation build (e.g. RD_ABL_TANH, or a compiler flag such as
+    -fno-slp-vectorize) as libreacher_<name>.so; never the product."""
     out = os.path.join(HERE, f"libreacher_{name}.so")
-    subprocess.check_call([HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-o", out, *sources()])
+    opts = [d if d.startswith("-") else f"-D{d}" for d in defines]
+    subprocess.check_call([HIPCC, *FLAGS, *opts, "-o", out, *sources()])
     return out
 
 

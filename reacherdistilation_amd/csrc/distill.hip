@@ -104,6 +104,7 @@ struct RolloutArgs {
     float* ws;                             // [gridDim.x][P_PAD]
     int loss, act_student, stagger;
     float inv_n_global;
+    int gs;                                // envs per group (16, 32 or 64)
     unsigned long long* dbg;               // RD_STAMPS builds: [grid*WAVES][16] stamp sums
     const float* obs_in;                   // observation-batch mode: [n][11] rows, no env step
     const float* timg;                     // prepacked LDS images (pack_net_kernel)
@@ -494,10 +495,24 @@ __global__ __launch_bounds__(256) void pack_net_kernel(const float* net, float* 
     for (int p = x; p < P_TOT; p += gridDim.x * 256) pack_param(img, p, net[p], student != 0, bf16 != 0);
 }
 
-__device__ __forceinline__ void copy_image(float* L, const float* img, int floats, int nthreads) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(img);
-    f32x4* dst = reinterpret_cast<f32x4*>(L);
-    for (int i = threadIdx.x; i < floats / 4; i += nthreads) dst[i] = src[i];
+// Both rollout images (contiguous in LDS: teacher then student) with every 16-B load of a
+// thread issued before its first LDS store, so a workgroup keeps ~3.7k loads in flight
+// instead of one round trip per loop iteration.
+template <int V4A, int V4B, int NT>
+__device__ __forceinline__ void copy_images(float* L, const float* ta, const float* sb) {
+    constexpr int TOT = V4A + V4B, PER = (TOT + NT - 1) / NT;
+    f32x4 r[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int x = threadIdx.x + u * NT;
+        if (x < V4A) r[u] = reinterpret_cast<const f32x4*>(ta)[x];
+        else if (x < TOT) r[u] = reinterpret_cast<const f32x4*>(sb)[x - V4A];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int x = threadIdx.x + u * NT;
+        if (x < TOT) reinterpret_cast<f32x4*>(L)[x] = r[u];
+    }
 }
 
 // bf16-student forward of a 16-env tile (same outputs/layouts as mlp_forward).
@@ -565,6 +580,37 @@ __device__ __forceinline__ void publish(uint32_t* f, uint32_t v) {
     __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// env.step of this lane's env with the policy's action, the episode clock (lockstep or
+// staggered) and the auto-reset; writes the state back and returns the reward (0 for a lane
+// without an env).  met_n counts the stepped envs.
+__device__ __forceinline__ float env_step_group(const RolloutArgs& a, uint32_t C, int64_t i, bool valid, float act0,
+                                                float act1, rd::State& st, float& met_n) {
+    const uint32_t iu = (uint32_t)i;
+#ifdef RD_ABL_PHYSICS   // ablation build: no dynamics (timing only)
+    const float rew = act0 + act1;
+    st.q0 += 0.01f * act0;
+#else
+    const float rew = rd::env_step<false>(st, act0, act1);
+#endif
+    // episode clock of this env (RDD_STAGGER_GROUP envs share an offset)
+    const int64_t gid = a.env_base + i;
+    const uint32_t u = C + (a.stagger ? (uint32_t)((gid / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);
+    const bool done_step = (u % rd::kEpisodeSteps) == rd::kEpisodeSteps - 1;
+    if (done_step) {
+        float dr[6];
+        rd::philox_draw(a.seed, (uint64_t)gid, u / rd::kEpisodeSteps + 1, dr);
+        rd::env_reset(st, dr);
+    }
+    if (!valid) return 0.0f;
+    float* s = a.state;
+    const int64_t n = a.n;
+    (s + 0 * n)[iu] = st.q0; (s + 1 * n)[iu] = st.q1; (s + 2 * n)[iu] = st.v0; (s + 3 * n)[iu] = st.v1;
+    if (done_step) { (s + 4 * n)[iu] = st.tx; (s + 5 * n)[iu] = st.ty; }
+    (s + 6 * n)[iu] = st.dx; (s + 7 * n)[iu] = st.dy;
+    met_n += 1.0f;
+    return rew;
+}
+
 template <bool BS>   // BS: bf16 student (RDD_DTYPE_BF16)
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
@@ -579,8 +625,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     uint32_t* err = a.ctl + 8;
 
     STAMP(0);
-    copy_image(LT, a.timg, NET, BLOCK);
-    copy_image(LS, a.simg, NET_S, BLOCK);
+    static_assert(NET % 4 == 0 && NET_S % 4 == 0, "16-B images");
+    copy_images<NET / 4, NET_S / 4, BLOCK>(LT, a.timg, a.simg);   // LS = LT + NET
     constexpr int SW3 = BS ? NB_W3 : N_W3, SMU = BS ? NB_MU : N_MU, SRS = BS ? NB_RS : N_RS;
     if (threadIdx.x < PAIRS * 4)
         reinterpret_cast<uint32_t*>(lds + NET + NET_S + (threadIdx.x >> 2) * PSCR + P_FLAGS)[threadIdx.x & 3] = 0u;
@@ -593,17 +639,24 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     __syncthreads();
     STAMP(1);
 
-    const int64_t ngroups = (a.n + GROUP - 1) / GROUP;
+    const int gs = a.gs;   // envs per group: 64, or 32 / 16 to spread a small batch over more pairs
+    const int64_t ngroups = (a.n + gs - 1) / gs;
     const int64_t gstride = (int64_t)gridDim.x * PAIRS;
     const int64_t gfirst = (int64_t)blockIdx.x * PAIRS + pair;
 
+#ifdef RD_PRIO_CONS   // experiment: static issue priority for the consumer half (waves 4-7)
+    if (!producer) __builtin_amdgcn_s_setprio(1);
+#endif
+#ifdef RD_PRIO_PROD
+    if (producer) __builtin_amdgcn_s_setprio(1);
+#endif
     if (producer) {
         // ============================================================ producer wave
         // partial sums: dW3 (env j of this lane, features 16x+4g+r), db3, dlogstd, metrics
         f32x4 gw3a[4], gw3b[4];
 #pragma unroll
         for (int x = 0; x < 4; ++x) gw3a[x] = gw3b[x] = f32x4{0.f, 0.f, 0.f, 0.f};
-        float gb3a = 0, gb3b = 0, gls0 = 0, gls1 = 0, met_l = 0, met_m = 0;
+        float gb3a = 0, gb3b = 0, gls0 = 0, gls1 = 0, met_l = 0, met_m = 0, met_r = 0, met_n = 0;
         const float tl0 = a.tnet[P_LS], tl1 = a.tnet[P_LS + 1];
         const float sl0 = a.snet[P_LS], sl1 = a.snet[P_LS + 1];
         const float sv0 = __expf(2.0f * sl0), sv1 = __expf(2.0f * sl1);
@@ -614,18 +667,19 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         for (int64_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
             // the consumer is done with group k-2 (same obs/action buffers)
             if (k >= 2 && !(ok = wait_ge(flags + 2, k - 1, err))) break;
-            const int64_t base = grp * GROUP;
+            const int64_t base = grp * gs;
             const int64_t i = base + lane;
+            const bool lvalid = lane < gs && i < a.n;   // this lane has an env
             float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
             float* act = PS + P_ACT + (k & 1) * GROUP * 2;
+            rd::State st{};   // this lane's env, kept in registers for the env.step after the tiles
             {
                 float ob[OBD];
                 if (a.obs_in) {   // observation-batch mode: rows given by the caller
 #pragma unroll
-                    for (int q = 0; q < OBD; ++q) ob[q] = i < a.n ? a.obs_in[i * OBD + q] : 0.0f;
+                    for (int q = 0; q < OBD; ++q) ob[q] = lvalid ? a.obs_in[i * OBD + q] : 0.0f;
                 } else {
-                    rd::State st{};
-                    if (i < a.n) load_state(a.state, a.n, (uint32_t)i, st);
+                    if (lvalid) load_state(a.state, a.n, (uint32_t)i, st);
                     rd::observe<false>(st, ob);
                 }
                 float* o = obs + lane * SOS;
@@ -634,7 +688,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 st4(o + 8, f32x4{ob[8], ob[9], ob[10], 1.0f});
             }
             wave_sync();
-            const int ntile = (int)min((int64_t)(GROUP / TILE), (a.n - base + TILE - 1) / TILE);
+            const int ntile = (int)min((int64_t)(gs / TILE), (a.n - base + TILE - 1) / TILE);
             for (int t = 0; t < ntile; ++t) {
                 const bool tvalid = base + TILE * t + j < a.n;
                 const float* obt = obs + TILE * t * SOS;
@@ -699,6 +753,19 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 }
                 publish(flags, ++tiles);
             }
+            if (!ok) break;
+            // ---------------------------------------------------------- env.step (one env per lane)
+            // The producer computed this group's actions itself, so it steps the envs at once:
+            // the consumer's share is then only the gradient tiles, and the pipeline drains
+            // behind the last tile instead of behind the last tile plus a group's physics.
+            STAMP(4);
+            if (a.obs_in) {   // observation-batch mode: no env to step
+                if (lvalid) met_n += 1.0f;
+            } else {
+                wave_sync();   // act[] rows were written by the g = 0 lanes of each tile
+                if (lane < gs) met_r += env_step_group(a, C, i, lvalid, act[lane * 2], act[lane * 2 + 1], st, met_n);
+            }
+            STAMP(5);
         }
         // ------------------------------------------------------------ this wave's share
 #pragma unroll
@@ -713,6 +780,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         gb3a = wave_sum(gb3a); gb3b = wave_sum(gb3b);
         gls0 = wave_sum(gls0); gls1 = wave_sum(gls1);
         met_l = wave_sum(met_l); met_m = wave_sum(met_m);
+        met_r = wave_sum(met_r); met_n = wave_sum(met_n);
         STAMP(6);
         __syncthreads();   // (one of the two barriers every wave meets) weights/scratch are free
         STAMP(9);
@@ -730,6 +798,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         if (lane == 0) {
             R[P_B3] = gb3a; R[P_B3 + 1] = gb3b; R[P_LS] = gls0; R[P_LS + 1] = gls1;
             R[P_TOT + 1] = met_l; R[P_TOT + 2] = met_m;
+            R[P_TOT] = met_r; R[P_TOT + 3] = met_n;
         }
     } else {
         // ============================================================ consumer wave
@@ -743,18 +812,15 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             gW1[x] = f32x4{0.f, 0.f, 0.f, 0.f};
             gb2[x] = 0.0f;
         }
-        float met_r = 0, met_n = 0;
         // student filter of input j for the dW1 A operand (lane-constant)
         const float smu = j < 12 ? LS[SMU + j] : 0.0f, srs = j < 12 ? LS[SRS + j] : 0.0f;
         uint32_t tiles = 0;
         uint32_t k = 0;
         bool ok = true;
         for (int64_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
-            const int64_t base = grp * GROUP;
-            const int64_t i = base + lane;
+            const int64_t base = grp * gs;
             const float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
-            const float* act = PS + P_ACT + (k & 1) * GROUP * 2;
-            const int ntile = (int)min((int64_t)(GROUP / TILE), (a.n - base + TILE - 1) / TILE);
+            const int ntile = (int)min((int64_t)(gs / TILE), (a.n - base + TILE - 1) / TILE);
             for (int t = 0; t < ntile; ++t) {
                 STAMP(2);
                 if (!(ok = wait_ge(flags, tiles + 1, err))) break;
@@ -880,49 +946,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 STAMP(15);
             }
             if (!ok) break;
-            // ---------------------------------------------------------- env.step (one env per lane)
-            STAMP(4);
-            const uint32_t iu = (uint32_t)i;
-            const bool valid = i < a.n;
-            if (a.obs_in) {   // observation-batch mode: no env to step
-                if (valid) met_n += 1.0f;
-                publish(flags + 2, k + 1);
-                continue;
-            }
-            rd::State st{};
-            if (valid) load_state(a.state, a.n, iu, st);
-            const float act0 = act[lane * 2], act1 = act[lane * 2 + 1];
-#ifdef RD_ABL_PHYSICS   // ablation build: no dynamics (timing only)
-            const float rew = act0 + act1;
-            st.q0 += 0.01f * act0;
-#else
-            const float rew = rd::env_step<false>(st, act0, act1);
-#endif
-            // episode clock of this env (RDD_STAGGER_GROUP envs share an offset)
-            const int64_t gid = a.env_base + i;
-            const uint32_t u = C + (a.stagger ? (uint32_t)((gid / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);
-            const bool done_step = (u % rd::kEpisodeSteps) == rd::kEpisodeSteps - 1;
-            if (done_step) {
-                float dr[6];
-                rd::philox_draw(a.seed, (uint64_t)gid, u / rd::kEpisodeSteps + 1, dr);
-                rd::env_reset(st, dr);
-            }
-            if (valid) {
-                float* s = a.state;
-                const int64_t n = a.n;
-                (s + 0 * n)[iu] = st.q0; (s + 1 * n)[iu] = st.q1; (s + 2 * n)[iu] = st.v0; (s + 3 * n)[iu] = st.v1;
-                if (done_step) { (s + 4 * n)[iu] = st.tx; (s + 5 * n)[iu] = st.ty; }
-                (s + 6 * n)[iu] = st.dx; (s + 7 * n)[iu] = st.dy;
-                met_r += rew;
-                met_n += 1.0f;
-            }
-            publish(flags + 2, k + 1);   // obs/action buffers of group k may be reused
-            STAMP(5);
+            publish(flags + 2, k + 1);   // the obs buffer of group k may be reused
         }
         // ------------------------------------------------------------ this wave's share
 #pragma unroll
         for (int x = 0; x < 4; ++x) gb2[x] = xsum32(xsum16(gb2[x]));   // over the k-groups g
-        met_r = wave_sum(met_r); met_n = wave_sum(met_n);
         STAMP(6);
         __syncthreads();   // (one of the two barriers every wave meets) weights/scratch are free
         STAMP(9);
@@ -945,7 +973,6 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb) R[P_B2 + 16 * nb + j] = gb2[nb];
         }
-        if (lane == 0) { R[P_TOT] = met_r; R[P_TOT + 3] = met_n; }
     }
 
     // Both roles passed exactly one s_barrier above (a wave-level count on gfx950, so the
@@ -1139,11 +1166,34 @@ struct rdd_trainer {
     uint32_t* ctl = nullptr;   // [16]: step words, snapshot, [8] hand-off timeout flag
     unsigned long long* dbg = nullptr;   // RD_STAMPS builds only
     int last_grid = 0;                   // workgroups of the last rollout (rows of ws to reduce)
+    int ws_rows = 0;                     // rows of ws (the device's CU count, or cfg.grid)
+    int gs = GROUP;                      // envs per group of the env rollout
     int accum = 1;                       // rollouts per optimiser step (MSE normalisation)
 
 };
 
 namespace {
+
+// Envs per group (one producer/consumer pair steps a group of gs envs, gs/16 tiles at a
+// time): 64 fills every lane of the physics and is fastest from one group per pair up
+// (measured: c3 = one 64-env group per pair 39.6 us vs 41.9 with 32-env groups); below
+// that a pair's tiles run serially while most CUs idle, so small batches use 32- or 16-env
+// groups over more pairs (c2, 4,096 envs: 19.1 us per launch vs 35.4 with 64-env groups).
+// RDD_GROUP_ENVS=16|32|64 overrides (measurement only).
+int group_envs(int64_t n, int pairs_total) {
+    if (const char* e = getenv("RDD_GROUP_ENVS")) {
+        const int v = atoi(e);
+        if (v == 16 || v == 32 || v == 64) return v;
+    }
+    if (n >= (int64_t)GROUP * pairs_total) return 64;
+    if (n >= (int64_t)32 * pairs_total) return 32;
+    return 16;
+}
+
+int grid_for(int64_t n, int gs, int cap) {
+    const int64_t want = ((n + gs - 1) / gs + PAIRS - 1) / PAIRS;   // one group per pair at least
+    return (int)(want < cap ? want : cap);
+}
 
 int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs = 0, int64_t n_obs_global = 0) {
     RolloutArgs a;
@@ -1164,10 +1214,11 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     a.dbg = t->dbg;
     // MSE averages over the envs of all ranks and over the accum_steps rollouts of one optimiser step
     a.inv_n_global = obs_in ? 1.0f / (float)n_obs_global : 1.0f / ((float)t->cfg.n_envs_global * (float)t->accum);
-    int grid = t->grid;   // the workspace holds t->grid partial rows
+    int grid = t->grid;   // <= t->ws_rows, the partial rows the workspace holds
+    a.gs = t->gs;
     if (obs_in) {
-        const int64_t want = ((n_obs + GROUP - 1) / GROUP + PAIRS - 1) / PAIRS;
-        grid = (int)(want < t->grid ? want : t->grid);
+        a.gs = group_envs(n_obs, t->ws_rows * PAIRS);
+        grid = grid_for(n_obs, a.gs, t->ws_rows);
     }
     t->last_grid = grid;
     if (t->cfg.student_dtype == RDD_DTYPE_BF16)
@@ -1236,10 +1287,10 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     t->accum = cfg->accum_steps > 1 ? cfg->accum_steps : 1;
     t->device = device;
     t->stream = (hipStream_t)hip_stream;
-    const int64_t ngroups = (cfg->n_envs + GROUP - 1) / GROUP;
-    const int64_t want = (ngroups + PAIRS - 1) / PAIRS;   // one group per producer/consumer pair
     const int cap = cfg->grid > 0 ? cfg->grid : num_cus(device);
-    t->grid = (int)(want < cap ? want : cap);
+    t->ws_rows = cap;
+    t->gs = group_envs(cfg->n_envs, cap * PAIRS);
+    t->grid = grid_for(cfg->n_envs, t->gs, cap);
     t->last_grid = t->grid;
     const size_t netf = P_TOT + 2 * OBD;
     hipError_t e = hipSuccess;
@@ -1256,7 +1307,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     alloc((void**)&t->v, sizeof(float) * P_TOT);
     alloc((void**)&t->own_grad, sizeof(float) * P_TOT);
     t->grad = t->own_grad;
-    alloc((void**)&t->ws, sizeof(float) * (size_t)t->grid * P_PAD);
+    alloc((void**)&t->ws, sizeof(float) * (size_t)t->ws_rows * P_PAD);
     alloc((void**)&t->hist, sizeof(float) * (size_t)t->cfg.metrics_len * N_MET);
     alloc((void**)&t->ctl, sizeof(uint32_t) * 16);
 #ifdef RD_STAMPS

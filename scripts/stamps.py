@@ -56,7 +56,7 @@ def main():
     res["consumer_slot_read"] = float(np.median(d(3, 13)[~prod]))
     res["consumer_dw2_dh1"] = float(np.median(d(13, 14)[~prod]))
     res["consumer_dz1_dw1"] = float(np.median(d(14, 15)[~prod]))
-    res["consumer_physics"] = float(np.median(d(4, 5)[~prod]))
+    res["producer_physics"] = float(np.median(d(4, 5)[prod]))
     # per wave slot (0-3 dispatched first; w and w+4 share a SIMD): time to finish the groups
     widx = np.flatnonzero(active) % 8
     res["finish_by_wave_slot"] = [float(np.median(d(0, 6)[widx == w])) for w in range(8)]
