@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--accum", type=int, default=50,
                     help="also time K env-steps per optimiser step (SURVEY §8d: K = 50 = one episode); 0 = skip")
+    ap.add_argument("--conv-steps", type=int, default=5000,
+                    help="convergence leg: optimiser steps allowed to reach student action-MSE < 1e-3; 0 = skip")
     return ap.parse_args()
 
 
@@ -205,6 +207,39 @@ def cpu_baseline(workload, seconds, threads):
                        f"OpenMP {threads} threads")
 
 
+def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=100):
+    """North-star check: optimiser steps (one per env step, the reference's lr 1e-4 TF1 Adam)
+    until the student's action-MSE vs the teacher, averaged over the last 10 steps and all
+    ranks, falls below 1e-3 -- against the reference's budget of 5000 episodes x 50 steps =
+    250,000 Adam steps (mlp_train.py:143-204)."""
+    import torch
+    import torch.distributed as dist
+
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
+                                      student_dtype=sdt), device=dev, rank=rank, world_size=world)
+    t0 = time.perf_counter()
+    steps, mse, hit = 0, float("nan"), None
+    while steps < max_steps:
+        for _ in range(chunk):
+            tr.step()
+        steps += chunk
+        met = tr.metrics(10)
+        mt = torch.tensor(met.sum(0), dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(mt)
+        mse = float(mt[2] / (2 * mt[3]))
+        if mse < target:
+            hit = steps
+            break
+    el = time.perf_counter() - t0
+    tr.close()
+    return {"target_mse": target, "lr": lr, "loss": wl["loss"], "steps_checked_every": chunk,
+            "opt_steps_to_target": hit, "env_steps_to_target": None if hit is None else hit * n * world,
+            "reference_budget_opt_steps": 5000 * 50, "student_mse_final": mse, "opt_steps_run": steps,
+            "seconds": el}
+
+
 def main():
     args = parse()
     import torch
@@ -299,6 +334,10 @@ def main():
                  "replicas_identical": tk.replicas_identical() if world > 1 else True}
         tk.close()
 
+    conv = None
+    if args.conv_steps > 0:
+        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps)
+
     # student action-MSE vs teacher over the last steps (all ranks)
     met = tr.metrics(min(10, tr.counter()))
     mt = torch.tensor(met.sum(0), dtype=torch.float64, device=dev)
@@ -343,6 +382,8 @@ def main():
         }
         if accum is not None:
             out["accum"] = accum
+        if conv is not None:
+            out["convergence"] = conv
         out["roofline_env"] = env_roofline(dev)
         out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / copy_gbs
         if world == 1 and not args.no_cpu_baseline:
