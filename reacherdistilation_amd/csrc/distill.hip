@@ -91,7 +91,17 @@ constexpr int PSCR = P_FLAGS + 4;
 constexpr int LDS_FLOATS = NET + NET_S + PAIRS * PSCR;
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
 static_assert(PSCR % 4 == 0 && P_H1T % 4 == 0 && P_DZT % 4 == 0 && P_SA % 4 == 0, "16-B aligned scratch");
-static_assert(PAIRS * P_PAD <= LDS_FLOATS, "final reduction must fit in the LDS");
+// Final per-workgroup reduction: pair p fills LDS region p.  The 76 rows of 64 that hold
+// W1 (with b1 as row 11) and W2 are stored with a row stride of 68 floats, so that the
+// consumer's register-layout writes (lane (g, j) -> row 4g + r, column j) hit 64 distinct
+// banks; everything after W2 follows at +304 (region of RPAD floats).
+constexpr int RROW = 68;
+constexpr int RSHIFT = (P_B2 / HID) * (RROW - HID);   // 304
+constexpr int RPAD = P_PAD + RSHIFT;
+static_assert(P_B1 == P_W1 + OBD * HID && P_W2 == P_B1 + HID && P_B2 % HID == 0, "W1|b1|W2 rows");
+static_assert(PAIRS * RPAD <= LDS_FLOATS && RPAD % 4 == 0 && P_PAD % 4 == 0, "final reduction must fit in the LDS");
+__device__ __forceinline__ int ridx(int p) { return p < P_B2 ? (p >> 6) * RROW + (p & 63) : p + RSHIFT; }
+[[maybe_unused]] constexpr int NSTAMP = 24;                      // RD_STAMPS debug slots per wave (scripts/stamps.py)
 constexpr uint32_t SPIN_LIMIT = 1u << 22;       // ~0.1 s of s_sleep: a broken hand-off ends the launch
 
 struct RolloutArgs {
@@ -105,7 +115,7 @@ struct RolloutArgs {
     int loss, act_student, stagger;
     float inv_n_global;
     int gs;                                // envs per group (16, 32 or 64)
-    unsigned long long* dbg;               // RD_STAMPS builds: [grid*WAVES][16] stamp sums
+    unsigned long long* dbg;               // RD_STAMPS builds: [grid*WAVES][NSTAMP] stamp sums
     const float* obs_in;                   // observation-batch mode: [n][11] rows, no env step
     const float* timg;                     // prepacked LDS images (pack_net_kernel)
     const float* simg;
@@ -167,10 +177,19 @@ __device__ __forceinline__ void load_state(const float* s, int64_t n, uint32_t i
         unsigned long long t_;                                                          \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
         __builtin_amdgcn_sched_barrier(0);                                              \
-        if (lane == 0 && a.dbg) a.dbg[(blockIdx.x * WAVES + wave) * 16 + (idx)] += t_;   \
+        if (lane == 0 && a.dbg) a.dbg[(blockIdx.x * WAVES + wave) * NSTAMP + (idx)] += t_;   \
+    } while (0)
+// s_memrealtime (100 MHz) at kernel start/end: with the s_memtime stamps, the shader clock
+#define RTSTAMP(idx)                                                                    \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                 \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        if (lane == 0 && a.dbg) a.dbg[(blockIdx.x * WAVES + wave) * NSTAMP + (idx)] += t_;   \
     } while (0)
 #else
 #define STAMP(idx) do {} while (0)
+#define RTSTAMP(idx) do {} while (0)
 #endif
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
@@ -624,7 +643,17 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     uint32_t* flags = reinterpret_cast<uint32_t*>(lds + NET + NET_S + pair * PSCR + P_FLAGS);
     uint32_t* err = a.ctl + 8;
 
+    RTSTAMP(16);
     STAMP(0);
+    const int gs = a.gs;   // envs per group: 64, or 32 / 16 to spread a small batch over more pairs
+    const int64_t ngroups = (a.n + gs - 1) / gs;
+    const int64_t gstride = (int64_t)gridDim.x * PAIRS;
+    const int64_t gfirst = (int64_t)blockIdx.x * PAIRS + pair;
+    // a producer's first group of envs: its state loads are issued before the image copy so
+    // that their HBM latency overlaps the prologue
+    rd::State st0{};
+    if (producer && !a.obs_in && gfirst < ngroups && lane < gs && gfirst * gs + lane < a.n)
+        load_state(a.state, a.n, (uint32_t)(gfirst * gs + lane), st0);
     static_assert(NET % 4 == 0 && NET_S % 4 == 0, "16-B images");
     copy_images<NET / 4, NET_S / 4, BLOCK>(LT, a.timg, a.simg);   // LS = LT + NET
     constexpr int SW3 = BS ? NB_W3 : N_W3, SMU = BS ? NB_MU : N_MU, SRS = BS ? NB_RS : N_RS;
@@ -639,17 +668,6 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     __syncthreads();
     STAMP(1);
 
-    const int gs = a.gs;   // envs per group: 64, or 32 / 16 to spread a small batch over more pairs
-    const int64_t ngroups = (a.n + gs - 1) / gs;
-    const int64_t gstride = (int64_t)gridDim.x * PAIRS;
-    const int64_t gfirst = (int64_t)blockIdx.x * PAIRS + pair;
-
-#ifdef RD_PRIO_CONS   // experiment: static issue priority for the consumer half (waves 4-7)
-    if (!producer) __builtin_amdgcn_s_setprio(1);
-#endif
-#ifdef RD_PRIO_PROD
-    if (producer) __builtin_amdgcn_s_setprio(1);
-#endif
     if (producer) {
         // ============================================================ producer wave
         // partial sums: dW3 (env j of this lane, features 16x+4g+r), db3, dlogstd, metrics
@@ -667,6 +685,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         for (int64_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
             // the consumer is done with group k-2 (same obs/action buffers)
             if (k >= 2 && !(ok = wait_ge(flags + 2, k - 1, err))) break;
+            STAMP(8);
             const int64_t base = grp * gs;
             const int64_t i = base + lane;
             const bool lvalid = lane < gs && i < a.n;   // this lane has an env
@@ -679,7 +698,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
 #pragma unroll
                     for (int q = 0; q < OBD; ++q) ob[q] = lvalid ? a.obs_in[i * OBD + q] : 0.0f;
                 } else {
-                    if (lvalid) load_state(a.state, a.n, (uint32_t)i, st);
+                    if (k == 0) st = st0;
+                    else if (lvalid) load_state(a.state, a.n, (uint32_t)i, st);
                     rd::observe<false>(st, ob);
                 }
                 float* o = obs + lane * SOS;
@@ -687,6 +707,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 st4(o + 4, f32x4{ob[4], ob[5], ob[6], ob[7]});
                 st4(o + 8, f32x4{ob[8], ob[9], ob[10], 1.0f});
             }
+            STAMP(11);
             wave_sync();
             const int ntile = (int)min((int64_t)(gs / TILE), (a.n - base + TILE - 1) / TILE);
             for (int t = 0; t < ntile; ++t) {
@@ -784,7 +805,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         STAMP(6);
         __syncthreads();   // (one of the two barriers every wave meets) weights/scratch are free
         STAMP(9);
-        float* R = lds + pair * P_PAD;   // pair p fills region p; its two waves write disjoint entries
+        float* R = lds + pair * RPAD + RSHIFT;   // pair p fills region p (entries past W2: ridx = p + RSHIFT)
         if (j == 0) {
 #pragma unroll
             for (int fb = 0; fb < 4; ++fb)
@@ -954,34 +975,39 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         STAMP(6);
         __syncthreads();   // (one of the two barriers every wave meets) weights/scratch are free
         STAMP(9);
-        float* R = lds + pair * P_PAD;
+        float* R = lds + pair * RPAD;   // rows of RROW floats: W1|b1 rows 0..11, W2 rows 12..75
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) R[P_W2 + (16 * mb + 4 * g + r) * HID + 16 * nb + j] = gW2[mb][nb][r];
+                for (int r = 0; r < 4; ++r) R[(12 + 16 * mb + 4 * g + r) * RROW + 16 * nb + j] = gW2[mb][nb][r];
+        if (g < 3) {   // rows 4g + r < 12: W1 rows 0..10 and b1 as row 11
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
+            for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int kk = 4 * g + r;
-                if (kk < OBD) R[P_W1 + kk * HID + 16 * nb + j] = gW1[nb][r];
-                else if (kk == OBD) R[P_B1 + 16 * nb + j] = gW1[nb][r];
-            }
+                for (int r = 0; r < 4; ++r) R[(4 * g + r) * RROW + 16 * nb + j] = gW1[nb][r];
+        }
         if (g == 0) {
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb) R[P_B2 + 16 * nb + j] = gb2[nb];
+            for (int nb = 0; nb < 4; ++nb) R[RSHIFT + P_B2 + 16 * nb + j] = gb2[nb];
         }
     }
 
     // Both roles passed exactly one s_barrier above (a wave-level count on gfx950, so the
     // two call sites pair up); this second one publishes the regions.
     __syncthreads();
-    float* out = a.ws + (int64_t)blockIdx.x * P_PAD;
-    for (int p = threadIdx.x; p < P_PAD; p += BLOCK)
-        out[p] = (lds[p] + lds[P_PAD + p]) + (lds[2 * P_PAD + p] + lds[3 * P_PAD + p]);
+    f32x4* out = reinterpret_cast<f32x4*>(a.ws + (int64_t)blockIdx.x * P_PAD);
+#pragma unroll
+    for (int u = 0; u < (P_PAD / 4 + BLOCK - 1) / BLOCK; ++u) {
+        const int p4 = threadIdx.x + u * BLOCK;
+        if (p4 < P_PAD / 4) {
+            const int q = ridx(4 * p4);   // 4 | 64: the four entries stay contiguous
+            out[p4] = (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q));
+        }
+    }
     STAMP(7);
+    RTSTAMP(17);
 }
 
 // ctl words: [0] env steps C (the episode clocks), [1] optimiser steps S (metrics ring),
@@ -1311,7 +1337,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     alloc((void**)&t->hist, sizeof(float) * (size_t)t->cfg.metrics_len * N_MET);
     alloc((void**)&t->ctl, sizeof(uint32_t) * 16);
 #ifdef RD_STAMPS
-    alloc((void**)&t->dbg, sizeof(unsigned long long) * (size_t)t->grid * WAVES * 16);
+    alloc((void**)&t->dbg, sizeof(unsigned long long) * (size_t)t->ws_rows * WAVES * NSTAMP);
 #endif
     if (e != hipSuccess) {
         rdd_destroy(t);
@@ -1524,7 +1550,7 @@ int rdd_read_metrics(rdd_trainer* t, int64_t count, double* out) {
 // Diagnostic build only: copy (and zero) the per-wave stamp sums [grid*8][16] to the host.
 int rdd_debug_stamps(rdd_trainer* t, unsigned long long* out, int64_t cap) {
     if (!t || !out || !t->dbg) return rd::set_error(RD_EINVAL, "rdd_debug_stamps: bad argument");
-    const int64_t cnt = (int64_t)t->grid * WAVES * 16;
+    const int64_t cnt = (int64_t)t->ws_rows * WAVES * NSTAMP;
     if (cap < cnt) return rd::set_error(RD_EINVAL, "rdd_debug_stamps: need %lld", (long long)cnt);
     RD_HIP(hipStreamSynchronize(t->stream), "rdd_debug_stamps");
     RD_HIP(hipMemcpy(out, t->dbg, sizeof(unsigned long long) * cnt, hipMemcpyDeviceToHost), "rdd_debug_stamps");

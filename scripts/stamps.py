@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Phase breakdown of rollout_kernel from the RD_STAMPS diagnostic build (per-wave s_memtime
-stamps).  Read SHARES, not absolute lengths: the stamps' waits forbid some overlap.
+stamps, summed per phase over a wave's groups/tiles; s_memrealtime at kernel start/end gives
+the shader clock).  Read SHARES, not absolute lengths: the stamps' waits forbid some overlap,
+and the two waves of a pair share their SIMD, so a phase's interval includes the partner's
+issue.
 usage: RD_LIB=libreacher_stamps.so python scripts/stamps.py [N]"""
 import ctypes
 import json
@@ -14,6 +17,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from reacherdistilation_amd import _native as nat  # noqa: E402
 from reacherdistilation_amd.distill import DistillConfig, DistillTrainer  # noqa: E402
 
+NSTAMP = 24
+
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
@@ -21,46 +26,50 @@ def main():
     lib = nat.load()
     lib.rdd_debug_stamps.restype = ctypes.c_int
     lib.rdd_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
-    buf = np.zeros(1 << 20, np.uint64)
+    buf = np.zeros(1 << 22, np.uint64)
     for _ in range(5):
         tr.step()
-    lib.rdd_debug_stamps(tr._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+    lib.rdd_debug_stamps(tr._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)   # reset the sums
     iters = 20
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
     for _ in range(iters):
         tr.launch(tr.STAGE_ROLLOUT)
         tr.launch(tr.STAGE_REDUCE_APPLY)
+    ev[1].record()
     torch.cuda.synchronize()
     cnt = lib.rdd_debug_stamps(tr._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
-    st = buf[:cnt].reshape(-1, 16).astype(np.float64)
-    active = st[:, 2] > 0
-    st = st[active]
-    d = lambda a, b: (st[:, b] - st[:, a]) / iters  # noqa: E731
-    res = {
-        "n": n, "waves": int(active.sum()),
-        "prologue_load_nets": float(np.median(d(0, 1))),
-        "obs_per_wave": float(np.median(d(2, 3))),
-        "tiles_per_wave": float(np.median(d(3, 4))),
-        "physics_per_wave": float(np.median(d(4, 5))),
-        "group_loop_total": float(np.median(d(2, 5))),
-        "epilogue_barrier_wait": float(np.median(d(6, 9))),
-        "epilogue_reduce": float(np.median(d(9, 7))),
-        "total": float(np.median(d(0, 7))),
-    }
-    prod = (np.flatnonzero(active) % 8) < 4
-    res["producer_teacher_fwd"] = float(np.median(d(10, 11)[prod]))
-    res["producer_student_fwd"] = float(np.median(d(11, 12)[prod]))
-    res["producer_loss_dz2_to_wait"] = float(np.median((d(12, 2))[prod]))
-    res["producer_wait"] = float(np.median(d(2, 3)[prod]))
-    res["producer_slot_write"] = float(np.median((d(3, 10) )[prod]))
-    res["consumer_wait"] = float(np.median(d(2, 3)[~prod]))
-    res["consumer_slot_read"] = float(np.median(d(3, 13)[~prod]))
-    res["consumer_dw2_dh1"] = float(np.median(d(13, 14)[~prod]))
-    res["consumer_dz1_dw1"] = float(np.median(d(14, 15)[~prod]))
-    res["producer_physics"] = float(np.median(d(4, 5)[prod]))
-    # per wave slot (0-3 dispatched first; w and w+4 share a SIMD): time to finish the groups
+    st = buf[:cnt].reshape(-1, NSTAMP).astype(np.float64)
+    active = st[:, 0] > 0
     widx = np.flatnonzero(active) % 8
-    res["finish_by_wave_slot"] = [float(np.median(d(0, 6)[widx == w])) for w in range(8)]
-    res["tiles_by_wave_slot"] = [float(np.median(d(3, 4)[widx == w])) for w in range(8)]
+    st = st[active]
+    prod = widx < 4
+
+    def d(a, b, sel=None):
+        v = (st[:, b] - st[:, a]) / iters
+        return float(np.median(v if sel is None else v[sel]))
+
+    cycles = d(0, 7)
+    real_ns = d(16, 17) * 10.0          # s_memrealtime ticks at 100 MHz
+    res = {
+        "n": n, "waves": int(active.sum()), "step_us_with_reduce": ev[0].elapsed_time(ev[1]) * 1e3 / iters,
+        "kernel_cycles": cycles, "kernel_us_in_kernel_clock": real_ns * 1e-3,
+        "shader_clock_ghz": cycles / real_ns if real_ns > 0 else None,
+        "prologue": d(0, 1),
+        "group_loop": d(1, 6),
+        "producer_obs": d(8, 11, prod),
+        "producer_fwd_tiles": d(10, 12, prod),
+        "producer_wait": d(2, 3, prod),
+        "producer_physics": d(4, 5, prod),
+        "consumer_wait": d(2, 3, ~prod),
+        "consumer_slot_read": d(3, 13, ~prod),
+        "consumer_dw2_dh1": d(13, 14, ~prod),
+        "consumer_dz1_dw1": d(14, 15, ~prod),
+        "epilogue_barrier_wait": d(6, 9),
+        "epilogue_reduce": d(9, 7),
+        # per wave slot (0-3 dispatched first; w and w+4 share a SIMD): time to reach the epilogue
+        "loop_end_by_wave_slot": [float(np.median(((st[:, 6] - st[:, 0]) / iters)[widx == w])) for w in range(8)],
+    }
     print(json.dumps(res))
 
 
