@@ -72,6 +72,11 @@ int rdl_forward(rdl_trainer* t, const float* ob, const float* prev_pdflat, const
 int rdl_rollout(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* t_pdflat,
                 const float* state0, int64_t windows, int64_t windows_global);
 int rdl_apply(rdl_trainer* t);
+/* final_state_batch of the last forward pass (rdl_forward / rdl_rollout / rdl_step) of
+ * `windows` windows, as [2][windows][200] = (c, h): the truncated-BPTT driver feeds it back as
+ * the next window's initial state (backup/lstm_bbpt.py:141-155 fetches it in the training
+ * sess.run); RD_EINVAL if the last pass had another window count */
+int rdl_final_state(rdl_trainer* t, int64_t windows, float* state_out);
 /* sess.run([loss, minimize_adam]) (lstm_train.py:145-160) == rollout + apply */
 int rdl_step(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* t_pdflat,
              const float* state0, int64_t windows);

@@ -283,6 +283,7 @@ struct rdl_trainer {
     float *split = nullptr, *colws = nullptr, *lpart = nullptr, *hist = nullptr;
     int64_t colws_floats = 0;
     uint32_t* ctl = nullptr;
+    int64_t last_B = 0;   // windows of the last forward pass (rdl_final_state)
 };
 
 namespace {
@@ -323,6 +324,7 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     const int T = t->T;
     const int64_t R = (int64_t)T * B;
     const float* P = t->params;
+    t->last_B = B;
     hipLaunchKernelGGL(inputs_kernel, dim3((unsigned)((R * XLD + 255) / 256)), dim3(256), 0, t->stream, ob, prev, P,
                        t->X, R, B, train ? t->cfg.keep_prob : 1.0f, t->cfg.seed, t->cfg.row_base,
                        (const uint32_t*)t->ctl);
@@ -555,6 +557,20 @@ int rdl_forward(rdl_trainer* t, const float* ob, const float* prev_pdflat, const
         RD_HIP(hipMemcpyAsync(state_out + windows * U, t->H + last, sizeof(float) * windows * U,
                               hipMemcpyDeviceToDevice, t->stream), "rdl_forward: state");
     }
+    return RD_OK;
+}
+
+int rdl_final_state(rdl_trainer* t, int64_t windows, float* state_out) {
+    if (!t || !state_out || windows <= 0 || windows != t->last_B)
+        return rd::set_error(RD_EINVAL, "rdl_final_state: no forward pass of %lld windows to read",
+                             (long long)windows);
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(dg.err, "rdl_final_state");
+    const int64_t last = (int64_t)t->T * windows * U;   // rows of step T: (c, h) after the last step
+    RD_HIP(hipMemcpyAsync(state_out, t->Cs + last, sizeof(float) * windows * U, hipMemcpyDeviceToDevice, t->stream),
+           "rdl_final_state");
+    RD_HIP(hipMemcpyAsync(state_out + windows * U, t->H + last, sizeof(float) * windows * U, hipMemcpyDeviceToDevice,
+                          t->stream), "rdl_final_state");
     return RD_OK;
 }
 

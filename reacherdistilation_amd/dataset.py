@@ -111,6 +111,24 @@ class DeviceDataset:
             yield (win[..., F_OB:F_REW].contiguous(), win[..., F_T:F_S].contiguous(),
                    prev[..., :PDFLAT_SHAPE].contiguous(), prev[..., PDFLAT_SHAPE:].contiguous())
 
+    def bptt_batches(self):
+        """The truncated-BPTT variant's windows (reference backup/dataset_bbpt.py:179-193):
+        LSTM_BATCH_SIZE episodes drawn with replacement once, then every start i in
+        [0, EPISODE_STEPS - T) in order -- consecutive windows slide by ONE step, and the
+        driver carries the LSTM state from one window to the next (backup/lstm_bbpt.py:
+        141-158).  Same tuple layout as training_batches()."""
+        n = self.stored()
+        if n == 0:
+            return
+        eps = torch.randint(0, n, (self.B,), generator=self._gen)
+        rec = self.ring[eps.to(self.device)]                          # [B, 50, REC]
+        prev = self._prev(rec)
+        for start in range(EPISODE_STEPS - self.T):
+            win = rec[:, start:start + self.T].transpose(0, 1)
+            p = prev[:, start:start + self.T].transpose(0, 1)
+            yield (win[..., F_OB:F_REW].contiguous(), win[..., F_T:F_S].contiguous(),
+                   p[..., :PDFLAT_SHAPE].contiguous(), p[..., PDFLAT_SHAPE:].contiguous())
+
     def current_prev(self):
         """(prev_pdflat [4], prev_rew [1]) of the record about to be written: the open
         episode's last teacher pdflat and reward, zeros at t = 0 (reference dataset.py:

@@ -81,3 +81,67 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
             if dataset.num_episodes() >= episodes:
                 break
     return st, dataset, losses
+
+
+def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EPISODES, loss: str = "kl",
+               lr: float = 1e-3, keep_prob: float = 1.0, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
+               warmup_episodes: int = 2 * LSTM_BATCH_SIZE, log=print):
+    """The truncated-BPTT variant of the driver (reference backup/lstm_bbpt.py:18-208), same
+    graph, loss and Adam.  After the teacher warm-up (:115-139) each round is
+      * one BPTT pass (:141-158): ``dataset.bptt_batches()`` -- LSTM_BATCH_SIZE episodes, the
+        40 windows that slide by one step -- one Adam step per window, the LSTM state carried
+        from window to window (the step's final_state_batch becomes the next window's
+        initial_state_batch; zero at the start of the pass);
+      * then one whole episode stepped by the student (:160-205): teacher relabel, the test
+        window's query with the carried query state, record with 's', env.step(student mean).
+    Returns (student trainer, dataset, per-episode summed training loss)."""
+    env = make_mujoco_env("Reacher-v2", seed, device=device)
+    teacher = TeacherAgent(restore=restore, path=teacher_path)
+    tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
+    st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
+                                              steps=STEPS_UNROLLED, max_windows=LSTM_BATCH_SIZE), device=device)
+    dataset = DeviceDataset(device=device, seed=seed, batch_size=LSTM_BATCH_SIZE, steps_unrolled=STEPS_UNROLLED)
+    losses = []
+    if not train:
+        return st, dataset, losses
+    ob = env.reset()
+    reward = 0.0
+
+    def teacher_query(o):
+        t, _ = tq.forward(torch.as_tensor(np.asarray(o, np.float32)).view(1, OBSPACE_SHAPE), student=False)
+        return t[0].cpu().numpy()
+
+    log("Begin Training! First Accumulate observation with teacher")
+    while dataset.num_episodes() <= warmup_episodes:
+        t_pdflat = teacher_query(ob)
+        dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, stepped_with="t")
+        ob, reward, new, _ = env.step(t_pdflat[:2])
+        if new:
+            ob = env.reset()
+            dataset.flush()
+    log("Accumulated sufficient data points from teacher. now train")
+
+    query_state = None   # curr_state_batch (lstm_bbpt.py:94)
+    while True:
+        total_loss = 0.0
+        s = None         # zero_state_batch at the start of each pass (:142)
+        for ob_b, t_b, prev_b, _prew_b in dataset.bptt_batches():
+            st.step(ob_b, prev_b, t_b, state0=s)
+            s = st.final_state(LSTM_BATCH_SIZE)
+            total_loss += float(st.metrics(1)[0, 0])
+        new = False
+        while not new:
+            t_pdflat = teacher_query(ob)
+            ob_w, prev_w, _ = dataset.test_windows(ob)
+            out, query_state = st.forward(ob_w, prev_w, query_state)
+            s_pdflat = out[STEPS_UNROLLED - 1, LSTM_BATCH_SIZE - 1].cpu().numpy()
+            dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, s_pdflat=s_pdflat, stepped_with="s")
+            ob, reward, new, _ = env.step(s_pdflat[:2])
+        log("************** Episode {0} ****************".format(dataset.num_episodes()))
+        ob = env.reset()
+        log("recent loss: %f " % total_loss)
+        losses.append(total_loss)
+        dataset.flush()
+        if dataset.num_episodes() >= episodes:
+            break
+    return st, dataset, losses

@@ -54,6 +54,7 @@ nat.register({
     "rdl_bind_grad_buffer": (INT, [P, P]),
     "rdl_get_counter": (INT, [P, ctypes.POINTER(I64)]),
     "rdl_read_metrics": (INT, [P, I64, P]),
+    "rdl_final_state": (INT, [P, I64, P]),
 })
 
 
@@ -229,6 +230,16 @@ class StudentLstmTrainer:
 
         step.graph, step.inputs = g, (ob, prev, tgt)
         return step
+
+    def final_state(self, windows: int) -> torch.Tensor:
+        """final_state_batch [2, B, 200] = (c, h) of the last forward pass over `windows`
+        windows (rollout/step: computed with the parameters before that step's update, as
+        the reference's sess.run([loss, final_state_batch, minimize_adam]) returns it,
+        backup/lstm_bbpt.py:147-155)."""
+        out = torch.empty(2, int(windows), NUM_UNITS, dtype=torch.float32, device=self.device)
+        self._sync_stream()
+        nat.check(self._lib.rdl_final_state(self._h, int(windows), nat.ptr(out)), "rdl_final_state")
+        return out
 
     def grad(self) -> torch.Tensor:
         return self._grad

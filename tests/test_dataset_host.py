@@ -94,3 +94,23 @@ def test_test_windows_carry_the_prev_series(length):
             assert prew_w[row, 19, 0] == 0.5 * want_prev
         else:
             assert not prev_w[row, 19].any() and prew_w[row, 19, 0] == 0
+
+
+def test_bptt_windows_slide_by_one_step_over_fixed_episodes():
+    """backup/dataset_bbpt.py:179-193: one draw of LSTM_BATCH_SIZE episodes, then the windows
+    starting at 0, 1, ..., EPISODE_STEPS - T - 1 in order, each with its prev fields."""
+    ds = DeviceDataset(capacity=8, device="cpu", seed=3)
+    _fill(ds, 6)
+    wins = list(ds.bptt_batches())
+    assert len(wins) == 40
+    first_eps = None
+    for i, (ob, t, prev, prew) in enumerate(wins):
+        assert ob.shape == (10, 20, 11) and prev.shape == (10, 20, 4) and prew.shape == (10, 20, 1)
+        code = ob[..., 0].numpy()
+        ep, step = code // 100, code % 100
+        assert np.all(step == (i + np.arange(10))[:, None])          # start i, consecutive steps
+        first_eps = ep[0] if first_eps is None else first_eps
+        assert np.array_equal(ep, np.broadcast_to(first_eps, ep.shape))   # the same episodes throughout
+        assert np.array_equal(t[..., 1].numpy(), step.astype(np.float32))
+        assert np.array_equal(prev[..., 1].numpy(), np.where(step > 0, step - 1, 0).astype(np.float32))
+    assert list(DeviceDataset(device="cpu").bptt_batches()) == []

@@ -186,3 +186,54 @@ def test_graph_step_equals_eager():
     assert torch.equal(eager.params(), graphed.params())
     assert eager.counter() == graphed.counter() == 3
     np.testing.assert_array_equal(eager.metrics(3), graphed.metrics(3))
+
+
+def test_final_state_of_a_training_step_is_the_pre_update_forward_state():
+    """rdl_final_state after rdl_step = final_state_batch of the same sess.run (computed with
+    the parameters before the update, backup/lstm_bbpt.py:147-155): equal to rdl_forward's
+    state at those parameters, and to the oracle."""
+    T, B = 10, 20
+    ob, prev, t = _batch(T, B, 31)
+    st0 = np.random.RandomState(4).uniform(-.5, .5, (2, B, 200)).astype(np.float32)
+    tr = _trainer(T, B, "kl")
+    p0 = tr.params().cpu().numpy()
+    _, fin = tr.forward(_t(ob), _t(prev), _t(st0))
+    tr.step(_t(ob), _t(prev), _t(t), _t(st0))
+    got = tr.final_state(B)
+    assert torch.equal(got, fin)
+    want = ln.forward(p0, ob, prev, st0)["state"]
+    np.testing.assert_allclose(got.cpu().numpy(), np.stack(want), atol=5e-5, rtol=1e-4)
+    assert not np.array_equal(tr.params().cpu().numpy(), p0)
+    with pytest.raises(RuntimeError):
+        tr.final_state(B - 1)                   # the last pass had B windows
+
+
+def test_carried_state_chain_matches_oracle():
+    """Truncated BPTT as the variant driver runs it: window k starts from window k-1's final
+    state (after that window's Adam step); gradients and carried states follow the oracle
+    over three windows."""
+    T, B = 10, 20
+    tr = _trainer(T, B, "kl")
+    s_dev, s_np = None, None
+    for k in range(3):
+        ob, prev, t = _batch(T, B, 40 + k)
+        p = tr.params().cpu().numpy()
+        g = tr.rollout(_t(ob), _t(prev), _t(t), s_dev).cpu().numpy()
+        fw = ln.forward(p, ob, prev, s_np)
+        _, d, _ = ln.loss_and_dout(fw["pdflat"], t, "kl", T * B)
+        _grad_check(g, ln.backward(p, fw, d))
+        tr.apply()
+        s_dev = tr.final_state(B)
+        s_np = np.stack(fw["state"]).astype(np.float32)
+        np.testing.assert_allclose(s_dev.cpu().numpy(), s_np, atol=5e-5, rtol=1e-4)
+    assert tr.counter() == 3
+
+
+def test_bptt_variant_driver_runs():
+    """lstm_train.train_bptt (backup/lstm_bbpt.py): teacher warm-up, then per episode a
+    40-window BPTT pass with carried state and an episode stepped by the student."""
+    from reacherdistilation_amd import lstm_train
+    st, ds, losses = lstm_train.train_bptt(episodes=5, warmup_episodes=2, keep_prob=0.5, log=lambda *a: None)
+    assert ds.num_episodes() == 5 and len(losses) == 2
+    assert st.counter() == 2 * 40
+    assert all(np.isfinite(losses)) and all(x > 0 for x in losses)
