@@ -393,7 +393,10 @@ def main():
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
             out["cpu_baseline"]["ref_loop"] = cpu_ref_loop(min(4.0, args.cpu_seconds))
             out["cpu_baseline"]["batched_env"] = cpu_batched_env(min(4.0, args.cpu_seconds))
-        print(json.dumps(out), flush=True)
+        # at N > 1 a communication library may have written to stdout without a newline
+        # (gloo's "[Gloo] Rank 0 is connected ..."): start the JSON line on a line of its own
+        sys.stdout.flush()
+        print(("\n" if world > 1 else "") + json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
