@@ -271,6 +271,9 @@ def main():
     tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world)
 
     def one_step(ev=None):
+        if ev is None and world == 1:
+            tr.step()                               # rdd_step: rollout + reduce/Adam, one host call
+            return
         if ev is not None:
             ev[0].record()
         tr.launch(tr.STAGE_ROLLOUT)
@@ -285,21 +288,25 @@ def main():
 
     for _ in range(args.warmup):
         one_step()
+    # rollout_kernel's launch time for the roofline: HIP events around every `every`-th launch
+    # of the timed region (a timing event costs the stream a few us, so bracketing every step
+    # would slow the very loop being timed: 122 vs 113 us per c4 step)
+    every = max(1, args.steps // 20)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+           for _ in range((args.steps + every - 1) // every)]
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(evs[k])
+        one_step(evs[k // every] if k % every == 0 else None)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
