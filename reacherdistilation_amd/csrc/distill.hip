@@ -1044,6 +1044,13 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
     const float b1p = __uint_as_float(a.ctl[6]), b2p = __uint_as_float(a.ctl[7]);
     const int col = threadIdx.x & (RED_COLS - 1), row = threadIdx.x / RED_COLS;
     const int p = blockIdx.x * RED_COLS + col;
+    // the Adam operands are loaded first, so their round trip overlaps the partial sums
+    float m_p = 0.f, v_p = 0.f, w_p = 0.f;
+    if (a.adam && row == 0 && p < P_TOT) {
+        m_p = a.m[p];
+        v_p = a.v[p];
+        w_p = a.params[p];
+    }
     if (a.reduce) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         if (p < P_PAD) {
@@ -1081,12 +1088,12 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
         if (a.adam && p < P_TOT) {
             // TF1 ApplyAdam functor (training_ops.cc)
             const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-            float m = a.m[p], v = a.v[p];
+            float m = m_p, v = v_p;
             m += (g - m) * (1.0f - a.b1);
             v += (g * g - v) * (1.0f - a.b2);
             a.m[p] = m;
             a.v[p] = v;
-            const float w = a.params[p] - (m * alpha) / (sqrtf(v) + a.eps);
+            const float w = w_p - (m * alpha) / (sqrtf(v) + a.eps);
             a.params[p] = w;
             pack_param(a.simg, p, w, true, a.bf16 != 0);
         }
