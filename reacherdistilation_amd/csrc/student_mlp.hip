@@ -4,7 +4,8 @@
 // Graph (reference student_nn.py:51-57): 16 -> 24 tanh -> 128 tanh -> 128 -> 32 tanh -> 4.
 // Unlike the 2x64 MlpPolicy path (distill.hip), a 16-row tile cannot keep the whole chain
 // plus its 24,380 weight gradients in one wave's registers, so a workgroup of 8 waves
-// cooperates on 64-row blocks:
+// cooperates on 64-row blocks (16-row blocks for small batches, where 64-row blocks would
+// leave CUs idle):
 //  * every layer is a small GEMM over the block, v_mfma_f32_16x16x4_f32 in the natural
 //    orientation (rows x features): A = the block's activations in LDS ([row][feature],
 //    row stride = width + 4 so the 16 rows x 4 k of one A operand hit 64 distinct banks),
@@ -20,6 +21,7 @@
 //  * exact f32 products (f32-input MFMA); tanh = 1 - 2 / (2^(2 log2(e) z) + 1).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <new>
 
@@ -71,21 +73,26 @@ constexpr int WS_ROW = GIMG + N_MET;
 // the A operand of 4 consecutive k-steps (k = 16 S + 4 sub + g) is one ds_read_b128.
 __host__ __device__ constexpr int pk(int k) { return (k & ~15) | ((k & 3) << 2) | ((k >> 2) & 3); }
 
-constexpr int WAVES = 8, BLOCK = 64 * WAVES, ROWS = 64;
-constexpr int RB = ROWS / 16;                   // 16-row blocks of a 64-row block
+constexpr int WAVES = 8, BLOCK = 64 * WAVES;
 
 // LDS buffers [row][pk(feature)], stride = width + 4
 constexpr int S_X0 = 20, S_X1 = 36, S_X2 = 132, S_X3 = 132, S_X4 = 36, S_D5 = 20, S_D4 = 36, S_DA = 132;
-constexpr int O_X0 = 0;
-constexpr int O_X1 = O_X0 + ROWS * S_X0;
-constexpr int O_X2 = O_X1 + ROWS * S_X1;
-constexpr int O_X3 = O_X2 + ROWS * S_X2;
-constexpr int O_X4 = O_X3 + ROWS * S_X3;
-constexpr int O_D5 = O_X4 + ROWS * S_X4;        // layer-5 outputs, then dZ5
-constexpr int O_D4 = O_D5 + ROWS * S_D5;        // dZ4
-constexpr int O_DA = O_D4 + ROWS * S_D4;        // dZ3, later dZ1
-constexpr int LDS_FLOATS = O_DA + ROWS * S_DA;  // 34,816 floats = 136 KiB
-static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+// Row block of ROWS rows per workgroup pass: 64 (the throughput kernel) or 16 (small
+// batches, e.g. the reference's 200-row step: 13 workgroups in parallel instead of 4).
+template <int ROWS>
+struct Lay {
+    static constexpr int RB = ROWS / 16;                   // 16-row MFMA blocks of a row block
+    static constexpr int O_X0 = 0;
+    static constexpr int O_X1 = O_X0 + ROWS * S_X0;
+    static constexpr int O_X2 = O_X1 + ROWS * S_X1;
+    static constexpr int O_X3 = O_X2 + ROWS * S_X2;
+    static constexpr int O_X4 = O_X3 + ROWS * S_X3;
+    static constexpr int O_D5 = O_X4 + ROWS * S_X4;        // layer-5 outputs, then dZ5
+    static constexpr int O_D4 = O_D5 + ROWS * S_D5;        // dZ4
+    static constexpr int O_DA = O_D4 + ROWS * S_D4;        // dZ3, later dZ1
+    static constexpr int LDS_FLOATS = O_DA + ROWS * S_DA;  // 34,816 floats = 136 KiB at 64 rows
+    static_assert(ROWS % 16 == 0 && ROWS * 4 <= BLOCK && LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+};
 static_assert(S_X0 == KP[0] + 4 && S_X1 == KP[1] + 4 && S_X2 == KP[2] + 4 && S_X3 == KP[3] + 4 &&
                   S_X4 == KP[4] + 4 && S_D5 == MP[4] + 4 && S_D4 == MP[3] + 4 && S_DA == MP[2] + 4,
               "buffer strides");
@@ -106,10 +113,10 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// Output blocks of a [ROWS x 16*NCB] result, split over the 8 waves: for NCB >= 8 a wave
-// owns NCB/8 column blocks x all RB row blocks (the B operand is shared by its row blocks);
-// for NCB < 8 a wave owns at most one block.
-template <int NCB>
+// Output blocks of a [ROWS x 16*NCB] result (RB = ROWS / 16), split over the 8 waves: for
+// NCB >= 8 a wave owns NCB/8 column blocks x all RB row blocks (the B operand is shared by
+// its row blocks); for NCB < 8 a wave owns at most one block.
+template <int NCB, int RB>
 struct Part {
     static constexpr int CPW = NCB >= WAVES ? NCB / WAVES : 1;
     static constexpr int RPW = NCB >= WAVES ? RB : 1;
@@ -122,10 +129,10 @@ struct Part {
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
 // Forward of layer L: Y[row][pk(c)] = act(b[c] + sum_k X[row][k] W[k][c]), c = 16 cb + i.
-template <int L, int SI, int SO>
+template <int RB, int L, int SI, int SO>
 __device__ __forceinline__ void fwd_layer(const float* X, float* Y, const float* img, int wave, int i, int g) {
     constexpr int NCB = MP[L] / 16, KG = (IN[L] + 15) / 16;
-    using PT = Part<NCB>;
+    using PT = Part<NCB, RB>;
     if (!PT::active(wave)) return;
     const float* W = img + FW[L];
     const float* bias = img + BB[L];
@@ -164,11 +171,11 @@ __device__ __forceinline__ void fwd_layer(const float* X, float* Y, const float*
 // Backward data of layer L: out[row][pk(c)] = (sum_m D[row][m] W[c][m]) * act'(H[row][c]),
 // c = 16 cb + i an input feature of layer L; act' = 1 - H^2 when layer L-1 ends in tanh
 // (H = X_L, the layer's input).
-template <int L, int SD, int SH, int SO>
+template <int RB, int L, int SD, int SH, int SO>
 __device__ __forceinline__ void dgrad_layer(const float* D, const float* H, float* out, const float* img, int wave,
                                             int i, int g) {
     constexpr int NCB = KP[L] / 16, MG = (OUT[L] + 15) / 16;
-    using PT = Part<NCB>;
+    using PT = Part<NCB, RB>;
     if (!PT::active(wave)) return;
     const float* W = img + BW[L];
     f32x4 acc[PT::CPW][PT::RPW];
@@ -218,7 +225,7 @@ struct WG {
     __device__ static bool ok(int wave, int t) { return KBN % STEP == 0 || kb(wave, t) < KBN; }
 };
 
-template <int L, int SH, int SD>
+template <int ROWS, int L, int SH, int SD>
 __device__ __forceinline__ void wgrad_layer(const float* H, const float* D, f32x4 (&G)[WG<L>::Q], int wave, int i,
                                             int g) {
     using W = WG<L>;
@@ -246,7 +253,7 @@ __device__ __forceinline__ void store_wgrad(float* ws, const f32x4 (&G)[WG<L>::Q
 }
 
 // bias gradient: thread t < OUT[L] sums column t of dZ_L over the block's rows
-template <int L, int SD>
+template <int ROWS, int L, int SD>
 __device__ __forceinline__ void bgrad_layer(const float* D, float& gb, int tid) {
     if (tid < OUT[L]) {
         const int col = pk(tid);
@@ -277,9 +284,11 @@ struct SmArgs {
     int64_t row_base;
 };
 
-template <bool TRAIN>
+template <bool TRAIN, int ROWS>
 __global__ __launch_bounds__(BLOCK) void student_mlp_kernel(SmArgs a) {
-    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+    using LY = Lay<ROWS>;
+    constexpr int RB = LY::RB;
+    __shared__ __attribute__((aligned(16))) float lds[LY::LDS_FLOATS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, g = lane >> 4;
     if (TRAIN && blockIdx.x == 0 && tid < 4) a.ctl[4 + tid] = a.ctl[tid];   // snapshot for the Adam kernel
     const uint32_t step = TRAIN ? a.ctl[0] : 0u;   // optimiser step (dropout counter); only Adam writes it
@@ -291,18 +300,18 @@ __global__ __launch_bounds__(BLOCK) void student_mlp_kernel(SmArgs a) {
     zero(G0); zero(G1); zero(G2); zero(G3); zero(G4);
     float gb0 = 0.f, gb1 = 0.f, gb2 = 0.f, gb3 = 0.f, gb4 = 0.f;
     float lsum = 0.f, ssum = 0.f, nrows = 0.f;
-    float* X0 = lds + O_X0;
-    float* X1 = lds + O_X1;
-    float* X2 = lds + O_X2;
-    float* X3 = lds + O_X3;
-    float* X4 = lds + O_X4;
-    float* D5 = lds + O_D5;
-    float* D4 = lds + O_D4;
-    float* DA = lds + O_DA;
+    float* X0 = lds + LY::O_X0;
+    float* X1 = lds + LY::O_X1;
+    float* X2 = lds + LY::O_X2;
+    float* X3 = lds + LY::O_X3;
+    float* X4 = lds + LY::O_X4;
+    float* D5 = lds + LY::O_D5;
+    float* D4 = lds + LY::O_D4;
+    float* DA = lds + LY::O_DA;
     const int64_t nblk = (a.n + ROWS - 1) / ROWS;
     for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const int64_t row0 = blk * ROWS;
-        if (tid < ROWS * 4) {   // 64 rows x 16 inputs as 16-B vectors
+        if (tid < ROWS * 4) {   // ROWS rows x 16 inputs as 16-B vectors
             const int r = tid >> 2, c = tid & 3;
             f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
             if (row0 + r < a.n) v = *reinterpret_cast<const f32x4*>(a.x + (row0 + r) * RDM_IN + 4 * c);
@@ -319,15 +328,15 @@ __global__ __launch_bounds__(BLOCK) void student_mlp_kernel(SmArgs a) {
             for (int k = 0; k < 4; ++k) X0[r * S_X0 + pk(4 * c + k)] = v[k];
         }
         __syncthreads();
-        fwd_layer<0, S_X0, S_X1>(X0, X1, a.img, wave, i, g);
+        fwd_layer<RB, 0, S_X0, S_X1>(X0, X1, a.img, wave, i, g);
         __syncthreads();
-        fwd_layer<1, S_X1, S_X2>(X1, X2, a.img, wave, i, g);
+        fwd_layer<RB, 1, S_X1, S_X2>(X1, X2, a.img, wave, i, g);
         __syncthreads();
-        fwd_layer<2, S_X2, S_X3>(X2, X3, a.img, wave, i, g);
+        fwd_layer<RB, 2, S_X2, S_X3>(X2, X3, a.img, wave, i, g);
         __syncthreads();
-        fwd_layer<3, S_X3, S_X4>(X3, X4, a.img, wave, i, g);
+        fwd_layer<RB, 3, S_X3, S_X4>(X3, X4, a.img, wave, i, g);
         __syncthreads();
-        fwd_layer<4, S_X4, S_D5>(X4, D5, a.img, wave, i, g);
+        fwd_layer<RB, 4, S_X4, S_D5>(X4, D5, a.img, wave, i, g);
         __syncthreads();
         if constexpr (!TRAIN) {
             // the next block's first write (X0) is ordered after this block's F0 by the barriers above
@@ -366,28 +375,28 @@ __global__ __launch_bounds__(BLOCK) void student_mlp_kernel(SmArgs a) {
             }
             __syncthreads();
             // layer 4 (32 -> 4): dW4, db4, dZ4 = (dZ5 W4^T) * (1 - H4^2)
-            wgrad_layer<4, S_X4, S_D5>(X4, D5, G4, wave, i, g);
-            bgrad_layer<4, S_D5>(D5, gb4, tid);
-            dgrad_layer<4, S_D5, S_X4, S_D4>(D5, X4, D4, a.img, wave, i, g);
+            wgrad_layer<ROWS, 4, S_X4, S_D5>(X4, D5, G4, wave, i, g);
+            bgrad_layer<ROWS, 4, S_D5>(D5, gb4, tid);
+            dgrad_layer<RB, 4, S_D5, S_X4, S_D4>(D5, X4, D4, a.img, wave, i, g);
             __syncthreads();
             // layer 3 (128 -> 32): dZ3 = dZ4 W3^T (H3 is linear)
-            wgrad_layer<3, S_X3, S_D4>(X3, D4, G3, wave, i, g);
-            bgrad_layer<3, S_D4>(D4, gb3, tid);
-            dgrad_layer<3, S_D4, S_X3, S_DA>(D4, X3, DA, a.img, wave, i, g);
+            wgrad_layer<ROWS, 3, S_X3, S_D4>(X3, D4, G3, wave, i, g);
+            bgrad_layer<ROWS, 3, S_D4>(D4, gb3, tid);
+            dgrad_layer<RB, 3, S_D4, S_X3, S_DA>(D4, X3, DA, a.img, wave, i, g);
             __syncthreads();
             // layer 2 (128 -> 128): dZ2 = (dZ3 W2^T) * (1 - H2^2) into X3's buffer (H3 is dead)
-            wgrad_layer<2, S_X2, S_DA>(X2, DA, G2, wave, i, g);
-            bgrad_layer<2, S_DA>(DA, gb2, tid);
-            dgrad_layer<2, S_DA, S_X2, S_X3>(DA, X2, X3, a.img, wave, i, g);
+            wgrad_layer<ROWS, 2, S_X2, S_DA>(X2, DA, G2, wave, i, g);
+            bgrad_layer<ROWS, 2, S_DA>(DA, gb2, tid);
+            dgrad_layer<RB, 2, S_DA, S_X2, S_X3>(DA, X2, X3, a.img, wave, i, g);
             __syncthreads();
             // layer 1 (24 -> 128): dZ1 = (dZ2 W1^T) * (1 - H1^2) into DA
-            wgrad_layer<1, S_X1, S_X3>(X1, X3, G1, wave, i, g);
-            bgrad_layer<1, S_X3>(X3, gb1, tid);
-            dgrad_layer<1, S_X3, S_X1, S_DA>(X3, X1, DA, a.img, wave, i, g);
+            wgrad_layer<ROWS, 1, S_X1, S_X3>(X1, X3, G1, wave, i, g);
+            bgrad_layer<ROWS, 1, S_X3>(X3, gb1, tid);
+            dgrad_layer<RB, 1, S_X3, S_X1, S_DA>(X3, X1, DA, a.img, wave, i, g);
             __syncthreads();
             // layer 0 (16 -> 24)
-            wgrad_layer<0, S_X0, S_DA>(X0, DA, G0, wave, i, g);
-            bgrad_layer<0, S_DA>(DA, gb0, tid);
+            wgrad_layer<ROWS, 0, S_X0, S_DA>(X0, DA, G0, wave, i, g);
+            bgrad_layer<ROWS, 0, S_DA>(DA, gb0, tid);
             __syncthreads();
         }
     }
@@ -556,6 +565,17 @@ struct rdm_trainer {
 
 namespace {
 
+// 16-row blocks for small batches: they are latency-bound, and four times the workgroups
+// run the rows in parallel (measured, scripts/bench_student_mlp.py: the reference's 200-row
+// step 21.8 us vs 35.8 us with 64-row blocks, 1,024 rows 27.2 vs 37.4 us).  Every workgroup
+// writes a 104 KB partial row, so once the 16-row blocks would occupy more than half of the
+// workgroups the 64-row kernel wins (4,096 rows: 51.2 vs 42.4 us).
+// RDM_ROWS=16|64 overrides (measurement only).
+bool use_small_rows(int64_t n, int grid) {
+    if (const char* e = getenv("RDM_ROWS")) return atoi(e) == 16;
+    return (n + 15) / 16 <= grid / 2;
+}
+
 int launch_train(rdm_trainer* t, const float* x, const float* tgt, int64_t n, int64_t n_global) {
     SmArgs a;
     a.x = x;
@@ -570,9 +590,14 @@ int launch_train(rdm_trainer* t, const float* x, const float* tgt, int64_t n, in
     a.keep_prob = t->cfg.keep_prob;
     a.seed = t->cfg.seed;
     a.row_base = t->cfg.row_base;
-    const int64_t nblk = (n + ROWS - 1) / ROWS;
+    const bool small = use_small_rows(n, t->grid);
+    const int rows = small ? 16 : 64;
+    const int64_t nblk = (n + rows - 1) / rows;
     t->last_grid = (int)(nblk < t->grid ? nblk : t->grid);
-    hipLaunchKernelGGL(student_mlp_kernel<true>, dim3(t->last_grid), dim3(BLOCK), 0, t->stream, a);
+    if (small)
+        hipLaunchKernelGGL((student_mlp_kernel<true, 16>), dim3(t->last_grid), dim3(BLOCK), 0, t->stream, a);
+    else
+        hipLaunchKernelGGL((student_mlp_kernel<true, 64>), dim3(t->last_grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "student_mlp_kernel launch");
     return RD_OK;
 }
@@ -714,9 +739,14 @@ int rdm_forward(rdm_trainer* t, const float* x, int64_t n, float* pdflat) {
     a.keep_prob = 1.0f;
     a.seed = 0;
     a.row_base = 0;
-    const int64_t nblk = (n + ROWS - 1) / ROWS;
+    const bool small = use_small_rows(n, t->grid);
+    const int rows = small ? 16 : 64;
+    const int64_t nblk = (n + rows - 1) / rows;
     const int grid = (int)(nblk < t->grid ? nblk : t->grid);
-    hipLaunchKernelGGL(student_mlp_kernel<false>, dim3(grid), dim3(BLOCK), 0, t->stream, a);
+    if (small)
+        hipLaunchKernelGGL((student_mlp_kernel<false, 16>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
+    else
+        hipLaunchKernelGGL((student_mlp_kernel<false, 64>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "student_mlp_kernel (forward) launch");
     return RD_OK;
 }
