@@ -28,6 +28,11 @@
 namespace {
 
 constexpr int OBD = 11, HID = 64, ZLD = 12;
+// Hidden activations are stored [row][HLD] with column HID = 1: a weight-gradient GEMM over
+// HID + 1 rows of A^T then yields dW (rows 0..HID-1) AND the bias gradient db (row HID) in
+// one launch, written straight into the flat [W | b] parameter layout (the input batch Z
+// carries the same 1 in column OBD).
+constexpr int HLD = HID + 4;
 // policy (MlpPolicy layout of reacher_distill.h)
 constexpr int PW1 = 0, PB1 = PW1 + OBD * HID, PW2 = PB1 + HID, PB2 = PW2 + HID * HID, PW3 = PB2 + HID,
               PB3 = PW3 + HID * 2, PLS = PB3 + 2, P_POL = PLS + 2;
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(256) void gather_kernel(const int* perm, int mb, co
     const int64_t r = perm[i];
 #pragma unroll
     for (int k = 0; k < OBD; ++k) Z[i * ZLD + k] = clip5((ob[r * OBD + k] - rms[k]) / rms[OBD + k]);
-    Z[i * ZLD + OBD] = 0.0f;
+    Z[i * ZLD + OBD] = 1.0f;   // the bias input of the layer-1 gradient GEMM
     A[2 * i] = ac[2 * r];
     A[2 * i + 1] = ac[2 * r + 1];
     LPO[i] = lpo[r];
@@ -413,25 +418,11 @@ __global__ void loss_final_kernel(const double* part, int nblk, float* grad, dou
     for (int k = 0; k < 4; ++k) ctl[4 + k] = ctl[k];
 }
 
-// deterministic column sums (as the LSTM path): out[c] = sum over rows
-__global__ __launch_bounds__(256) void colsum_kernel(const float* src, int64_t M, int N, int64_t ld, int64_t chunk,
-                                                     float* out, int64_t ld_out) {
-    __shared__ float s[4][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
-    const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = min(M, r0 + chunk);
-    float a = 0.f, b = 0.f;
-    if (c < N) {
-        int64_t r = r0 + ph;
-        for (; r + 4 < r1; r += 8) {
-            a += src[r * ld + c];
-            b += src[(r + 4) * ld + c];
-        }
-        if (r < r1) a += src[r * ld + c];
-    }
-    s[ph][threadIdx.x & 63] = a + b;
-    __syncthreads();
-    if (ph == 0 && c < N) out[(int64_t)blockIdx.y * ld_out + c] = (s[0][threadIdx.x] + s[1][threadIdx.x]) +
-                                                                 (s[2][threadIdx.x] + s[3][threadIdx.x]);
+// column HID of a [rows][HLD] activation buffer = 1 (the bias input of the next layer's
+// weight-gradient GEMM); the forward GEMMs write columns 0..HID-1 only
+__global__ __launch_bounds__(256) void ones_column_kernel(float* H, int64_t rows) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r < rows) H[r * HLD + HID] = 1.0f;
 }
 
 struct AdamArgs {
@@ -530,7 +521,7 @@ struct rdp_trainer {
     float *Z = nullptr, *A = nullptr, *LPO = nullptr, *ATG = nullptr, *RET = nullptr;
     float *H1 = nullptr, *H2 = nullptr, *MEAN = nullptr, *G1 = nullptr, *G2 = nullptr, *V = nullptr;
     float *dMEAN = nullptr, *dV = nullptr, *D2 = nullptr, *D1 = nullptr, *E2 = nullptr, *E1 = nullptr;
-    float *split = nullptr, *colws = nullptr;
+    float* split = nullptr;
     float* hist = nullptr;
     uint32_t* ctl = nullptr;
     int64_t part_doubles = 0;
@@ -539,7 +530,6 @@ struct rdp_trainer {
 namespace {
 
 constexpr int64_t SPLIT_FLOATS = 4 << 20;
-constexpr int COLSUM_CHUNK = 512;
 
 hipError_t mm(rdp_trainer* t, int M, int N, int K, const float* A, int64_t lda, int ta, const float* B, int64_t ldb,
               int tb, float* C, int64_t ldc, const float* bias = nullptr, int epi = rdg::EPI_NONE,
@@ -553,20 +543,6 @@ hipError_t mm(rdp_trainer* t, int M, int N, int K, const float* A, int64_t lda, 
     return rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus);
 }
 
-hipError_t colsum(rdp_trainer* t, const float* src, int64_t M, int N, int64_t ld, float* out) {
-    const unsigned gx = (unsigned)((N + 63) / 64);
-    if (M <= COLSUM_CHUNK) {
-        hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, t->stream, src, M, N, ld, (int64_t)COLSUM_CHUNK,
-                           out, (int64_t)0);
-        return hipGetLastError();
-    }
-    const int64_t nch = (M + COLSUM_CHUNK - 1) / COLSUM_CHUNK;
-    hipLaunchKernelGGL(colsum_kernel, dim3(gx, (unsigned)nch), dim3(256), 0, t->stream, src, M, N, ld,
-                       (int64_t)COLSUM_CHUNK, t->colws, (int64_t)N);
-    hipLaunchKernelGGL(colsum_kernel, dim3(gx, 1), dim3(256), 0, t->stream, (const float*)t->colws, nch, N,
-                       (int64_t)N, nch, out, (int64_t)0);
-    return hipGetLastError();
-}
 
 #define RDP_CK(call, what) RD_HIP((call), what)
 
@@ -613,12 +589,12 @@ int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
                        (const float*)t->atarg, (const float*)t->ret, t->Z, t->A, t->LPO, t->ATG, t->RET);
     RDP_CK(hipGetLastError(), "rdp gather");
     // forward (pol, vf)
-    RDP_CK(mm(t, mb, HID, OBD, t->Z, ZLD, 0, P + PW1, HID, 0, t->H1, HID, P + PB1, rdg::EPI_TANH), "rdp pol1");
-    RDP_CK(mm(t, mb, HID, HID, t->H1, HID, 0, P + PW2, HID, 0, t->H2, HID, P + PB2, rdg::EPI_TANH), "rdp pol2");
-    RDP_CK(mm(t, mb, 2, HID, t->H2, HID, 0, P + PW3, 2, 0, t->MEAN, 2, P + PB3), "rdp pol3");
-    RDP_CK(mm(t, mb, HID, OBD, t->Z, ZLD, 0, Pv + VW1, HID, 0, t->G1, HID, Pv + VC1, rdg::EPI_TANH), "rdp vf1");
-    RDP_CK(mm(t, mb, HID, HID, t->G1, HID, 0, Pv + VW2, HID, 0, t->G2, HID, Pv + VC2, rdg::EPI_TANH), "rdp vf2");
-    RDP_CK(mm(t, mb, 1, HID, t->G2, HID, 0, Pv + VW3, 1, 0, t->V, 1, Pv + VC3), "rdp vf3");
+    RDP_CK(mm(t, mb, HID, OBD, t->Z, ZLD, 0, P + PW1, HID, 0, t->H1, HLD, P + PB1, rdg::EPI_TANH), "rdp pol1");
+    RDP_CK(mm(t, mb, HID, HID, t->H1, HLD, 0, P + PW2, HID, 0, t->H2, HLD, P + PB2, rdg::EPI_TANH), "rdp pol2");
+    RDP_CK(mm(t, mb, 2, HID, t->H2, HLD, 0, P + PW3, 2, 0, t->MEAN, 2, P + PB3), "rdp pol3");
+    RDP_CK(mm(t, mb, HID, OBD, t->Z, ZLD, 0, Pv + VW1, HID, 0, t->G1, HLD, Pv + VC1, rdg::EPI_TANH), "rdp vf1");
+    RDP_CK(mm(t, mb, HID, HID, t->G1, HLD, 0, Pv + VW2, HID, 0, t->G2, HLD, Pv + VC2, rdg::EPI_TANH), "rdp vf2");
+    RDP_CK(mm(t, mb, 1, HID, t->G2, HLD, 0, Pv + VW3, 1, 0, t->V, 1, Pv + VC3), "rdp vf3");
     const int lblk = (mb + RB - 1) / RB;
     hipLaunchKernelGGL(ppo_loss_kernel, dim3(lblk), dim3(RB), 0, t->stream, mb, P, (const float*)t->MEAN,
                        (const float*)t->V, (const float*)t->A, (const float*)t->LPO, (const float*)t->ATG,
@@ -626,26 +602,20 @@ int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
     hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, t->stream, (const double*)t->part, lblk, g, t->acc,
                        last_epoch ? 1 : 0, t->ctl);
     RDP_CK(hipGetLastError(), "rdp loss");
-    // policy backward
-    RDP_CK(mm(t, HID, 2, mb, t->H2, HID, 1, t->dMEAN, 2, 0, g + PW3, 2), "rdp gW3");
-    RDP_CK(colsum(t, t->dMEAN, mb, 2, 2, g + PB3), "rdp gb3");
-    RDP_CK(mm(t, mb, HID, 2, t->dMEAN, 2, 0, P + PW3, 2, 1, t->D2, HID, nullptr, rdg::EPI_DTANH, t->H2, HID), "rdp d2");
-    RDP_CK(mm(t, HID, HID, mb, t->H1, HID, 1, t->D2, HID, 0, g + PW2, HID), "rdp gW2");
-    RDP_CK(colsum(t, t->D2, mb, HID, HID, g + PB2), "rdp gb2");
-    RDP_CK(mm(t, mb, HID, HID, t->D2, HID, 0, P + PW2, HID, 1, t->D1, HID, nullptr, rdg::EPI_DTANH, t->H1, HID),
+    // policy backward: [dW; db] of a layer in one GEMM (the ones column of its input)
+    RDP_CK(mm(t, HID + 1, 2, mb, t->H2, HLD, 1, t->dMEAN, 2, 0, g + PW3, 2), "rdp gW3 gb3");
+    RDP_CK(mm(t, mb, HID, 2, t->dMEAN, 2, 0, P + PW3, 2, 1, t->D2, HID, nullptr, rdg::EPI_DTANH, t->H2, HLD), "rdp d2");
+    RDP_CK(mm(t, HID + 1, HID, mb, t->H1, HLD, 1, t->D2, HID, 0, g + PW2, HID), "rdp gW2 gb2");
+    RDP_CK(mm(t, mb, HID, HID, t->D2, HID, 0, P + PW2, HID, 1, t->D1, HID, nullptr, rdg::EPI_DTANH, t->H1, HLD),
            "rdp d1");
-    RDP_CK(mm(t, OBD, HID, mb, t->Z, ZLD, 1, t->D1, HID, 0, g + PW1, HID), "rdp gW1");
-    RDP_CK(colsum(t, t->D1, mb, HID, HID, g + PB1), "rdp gb1");
+    RDP_CK(mm(t, OBD + 1, HID, mb, t->Z, ZLD, 1, t->D1, HID, 0, g + PW1, HID), "rdp gW1 gb1");
     // value backward
-    RDP_CK(mm(t, HID, 1, mb, t->G2, HID, 1, t->dV, 1, 0, gv + VW3, 1), "rdp gV3");
-    RDP_CK(colsum(t, t->dV, mb, 1, 1, gv + VC3), "rdp gc3");
-    RDP_CK(mm(t, mb, HID, 1, t->dV, 1, 0, Pv + VW3, 1, 1, t->E2, HID, nullptr, rdg::EPI_DTANH, t->G2, HID), "rdp e2");
-    RDP_CK(mm(t, HID, HID, mb, t->G1, HID, 1, t->E2, HID, 0, gv + VW2, HID), "rdp gV2");
-    RDP_CK(colsum(t, t->E2, mb, HID, HID, gv + VC2), "rdp gc2");
-    RDP_CK(mm(t, mb, HID, HID, t->E2, HID, 0, Pv + VW2, HID, 1, t->E1, HID, nullptr, rdg::EPI_DTANH, t->G1, HID),
+    RDP_CK(mm(t, HID + 1, 1, mb, t->G2, HLD, 1, t->dV, 1, 0, gv + VW3, 1), "rdp gV3 gc3");
+    RDP_CK(mm(t, mb, HID, 1, t->dV, 1, 0, Pv + VW3, 1, 1, t->E2, HID, nullptr, rdg::EPI_DTANH, t->G2, HLD), "rdp e2");
+    RDP_CK(mm(t, HID + 1, HID, mb, t->G1, HLD, 1, t->E2, HID, 0, gv + VW2, HID), "rdp gV2 gc2");
+    RDP_CK(mm(t, mb, HID, HID, t->E2, HID, 0, Pv + VW2, HID, 1, t->E1, HID, nullptr, rdg::EPI_DTANH, t->G1, HLD),
            "rdp e1");
-    RDP_CK(mm(t, OBD, HID, mb, t->Z, ZLD, 1, t->E1, HID, 0, gv + VW1, HID), "rdp gV1");
-    RDP_CK(colsum(t, t->E1, mb, HID, HID, gv + VC1), "rdp gc1");
+    RDP_CK(mm(t, OBD + 1, HID, mb, t->Z, ZLD, 1, t->E1, HID, 0, gv + VW1, HID), "rdp gV1 gc1");
     AdamArgs aa{t->grad, t->params, t->m, t->v, t->ctl, t->cfg.optim_stepsize * t->lrmult, 0.9f, 0.999f, 1e-8f};
     hipLaunchKernelGGL(adam_kernel, dim3((P_ALL + 255) / 256), dim3(256), 0, t->stream, aa);
     RDP_CK(hipGetLastError(), "rdp adam");
@@ -744,16 +714,22 @@ int rdp_create(rdp_trainer** out, const rdp_config* cfg, int device, void* hip_s
     af(&t->rms, 2 * OBD);
     ai(&t->perm, (int64_t)cfg->optim_epochs * S);
     af(&t->Z, mb * ZLD); af(&t->A, 2 * mb); af(&t->LPO, mb); af(&t->ATG, mb); af(&t->RET, mb);
-    af(&t->H1, mb * HID); af(&t->H2, mb * HID); af(&t->MEAN, 2 * mb); af(&t->G1, mb * HID); af(&t->G2, mb * HID);
+    af(&t->H1, mb * HLD); af(&t->H2, mb * HLD); af(&t->MEAN, 2 * mb); af(&t->G1, mb * HLD); af(&t->G2, mb * HLD);
     af(&t->V, mb); af(&t->dMEAN, 2 * mb); af(&t->dV, mb); af(&t->D2, mb * HID); af(&t->D1, mb * HID);
     af(&t->E2, mb * HID); af(&t->E1, mb * HID);
     af(&t->split, SPLIT_FLOATS);
-    af(&t->colws, ((mb + COLSUM_CHUNK - 1) / COLSUM_CHUNK) * HID);
     af(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
     if (e == hipSuccess) e = hipMalloc((void**)&t->ctl, sizeof(uint32_t) * 8);
     if (e != hipSuccess) {
         rdp_destroy(t);
         return rd::hip_fail(e, "rdp_create: allocation");
+    }
+    for (float* h : {t->H1, t->H2, t->G1, t->G2})
+        hipLaunchKernelGGL(ones_column_kernel, dim3((unsigned)((mb + 255) / 256)), dim3(256), 0, t->stream, h,
+                           (int64_t)mb);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        rdp_destroy(t);
+        return rd::hip_fail(e, "rdp_create: ones columns");
     }
     if (int rc = rdp_reset(t)) {
         rdp_destroy(t);
@@ -770,7 +746,7 @@ int rdp_destroy(rdp_trainer* t) {
                     t->ep_step, t->ep_idx, t->ob, t->ac, t->vpred, t->rew, t->newf, t->nextv, t->adv, t->ret,
                     t->atarg, t->lpo, t->rms_sums, t->part, t->stats, t->acc, t->rms, t->perm, t->Z, t->A, t->LPO,
                     t->ATG, t->RET, t->H1, t->H2, t->MEAN, t->G1, t->G2, t->V, t->dMEAN, t->dV, t->D2, t->D1,
-                    t->E2, t->E1, t->split, t->colws, t->hist, t->ctl};
+                    t->E2, t->E1, t->split, t->hist, t->ctl};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     delete t;
