@@ -33,6 +33,10 @@ constexpr int G4 = 4 * U;                // 800 gates
 constexpr int XI = 11 + 32;              // 43 cell inputs
 constexpr int XLD = 44;                  // X row stride (16-B rows)
 constexpr int H1 = 64, H2 = 128, H3 = 64, H4 = 32;
+// head activations A_l are stored [row][H_l + 4] with column H_l = 1, so the next layer's
+// weight-gradient GEMM over H_l + 1 rows of A^T yields [dW; db] in the flat [W | b] layout
+// (tf.layers.dense order) in one launch, no column-sum pass
+constexpr int L1 = H1 + 4, L2 = H2 + 4, L3 = H3 + 4, L4 = H4 + 4;
 
 // flat parameter offsets (variable-creation order)
 constexpr int OFF_WP = 0;
@@ -202,6 +206,12 @@ __global__ void metrics_kernel(const float* part, int nblk, float rows, uint32_t
 }
 
 // deterministic column sums: out[c] (+ blockIdx.y * ld_out) = sum over rows [y*chunk, ...)
+// column `col` of a [rows][ld] buffer = 1
+__global__ __launch_bounds__(256) void ones_column_kernel(float* A, int64_t rows, int ld, int col) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r < rows) A[r * ld + col] = 1.0f;
+}
+
 __global__ __launch_bounds__(256) void colsum_kernel(const float* src, int64_t M, int N, int64_t ld, int64_t chunk,
                                                      float* out, int64_t ld_out) {
     __shared__ float s[4][64];
@@ -352,11 +362,11 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     }
     // head over all T x B rows (student_nn.py:42-46)
     const float* Hc = t->H + B * U;
-    RDL_CK(mm(t, (int)R, H1, U, Hc, U, 0, P + OFF_W1, H1, 0, t->A1, H1, P + OFF_B1, rdg::EPI_TANH), "rdl head1");
-    RDL_CK(mm(t, (int)R, H2, H1, t->A1, H1, 0, P + OFF_W2, H2, 0, t->A2, H2, P + OFF_B2, rdg::EPI_TANH), "rdl head2");
-    RDL_CK(mm(t, (int)R, H3, H2, t->A2, H2, 0, P + OFF_W3, H3, 0, t->A3, H3, P + OFF_B3, rdg::EPI_TANH), "rdl head3");
-    RDL_CK(mm(t, (int)R, H4, H3, t->A3, H3, 0, P + OFF_W4, H4, 0, t->A4, H4, P + OFF_B4, rdg::EPI_TANH), "rdl head4");
-    RDL_CK(mm(t, (int)R, 4, H4, t->A4, H4, 0, P + OFF_W5, 4, 0, out_pdflat, 4, P + OFF_B5), "rdl head5");
+    RDL_CK(mm(t, (int)R, H1, U, Hc, U, 0, P + OFF_W1, H1, 0, t->A1, L1, P + OFF_B1, rdg::EPI_TANH), "rdl head1");
+    RDL_CK(mm(t, (int)R, H2, H1, t->A1, L1, 0, P + OFF_W2, H2, 0, t->A2, L2, P + OFF_B2, rdg::EPI_TANH), "rdl head2");
+    RDL_CK(mm(t, (int)R, H3, H2, t->A2, L2, 0, P + OFF_W3, H3, 0, t->A3, L3, P + OFF_B3, rdg::EPI_TANH), "rdl head3");
+    RDL_CK(mm(t, (int)R, H4, H3, t->A3, L3, 0, P + OFF_W4, H4, 0, t->A4, L4, P + OFF_B4, rdg::EPI_TANH), "rdl head4");
+    RDL_CK(mm(t, (int)R, 4, H4, t->A4, L4, 0, P + OFF_W5, 4, 0, out_pdflat, 4, P + OFF_B5), "rdl head5");
     return RD_OK;
 }
 
@@ -374,20 +384,16 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
                        t->ctl, t->hist, t->cfg.metrics_len);
     RDL_CK(hipGetLastError(), "rdl metrics_kernel");
     // head backward (weight gradients over all rows; data gradients with the tanh derivative fused)
-    RDL_CK(mm(t, H4, 4, Ri, t->A4, H4, 1, t->dY, 4, 0, g + OFF_W5, 4), "rdl dW5");
-    RDL_CK(colsum(t, t->dY, R, 4, 4, g + OFF_B5), "rdl db5");
-    RDL_CK(mm(t, Ri, H4, 4, t->dY, 4, 0, P + OFF_W5, 4, 1, t->D32, H4, nullptr, rdg::EPI_DTANH, t->A4, H4), "rdl dZ4");
-    RDL_CK(mm(t, H3, H4, Ri, t->A3, H3, 1, t->D32, H4, 0, g + OFF_W4, H4), "rdl dW4");
-    RDL_CK(colsum(t, t->D32, R, H4, H4, g + OFF_B4), "rdl db4");
-    RDL_CK(mm(t, Ri, H3, H4, t->D32, H4, 0, P + OFF_W4, H4, 1, t->D64a, H3, nullptr, rdg::EPI_DTANH, t->A3, H3),
+    RDL_CK(mm(t, H4 + 1, 4, Ri, t->A4, L4, 1, t->dY, 4, 0, g + OFF_W5, 4), "rdl dW5 db5");
+    RDL_CK(mm(t, Ri, H4, 4, t->dY, 4, 0, P + OFF_W5, 4, 1, t->D32, H4, nullptr, rdg::EPI_DTANH, t->A4, L4), "rdl dZ4");
+    RDL_CK(mm(t, H3 + 1, H4, Ri, t->A3, L3, 1, t->D32, H4, 0, g + OFF_W4, H4), "rdl dW4 db4");
+    RDL_CK(mm(t, Ri, H3, H4, t->D32, H4, 0, P + OFF_W4, H4, 1, t->D64a, H3, nullptr, rdg::EPI_DTANH, t->A3, L3),
            "rdl dZ3");
-    RDL_CK(mm(t, H2, H3, Ri, t->A2, H2, 1, t->D64a, H3, 0, g + OFF_W3, H3), "rdl dW3");
-    RDL_CK(colsum(t, t->D64a, R, H3, H3, g + OFF_B3), "rdl db3");
-    RDL_CK(mm(t, Ri, H2, H3, t->D64a, H3, 0, P + OFF_W3, H3, 1, t->D128, H2, nullptr, rdg::EPI_DTANH, t->A2, H2),
+    RDL_CK(mm(t, H2 + 1, H3, Ri, t->A2, L2, 1, t->D64a, H3, 0, g + OFF_W3, H3), "rdl dW3 db3");
+    RDL_CK(mm(t, Ri, H2, H3, t->D64a, H3, 0, P + OFF_W3, H3, 1, t->D128, H2, nullptr, rdg::EPI_DTANH, t->A2, L2),
            "rdl dZ2");
-    RDL_CK(mm(t, H1, H2, Ri, t->A1, H1, 1, t->D128, H2, 0, g + OFF_W2, H2), "rdl dW2");
-    RDL_CK(colsum(t, t->D128, R, H2, H2, g + OFF_B2), "rdl db2");
-    RDL_CK(mm(t, Ri, H1, H2, t->D128, H2, 0, P + OFF_W2, H2, 1, t->D64b, H1, nullptr, rdg::EPI_DTANH, t->A1, H1),
+    RDL_CK(mm(t, H1 + 1, H2, Ri, t->A1, L1, 1, t->D128, H2, 0, g + OFF_W2, H2), "rdl dW2 db2");
+    RDL_CK(mm(t, Ri, H1, H2, t->D128, H2, 0, P + OFF_W2, H2, 1, t->D64b, H1, nullptr, rdg::EPI_DTANH, t->A1, L1),
            "rdl dZ1");
     const float* Hc = t->H + B * U;
     RDL_CK(mm(t, U, H1, Ri, Hc, U, 1, t->D64b, H1, 0, g + OFF_W1, H1), "rdl dW1");
@@ -466,10 +472,10 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     alloc(&t->Cs, (R + B) * U);
     alloc(&t->Z, R * G4);
     alloc(&t->G, R * G4);
-    alloc(&t->A1, R * H1);
-    alloc(&t->A2, R * H2);
-    alloc(&t->A3, R * H3);
-    alloc(&t->A4, R * H4);
+    alloc(&t->A1, R * L1);
+    alloc(&t->A2, R * L2);
+    alloc(&t->A3, R * L3);
+    alloc(&t->A4, R * L4);
     alloc(&t->Y, R * 4);
     alloc(&t->dY, R * 4);
     alloc(&t->D32, R * H4);
@@ -489,6 +495,17 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     if (e != hipSuccess) {
         rdl_destroy(t);
         return rd::hip_fail(e, "rdl_create: allocation");
+    }
+    {   // the ones columns of the head activations (the head GEMMs write columns 0..H_l-1)
+        const unsigned gr = (unsigned)((R + 255) / 256);
+        hipLaunchKernelGGL(ones_column_kernel, dim3(gr), dim3(256), 0, t->stream, t->A1, R, L1, H1);
+        hipLaunchKernelGGL(ones_column_kernel, dim3(gr), dim3(256), 0, t->stream, t->A2, R, L2, H2);
+        hipLaunchKernelGGL(ones_column_kernel, dim3(gr), dim3(256), 0, t->stream, t->A3, R, L3, H3);
+        hipLaunchKernelGGL(ones_column_kernel, dim3(gr), dim3(256), 0, t->stream, t->A4, R, L4, H4);
+        if ((e = hipGetLastError()) != hipSuccess) {
+            rdl_destroy(t);
+            return rd::hip_fail(e, "rdl_create: ones columns");
+        }
     }
     if (int rc = rdl_reset(t)) {
         rdl_destroy(t);
