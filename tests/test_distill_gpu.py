@@ -82,7 +82,7 @@ def _grad_check(tr, loss, act):
     return g, g64, L, sq
 
 
-@pytest.mark.parametrize("n", [1000, 4096, 65536])
+@pytest.mark.parametrize("n", [17, 1000, 4096, 40001, 65536])   # 16-, 16-, 16-, 32-, 64-env groups
 @pytest.mark.parametrize("loss", ["mse", "kl"])
 def test_rollout_gradient_matches_oracle(n, loss):
     tr = _trainer(n, loss=loss)
@@ -291,3 +291,21 @@ def test_accumulated_mse_normalises_over_k_rollouts():
     b.launch(b.STAGE_ROLLOUT)
     b.launch(b.STAGE_REDUCE)
     torch.testing.assert_close(a.grad() * K, b.grad(), rtol=1e-6, atol=1e-9)
+
+
+def test_group_size_changes_only_the_summation_order(monkeypatch):
+    """16-, 32- and 64-env groups (chosen by batch size) step every env
+    identically (bitwise) and give the same gradient up to f32 reordering of the sums."""
+    n = 3000
+    out = {}
+    for gs in (16, 32, 64):
+        monkeypatch.setenv("RDD_GROUP_ENVS", str(gs))
+        tr = _trainer(n, loss="kl")
+        tr.rollout()
+        out[gs] = (tr.grad().cpu().numpy().astype(np.float64), tr.env_state().cpu().numpy())
+        tr.close()
+    g16, s16 = out[16]
+    for gs in (32, 64):
+        g, s_ = out[gs]
+        assert np.array_equal(s_, s16)
+        assert np.abs(g - g16).max() <= 1e-5 * np.abs(g16).max()
