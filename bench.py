@@ -131,7 +131,7 @@ def cpu_batched_env(seconds, n=65536):
     return out
 
 
-def env_roofline(dev, n=1 << 24, iters=30):
+def env_roofline(dev, n=1 << 24, iters=100, warmup=20):
     """The standalone env.step kernel (rd_step) at 16.8M envs: algorithmic 113 B per
     env-step (read act 8 + q,v 16 + target 8 + held offset 8; write q,v 16 + offset 8 +
     obs 44 + rew 4 + done 1) over its launch time, vs the 8 TB/s HBM peak."""
@@ -141,7 +141,7 @@ def env_roofline(dev, n=1 << 24, iters=30):
     env = BatchedReacher(n, seed=0, device=dev)
     env.reset()
     a = (torch.rand(n, 2, device=dev) * 2 - 1).contiguous()
-    for _ in range(5):
+    for _ in range(warmup):
         env.step(a)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
@@ -157,14 +157,14 @@ def env_roofline(dev, n=1 << 24, iters=30):
             "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
 
 
-def copy_bandwidth(dev, gib=1.0, iters=20):
+def copy_bandwidth(dev, gib=1.0, iters=40):
     """Measured device-to-device copy bandwidth (read + write bytes / s), the practical HBM
     ceiling the roofline is also quoted against."""
     import torch
     n = int(gib * (1 << 30)) // 4
     a = torch.empty(n, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
-    for _ in range(3):
+    for _ in range(10):
         b.copy_(a)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
