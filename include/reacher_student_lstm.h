@@ -63,6 +63,12 @@ int rdl_set_params(rdl_trainer* t, const float* params);
 int rdl_get_params(rdl_trainer* t, float* params);
 /* Adam slots, beta powers, step counter to zero (lstm_train.py:99) */
 int rdl_reset(rdl_trainer* t);
+/* the Adam slots m, v [RDL_PARAMS] (device pointers): with the params, what the reference's
+ * tf.train.Saver over the 'LSTM' scope checkpoints every episode and restores with -r
+ * (lstm_train.py:86-87,102-107,199); the beta powers are not in that scope, so a restore
+ * starts them afresh (rdl_reset, then rdl_set_params + rdl_set_slots) */
+int rdl_get_slots(rdl_trainer* t, float* m, float* v);
+int rdl_set_slots(rdl_trainer* t, const float* m, const float* v);
 /* sess.run((s_action, s_pdflat_slice, final_state)) (lstm_train.py:171-183), all T x B outputs:
  * state0 may be null (zero state); state_out may be null */
 int rdl_forward(rdl_trainer* t, const float* ob, const float* prev_pdflat, const float* state0, int64_t windows,

@@ -550,6 +550,22 @@ int rdl_get_params(rdl_trainer* t, float* params) {
     return RD_OK;
 }
 
+int rdl_get_slots(rdl_trainer* t, float* m, float* v) {
+    if (!t || !m || !v) return rd::set_error(RD_EINVAL, "rdl_get_slots: null argument");
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(hipMemcpyAsync(m, t->m, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream), "rdl_get_slots");
+    RD_HIP(hipMemcpyAsync(v, t->v, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream), "rdl_get_slots");
+    return RD_OK;
+}
+
+int rdl_set_slots(rdl_trainer* t, const float* m, const float* v) {
+    if (!t || !m || !v) return rd::set_error(RD_EINVAL, "rdl_set_slots: null argument");
+    rd::DeviceGuard dg(t->device);
+    RD_HIP(hipMemcpyAsync(t->m, m, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream), "rdl_set_slots");
+    RD_HIP(hipMemcpyAsync(t->v, v, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream), "rdl_set_slots");
+    return RD_OK;
+}
+
 int rdl_reset(rdl_trainer* t) {
     if (!t) return rd::set_error(RD_EINVAL, "rdl_reset: null handle");
     rd::DeviceGuard dg(t->device);

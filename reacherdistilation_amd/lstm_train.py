@@ -18,6 +18,8 @@ broadcasts at 0 or >= T-1 records.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -29,16 +31,30 @@ from .policy import TeacherAgent
 from .student_lstm import StudentLstmConfig, StudentLstmTrainer
 
 
+def _restore(st, restore: bool, path: str | None, log):
+    """lstm_train.py:102-107: fresh variables unless restoring; a missing checkpoint only
+    prints, as the reference does."""
+    if not restore:
+        return
+    if path and os.path.exists(path):
+        st.load(path)
+    else:
+        log("attempt to restore trained data but {0} does not exist".format(path))
+
+
 def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EPISODES, loss: str = "kl",
           lr: float = 1e-3, keep_prob: float = 1.0, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
-          warmup_episodes: int = 2 * LSTM_BATCH_SIZE, log=print):
-    """Returns (student trainer, dataset, per-episode summed training loss)."""
+          warmup_episodes: int = 2 * LSTM_BATCH_SIZE, student_path: str | None = None, log=print):
+    """Returns (student trainer, dataset, per-episode summed training loss).  With
+    ``student_path`` the student (params + Adam slots) is restored from it when ``restore``
+    (lstm_train.py:102-107) and saved to it after every episode (:199)."""
     env = make_mujoco_env("Reacher-v2", seed, device=device)
     teacher = TeacherAgent(restore=restore, path=teacher_path)
     tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
     st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
                                               steps=STEPS_UNROLLED, max_windows=LSTM_BATCH_SIZE), device=device)
     dataset = DeviceDataset(device=device, seed=seed, batch_size=LSTM_BATCH_SIZE, steps_unrolled=STEPS_UNROLLED)
+    _restore(st, restore, student_path, log)
     losses = []
     if not train:
         return st, dataset, losses
@@ -78,6 +94,8 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
             losses.append(total_loss)
             total_loss = 0.0
             dataset.flush()
+            if student_path:
+                st.save(student_path)   # saver.save every episode (lstm_train.py:199)
             if dataset.num_episodes() >= episodes:
                 break
     return st, dataset, losses
@@ -85,7 +103,7 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
 
 def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EPISODES, loss: str = "kl",
                lr: float = 1e-3, keep_prob: float = 1.0, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
-               warmup_episodes: int = 2 * LSTM_BATCH_SIZE, log=print):
+               warmup_episodes: int = 2 * LSTM_BATCH_SIZE, student_path: str | None = None, log=print):
     """The truncated-BPTT variant of the driver (reference backup/lstm_bbpt.py:18-208), same
     graph, loss and Adam.  After the teacher warm-up (:115-139) each round is
       * one BPTT pass (:141-158): ``dataset.bptt_batches()`` -- LSTM_BATCH_SIZE episodes, the
@@ -101,6 +119,7 @@ def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOT
     st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
                                               steps=STEPS_UNROLLED, max_windows=LSTM_BATCH_SIZE), device=device)
     dataset = DeviceDataset(device=device, seed=seed, batch_size=LSTM_BATCH_SIZE, steps_unrolled=STEPS_UNROLLED)
+    _restore(st, restore, student_path, log)
     losses = []
     if not train:
         return st, dataset, losses
@@ -142,6 +161,8 @@ def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOT
         log("recent loss: %f " % total_loss)
         losses.append(total_loss)
         dataset.flush()
+        if student_path:
+            st.save(student_path)
         if dataset.num_episodes() >= episodes:
             break
     return st, dataset, losses

@@ -55,6 +55,8 @@ nat.register({
     "rdl_get_counter": (INT, [P, ctypes.POINTER(I64)]),
     "rdl_read_metrics": (INT, [P, I64, P]),
     "rdl_final_state": (INT, [P, I64, P]),
+    "rdl_get_slots": (INT, [P, P, P]),
+    "rdl_set_slots": (INT, [P, P, P]),
 })
 
 
@@ -139,6 +141,33 @@ class StudentLstmTrainer:
         self._sync_stream()
         nat.check(self._lib.rdl_get_params(self._h, nat.ptr(out)), "rdl_get_params")
         return out
+
+    def save(self, path: str):
+        """tf.train.Saver(var_list=LSTM/*).save (reference lstm_train.py:86-87,199): the
+        parameters and the Adam slots m, v, as a safetensors file (nothing executable)."""
+        from safetensors.torch import save_file
+        m = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
+        v = torch.empty_like(m)
+        self._sync_stream()
+        nat.check(self._lib.rdl_get_slots(self._h, nat.ptr(m), nat.ptr(v)), "rdl_get_slots")
+        torch.cuda.current_stream(self.device).synchronize()
+        save_file({"params": self.params().cpu(), "adam_m": m.cpu(), "adam_v": v.cpu()}, path)
+
+    def load(self, path: str):
+        """saver.restore (reference lstm_train.py:102-107): parameters and Adam slots from
+        `path`; the beta powers and step counter start afresh, as the reference initialises
+        the Adam variables before restoring the 'LSTM' scope (:99-105)."""
+        from safetensors.torch import load_file
+        d = load_file(path)
+        if d["params"].numel() != N_PARAMS:
+            raise ValueError(f"{path}: {d['params'].numel()} parameters, expected {N_PARAMS}")
+        self.reset_optimizer()
+        self.set_params(d["params"])
+        m = d["adam_m"].to(self.device, torch.float32).contiguous()
+        v = d["adam_v"].to(self.device, torch.float32).contiguous()
+        self._sync_stream()
+        nat.check(self._lib.rdl_set_slots(self._h, nat.ptr(m), nat.ptr(v)), "rdl_set_slots")
+        torch.cuda.current_stream(self.device).synchronize()
 
     def reset_optimizer(self):
         self._sync_stream()
