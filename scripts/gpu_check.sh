@@ -13,7 +13,7 @@ ok_or_stop() {  # $1 = exit code, $2 = step; test failures (1) continue, faults 
     *) echo "STOP after $2: exit $1"; exit "$1" ;;
   esac
 }
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; tail -5 "$OUT/pytest_gpu.log"; ok_or_stop $rc pytest
 timeout -k 10 420 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -eq 0 ] || { echo "bench exit $rc"; exit $rc; }
