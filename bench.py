@@ -207,7 +207,7 @@ def cpu_baseline(workload, seconds, threads):
                        f"OpenMP {threads} threads")
 
 
-def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=100):
+def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=100, comm=None):
     """North-star check: optimiser steps (one per env step, the reference's lr 1e-4 TF1 Adam)
     until the student's action-MSE vs the teacher, averaged over the last 10 steps and all
     ranks, falls below 1e-3 -- against the reference's budget of 5000 episodes x 50 steps =
@@ -217,7 +217,7 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
 
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
     tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
-                                      student_dtype=sdt), device=dev, rank=rank, world_size=world)
+                                      student_dtype=sdt), device=dev, rank=rank, world_size=world, comm=comm)
     t0 = time.perf_counter()
     steps, mse, hit = 0, float("nan"), None
     while steps < max_steps:
@@ -264,15 +264,36 @@ def main():
             dist.init_process_group(backend)
 
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    # N > 1 over RCCL: the gradient all-reduce is issued by the native step on the trainer's
+    # stream (include/reacher_comm.h); RD_COMM=torch keeps torch.distributed's collective.
+    # A communicator that fails its one-shot self-check is dropped for torch's (reported).
+    comm, collective = None, "none"
+    if world > 1:
+        collective = "torch.distributed"
+        if dist.get_backend() == "nccl" and os.environ.get("RD_COMM", "rccl") == "rccl":
+            from reacherdistilation_amd.dist import RcclComm
+            try:
+                comm = RcclComm(dev)
+                ok = comm.self_check()
+            except Exception as e:   # noqa: BLE001  (reported in the line, never silent)
+                print(f"RCCL communicator unavailable ({e}); using torch.distributed", file=sys.stderr)
+                comm, ok = None, False
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 1:
+                collective = "rccl (native, trainer stream)"
+            else:
+                comm = None
+                collective = "torch.distributed (native RCCL self-check failed)"
     wl = WORKLOADS[args.workload]
     n = args.envs_per_gpu or wl["envs"]
     sdt = wl.get("student_dtype", "f32")
     cfg = DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr, student_dtype=sdt)
-    tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world)
+    tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world, comm=comm)
 
     def one_step(ev=None):
-        if ev is None and world == 1:
-            tr.step()                               # rdd_step: rollout + reduce/Adam, one host call
+        if ev is None and (world == 1 or comm is not None):
+            tr.step()     # rdd_step: rollout + reduce (+ RCCL all-reduce) + Adam, one host call
             return
         if ev is not None:
             ev[0].record()
@@ -318,7 +339,7 @@ def main():
     if args.accum > 1:   # secondary line: one optimiser step (+ all-reduce) per K env-steps
         tk = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr,
                                           student_dtype=sdt, accum_steps=args.accum),
-                            device=dev, rank=rank, world_size=world)
+                            device=dev, rank=rank, world_size=world, comm=comm)
         ksteps = 2 * args.accum
         for _ in range(args.accum):
             tk.step()
@@ -343,7 +364,7 @@ def main():
 
     conv = None
     if args.conv_steps > 0:
-        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps)
+        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm)
 
     # student action-MSE vs teacher over the last steps (all ranks)
     met = tr.metrics(min(10, tr.counter()))
@@ -377,7 +398,7 @@ def main():
                        "envs_total": n * world, "student": f"MlpPolicy 2x64 tanh (5060 params, {sdt})",
                        "teacher": "MlpPolicy 2x64 tanh", "loss": wl["loss"], "act_with": wl["act_with"],
                        "optimizer": f"TF1 Adam lr {args.lr}, 1 step per env-step",
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "collective": collective},
             # the north star's student action-MSE: after the convergence leg (< 1e-3 within its
             # budget); the timed run's own value (220 steps from init) is kept beside it
             "student_mse": conv["student_mse_final"] if conv is not None else mse,
@@ -405,6 +426,9 @@ def main():
         sys.stdout.flush()
         print(("\n" if world > 1 else "") + json.dumps(out), flush=True)
     if world > 1:
+        tr.close()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -1,0 +1,50 @@
+/* reacher_comm.h -- the one data-path collective of the sharded rollout (libreacher.so):
+ * an in-place SUM all-reduce of a flat f32 gradient over RCCL (xGMI), issued on the
+ * trainer's own HIP stream.
+ *
+ * Why a communicator of our own beside torch.distributed: torch's collective runs on an
+ * internal stream, so every step pays two cross-stream event waits plus ~19 us of host
+ * dispatch per call (measured on one MI355X with a world-size-1 group, 262,144 envs: the
+ * torch path costs a c4 step 117 -> 126 us before any exchange happens;
+ * scripts/allreduce_overhead.py).  Here the all-reduce is one more launch on the stream that
+ * already holds the rollout and the Adam kernel, and rdd_step() issues the whole sharded
+ * step (rollout, reduce, all-reduce, Adam) from one host call.
+ *
+ * The reference has no multi-GPU path in src/distilation; its only collective is MpiAdam's
+ * Allreduce(SUM) of the flat gradient (reference backup/student_rollout.py:658-659,709) --
+ * this is that exchange, once per optimiser step.
+ *
+ * RCCL is resolved at run time (dlopen of librccl.so.1, reusing the copy torch loaded), so
+ * the library loads on hosts without RCCL; rd_comm_* then fail with RD_EINVAL and a message.
+ * Usage (one process per GPU): rank 0 calls rd_comm_unique_id() and broadcasts the 128
+ * bytes (e.g. over the torch.distributed group); every rank calls rd_comm_create() with
+ * them; bind with rdd_bind_comm() (reacher_distill.h).  Conventions as in reacher.h.
+ */
+#ifndef REACHER_COMM_H
+#define REACHER_COMM_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RD_COMM_ID_BYTES 128
+
+typedef struct rd_comm rd_comm;
+
+/* A fresh RCCL unique id (rank 0 only); id: host buffer of RD_COMM_ID_BYTES. */
+int rd_comm_unique_id(uint8_t* id);
+
+/* Collective over all ranks: an RCCL communicator of nranks ranks on HIP device `device`. */
+int rd_comm_create(rd_comm** out, const uint8_t* id, int nranks, int rank, int device);
+
+/* In-place SUM all-reduce of n floats of device memory, asynchronous on hip_stream. */
+int rd_comm_allreduce_f32(rd_comm* c, float* buf, int64_t n, void* hip_stream);
+
+int rd_comm_nranks(const rd_comm* c);
+int rd_comm_destroy(rd_comm* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

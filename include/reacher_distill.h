@@ -18,8 +18,10 @@
  * Conventions as in reacher.h: device pointers, asynchronous on the handle's stream, no
  * host sync except rdd_read_metrics / rdd_get_counter; 0 = OK, RD_EINVAL, -(hipError_t).
  *
- * Multi-GPU (one process per GPU, envs sharded contiguously): per step call
- * rdd_rollout(), all-reduce(SUM) rdd_grad_buffer() across ranks (RCCL), then rdd_apply().
+ * Multi-GPU (one process per GPU, envs sharded contiguously): bind an RCCL communicator
+ * (rdd_bind_comm, reacher_comm.h) and rdd_step() issues rollout, reduce, the all-reduce
+ * (SUM) of the gradient and Adam on the trainer's stream from one call; or per step call
+ * rdd_rollout(), all-reduce rdd_grad_buffer() across ranks yourself, then rdd_apply().
  * Single GPU: rdd_step() == rdd_rollout() + rdd_apply() fused into two kernels.
  */
 #ifndef REACHER_DISTILL_H
@@ -27,6 +29,7 @@
 #include <stdint.h>
 
 #include "reacher.h"
+#include "reacher_comm.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -128,6 +131,12 @@ float* rdd_grad_buffer(rdd_trainer* tr);   /* device [P], valid after rdd_rollou
 /* Use a caller-owned device buffer [P] as the gradient buffer (e.g. a torch tensor that
  * the host all-reduces in place with RCCL); NULL restores the trainer's own buffer. */
 int rdd_bind_grad_buffer(rdd_trainer* tr, float* grad);
+/* Bind (NULL: unbind) the communicator of this rank.  While bound, rdd_step() =
+ * rollout, reduce, rd_comm_allreduce_f32(grad) on the trainer's stream, Adam; and
+ * rdd_allreduce_grad() all-reduces the gradient buffer (between the REDUCE and APPLY
+ * stages, or rdd_rollout_obs and rdd_apply).  The trainer does not own the communicator. */
+int rdd_bind_comm(rdd_trainer* tr, rd_comm* comm);
+int rdd_allreduce_grad(rdd_trainer* tr);
 
 /* Policy query without stepping (teacher.pi.pd.flat / student pdflat):
  * obs [n][11] -> t_pdflat, s_pdflat [n][4] (either output may be NULL). */

@@ -40,6 +40,12 @@ SIGNATURES = {
     "rd_gym_reset_draws": (INT, [U64, I32, P]),
     "rd_version": (ctypes.c_char_p, []),
     "rd_last_error": (ctypes.c_char_p, []),
+    # reacher_comm.h
+    "rd_comm_unique_id": (INT, [P]),
+    "rd_comm_create": (INT, [ctypes.POINTER(P), P, INT, INT, INT]),
+    "rd_comm_allreduce_f32": (INT, [P, P, I64, P]),
+    "rd_comm_nranks": (INT, [P]),
+    "rd_comm_destroy": (INT, [P]),
 }
 
 _lib = None

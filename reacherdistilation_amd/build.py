@@ -21,7 +21,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 # -O3; keep IEEE f32 semantics (no -ffast-math): parity tolerances are stated for it.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wall",
-         "-Wno-unused-function", "-Werror=return-type", "-munsafe-fp-atomics"]
+         "-Wno-unused-function", "-Werror=return-type", "-munsafe-fp-atomics", "-ldl"]
 
 
 def sources():

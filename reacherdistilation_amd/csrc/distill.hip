@@ -1202,6 +1202,7 @@ struct rdd_trainer {
     int ws_rows = 0;                     // rows of ws (the device's CU count, or cfg.grid)
     int gs = GROUP;                      // envs per group of the env rollout
     int accum = 1;                       // rollouts per optimiser step (MSE normalisation)
+    rd_comm* comm = nullptr;             // bound RCCL communicator (multi-GPU), not owned
 
 };
 
@@ -1430,7 +1431,22 @@ int rdd_step(rdd_trainer* t) {
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_step: hipSetDevice");
     if (int rc = launch_rollout(t)) return rc;
-    return launch_reduce(t, 1, 1);
+    if (!t->comm) return launch_reduce(t, 1, 1);
+    // sharded step: the exchange sits between the reduction and Adam, all on one stream
+    if (int rc = launch_reduce(t, 1, 0)) return rc;
+    if (int rc = rd_comm_allreduce_f32(t->comm, t->grad, P_TOT, t->stream)) return rc;
+    return launch_reduce(t, 0, 1);
+}
+
+int rdd_bind_comm(rdd_trainer* t, rd_comm* comm) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdd_bind_comm: null handle");
+    t->comm = comm;
+    return RD_OK;
+}
+
+int rdd_allreduce_grad(rdd_trainer* t) {
+    if (!t || !t->comm) return rd::set_error(RD_EINVAL, "rdd_allreduce_grad: no communicator bound");
+    return rd_comm_allreduce_f32(t->comm, t->grad, P_TOT, t->stream);
 }
 
 int rdd_rollout_obs(rdd_trainer* t, const float* obs, int64_t n, int64_t n_global) {

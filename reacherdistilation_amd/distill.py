@@ -61,6 +61,8 @@ nat.register({
     "rdd_rollout_obs": (INT, [P, P, I64, I64]),
     "rdd_step_obs": (INT, [P, P, I64]),
     "rdd_read_metrics": (INT, [P, I64, P]),
+    "rdd_bind_comm": (INT, [P, P]),
+    "rdd_allreduce_grad": (INT, [P]),
 })
 
 
@@ -87,7 +89,7 @@ class DistillConfig:
 class DistillTrainer:
     def __init__(self, cfg: DistillConfig, device="cuda:0", rank: int = 0, world_size: int = 1,
                  process_group=None, teacher: MlpPolicyParams | None = None,
-                 student: MlpPolicyParams | None = None):
+                 student: MlpPolicyParams | None = None, comm=None):
         self.cfg = cfg
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -123,6 +125,16 @@ class DistillTrainer:
         nat.check(self._lib.rdd_bind_grad_buffer(self._h, nat.ptr(self._grad)), "rdd_bind_grad_buffer")
         self.steps = 0
         self._k = 0   # rollouts accumulated into the current optimiser step (accum_steps > 1)
+        # an RcclComm (dist.py) makes the exchange part of the native step, on this stream
+        self.comm = None
+        if comm is not None:
+            self.bind_comm(comm)
+
+    def bind_comm(self, comm):
+        if comm is not None and comm.world != self.world:
+            raise ValueError(f"communicator of {comm.world} ranks for a trainer of {self.world}")
+        nat.check(self._lib.rdd_bind_comm(self._h, comm.handle if comm is not None else None), "rdd_bind_comm")
+        self.comm = comm
 
     # -- parameters ------------------------------------------------------------------
     def set_teacher(self, p: MlpPolicyParams):
@@ -151,7 +163,7 @@ class DistillTrainer:
         taken every K-th call."""
         K = max(1, int(self.cfg.accum_steps))
         if K == 1:
-            if self.world == 1:
+            if self.world == 1 or self.comm is not None:   # one host call (+ RCCL on our stream)
                 nat.check(self._lib.rdd_step(self._h), "rdd_step")
             else:
                 nat.check(self._lib.rdd_rollout(self._h), "rdd_rollout")
@@ -161,7 +173,7 @@ class DistillTrainer:
             k = self._k
             last = k == K - 1
             self.launch(self.STAGE_ROLLOUT)
-            if last and self.world == 1:
+            if last and self.world == 1 and self.comm is None:
                 self.launch(self.STAGE_REDUCE_ACCUM_APPLY if k else self.STAGE_REDUCE_APPLY)
             else:
                 self.launch(self.STAGE_REDUCE_ACCUM if k else self.STAGE_REDUCE)
@@ -242,7 +254,10 @@ class DistillTrainer:
         return self._grad
 
     def allreduce_grad(self):
-        allreduce_sum_(self._grad, self.pg)
+        if self.comm is not None:
+            nat.check(self._lib.rdd_allreduce_grad(self._h), "rdd_allreduce_grad")
+        else:
+            allreduce_sum_(self._grad, self.pg)
 
     def replicas_identical(self) -> bool:
         """student weights stay bit-identical across ranks (same init, same

@@ -54,3 +54,63 @@ def test_two_ranks_match_single_rank():
     np.testing.assert_allclose(np.concatenate([st0, st1], axis=1), st_ref, atol=1e-4)
     np.testing.assert_allclose(m0[:, 3] + m1[:, 3], m_ref[:, 3])
     np.testing.assert_allclose(m0[:, 1] + m1[:, 1], m_ref[:, 1], rtol=1e-4)
+
+
+class _Comm1:
+    """A one-rank native RCCL communicator (include/reacher_comm.h) without a process group."""
+
+    def __init__(self):
+        import ctypes
+
+        from reacherdistilation_amd import _native as nat
+        self._lib = nat.load()
+        idb = (ctypes.c_uint8 * 128)()
+        nat.check(self._lib.rd_comm_unique_id(idb), "rd_comm_unique_id")
+        h = ctypes.c_void_p()
+        nat.check(self._lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0), "rd_comm_create")
+        self.handle, self.world = h, 1
+
+    def close(self):
+        self._lib.rd_comm_destroy(self.handle)
+
+
+def test_native_rccl_allreduce_one_rank():
+    """rd_comm_allreduce_f32 over one rank is the identity, on the caller's stream."""
+    import ctypes
+
+    from reacherdistilation_amd import _native as nat
+    c = _Comm1()
+    try:
+        assert c._lib.rd_comm_nranks(c.handle) == 1
+        x = torch.randn(5060, device="cuda:0")
+        want = x.clone()
+        nat.check(c._lib.rd_comm_allreduce_f32(c.handle, ctypes.c_void_p(x.data_ptr()), x.numel(),
+                                               nat.stream_handle(x.device)), "allreduce")
+        torch.cuda.synchronize()
+        assert torch.equal(x, want)
+        assert c._lib.rd_comm_allreduce_f32(c.handle, None, 4, None) != 0   # bad argument -> error
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("accum", [1, 3])
+def test_bound_comm_step_is_bitwise_the_single_rank_step(accum):
+    """With a communicator bound, rdd_step = rollout, reduce, RCCL all-reduce, Adam on the
+    trainer's stream; over one rank that is bitwise the fused single-rank step (and the
+    staged accumulation path with rdd_allreduce_grad likewise)."""
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    cfg = DistillConfig(n_envs=20000, seed=3, lr=1e-3, accum_steps=accum)
+    c = _Comm1()
+    try:
+        a = DistillTrainer(cfg, device="cuda:0")
+        b = DistillTrainer(cfg, device="cuda:0", comm=c)
+        for _ in range(4 * accum):
+            a.step()
+            b.step()
+        assert torch.equal(a.student_params(), b.student_params())
+        assert torch.equal(a.env_state(), b.env_state())
+        assert np.array_equal(a.metrics(4), b.metrics(4))
+        a.close()
+        b.close()
+    finally:
+        c.close()
