@@ -2,7 +2,9 @@
 //   C[M x N] (+)= epi( op(A)[M x K] . op(B)[K x N] + bias[N] )
 // op(A) = A stored [M][lda] (ta = 0) or [K][lda] (ta = 1, A^T); likewise B [K][ldb] / [N][ldb].
 // Epilogues: none, tanh, or x (1 - aux^2) (the tanh derivative of a stored activation);
-// optional accumulate into C.  Deterministic: fixed tiling, split-K partials summed in a
+// optional accumulate into C; or EPI_LSTM_BWD: the output (row, unit) is dh_{t-1} of the
+// LSTM student's BPTT and the epilogue runs TF1 LSTMCell's backward for step t-1 instead of
+// a store (csrc/student_lstm.hip).  Deterministic: fixed tiling, split-K partials summed in a
 // fixed order by a second kernel (no atomics).
 //
 // Tiling: 256-thread workgroups own a 128 x 128 (or, for thin problems, 64 x 64) C tile; 4
@@ -19,7 +21,7 @@ namespace rdg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-enum { EPI_NONE = 0, EPI_TANH = 1, EPI_DTANH = 2 };
+enum { EPI_NONE = 0, EPI_TANH = 1, EPI_DTANH = 2, EPI_LSTM_BWD = 3 };
 
 struct GemmArgs {
     int M, N, K;
@@ -39,7 +41,33 @@ struct GemmArgs {
     float* part;          // split-K partials [splits][M][N] (splits > 1)
     int splits;
     int kchunk;           // K range per split (multiple of 32)
+    // EPI_LSTM_BWD (N = units U): aux = dh from the head [M][ldaux]; gate activations
+    // lg [M][4U] (i, j, f, o); c_t lct and c_{t-1} lcp [M][U]; dc carried in place lcc [M][U];
+    // dz written to lz [M][4U]
+    const float* lg;
+    const float* lct;
+    const float* lcp;
+    float* lcc;
+    float* lz;
 };
+
+// TF1 LSTMCell backward at one (row, unit) with dh = dh_head + dh_next: the arithmetic of
+// the standalone cell kernel in csrc/student_lstm.hip, operation for operation (bitwise).
+__device__ __forceinline__ void lstm_bwd_point(const GemmArgs& g, int64_t row, int u, float dh_next) {
+    const int U = g.N;
+    const int64_t idx = row * U + u;
+    const float* gg = g.lg + row * 4 * U;
+    const float gi = gg[u], gj = gg[U + u], gf = gg[2 * U + u], go = gg[3 * U + u];
+    const float dh = g.aux[row * g.ldaux + u] + dh_next;
+    const float tc = tanhf(g.lct[idx]);
+    const float dcv = fmaf(dh * go, fmaf(-tc, tc, 1.0f), g.lcc[idx]);
+    float* dz = g.lz + row * 4 * U;
+    dz[u] = dcv * gj * gi * (1.0f - gi);
+    dz[U + u] = dcv * gi * fmaf(-gj, gj, 1.0f);
+    dz[2 * U + u] = dcv * g.lcp[idx] * gf * (1.0f - gf);
+    dz[3 * U + u] = dh * tc * go * (1.0f - go);
+    g.lcc[idx] = dcv * gf;
+}
 
 constexpr int TK = 16, GEMM_THREADS = 256;
 
@@ -180,6 +208,19 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
         __syncthreads();
     }
 
+    if (g.epi == EPI_LSTM_BWD && g.splits <= 1) {   // (uniform) the cell backward per output
+#pragma unroll
+        for (int x = 0; x < FB; ++x)
+#pragma unroll
+            for (int y = 0; y < FB; ++y)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + (BT / 2) * wm + 16 * x + 4 * gq + r, col = n0 + (BT / 2) * wn + 16 * y + i;
+                    // + 0.0f: the value the unfused path stored (epi_value adds the zero bias)
+                    if (row < g.M && col < g.N) lstm_bwd_point(g, row, col, acc[x][y][r] + 0.0f);
+                }
+        return;
+    }
     // epilogue in two passes: every operand load (C when accumulating, the tanh' activation,
     // the bias) is issued before any result is formed, so their latencies overlap
     float in_c[FB][FB][4], in_a[FB][FB][4], in_b[FB][FB];
@@ -361,7 +402,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
     if (ph == 0 && idx < MN) {
         const float v = (s[0][threadIdx.x] + s[1][threadIdx.x]) + (s[2][threadIdx.x] + s[3][threadIdx.x]);
         const int row = (int)(idx / g.N), col = (int)(idx % g.N);
-        g.C[(int64_t)row * g.ldc + col] = apply_epi(g, row, col, v);
+        if (g.epi == EPI_LSTM_BWD)
+            lstm_bwd_point(g, row, col, v);
+        else
+            g.C[(int64_t)row * g.ldc + col] = apply_epi(g, row, col, v);
     }
 }
 

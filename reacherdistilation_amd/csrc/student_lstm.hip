@@ -110,7 +110,92 @@ __global__ __launch_bounds__(256) void cell_fwd_kernel(const float* Z, const flo
     h_out[idx] = go * tanhf(c);
 }
 
-// BPTT through one cell: dh = dh_head + dh_next; dc carried in place
+// One step of the forward recurrence with the cell in the epilogue (replaces the recurrent
+// GEMM accumulating into Z + cell_fwd_kernel): a workgroup owns 64 rows x 16 units, i.e. the
+// 64 gate columns {i, j, f, o} x those units of Wr, so at the end of the K loop every lane
+// holds all four gate pre-activations of its (row, unit) outputs.  4 waves, wave w = rows
+// 16w..16w+15 x the 4 gate blocks (one A and four B operands per k-step, 4 MFMAs).  The k
+// order and the epilogue's z = (acc + 0) + Zx are the unfused path's, so G, c and h are
+// bitwise those of the two-launch form.  Z_s keeps the input half (the backward reuses Z).
+constexpr int RF_ROWS = 64, RF_UNITS = 16, RF_TK = 16, RF_LS = 64 + 16;
+__global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restrict__ Hp, const float* __restrict__ Wr,
+                                                           const float* __restrict__ Zx,
+                                                           const float* __restrict__ cprev, float* __restrict__ Gs,
+                                                           float* __restrict__ cs, float* __restrict__ hs,
+                                                           int64_t B) {
+    __shared__ __attribute__((aligned(16))) float As[2][RF_TK][RF_LS];   // [k][row]
+    __shared__ __attribute__((aligned(16))) float Bs[2][RF_TK][RF_LS];   // [k][16 gate + unit]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
+    const int64_t m0 = (int64_t)blockIdx.y * RF_ROWS;
+    const int u0 = blockIdx.x * RF_UNITS;
+    // staging: thread t loads 4 consecutive k of row m0 + t/4 (A) and 4 consecutive units of
+    // gate (t%16)/4 at k row t/16 (B, one 16-B load from Wr's row)
+    const int64_t am = m0 + (tid >> 2);
+    const int ak = 4 * (tid & 3);
+    const int bk = tid >> 4, bq = tid & 15, by = bq >> 2, bu = u0 + 4 * (bq & 3);
+    auto load_a = [&](int k0) { return rdg::load4<true>(Hp + am * U + k0 + ak, am < B ? min(4, U - (k0 + ak)) : 0); };
+    auto load_b = [&](int k0) {
+        const int k = k0 + bk;
+        return rdg::load4<true>(Wr + (int64_t)k * G4 + by * U + bu, k < U ? min(4, U - bu) : 0);
+    };
+    auto stage = [&](int buf, rdg::f32x4 a, rdg::f32x4 b) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) As[buf][ak + e][tid >> 2] = a[e];
+        *reinterpret_cast<rdg::f32x4*>(&Bs[buf][bk][16 * by + 4 * (bq & 3)]) = b;
+    };
+    rdg::f32x4 acc[4];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[y] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int NT = (U + RF_TK - 1) / RF_TK;
+    stage(0, load_a(0), load_b(0));
+    __syncthreads();
+    for (int kt = 0; kt < NT; ++kt) {
+        const int buf = kt & 1;
+        const bool more = kt + 1 < NT;
+        rdg::f32x4 na, nb;
+        if (more) {
+            na = load_a((kt + 1) * RF_TK);
+            nb = load_b((kt + 1) * RF_TK);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int kk = 4 * s + gq;
+            const float a = As[buf][kk][16 * wave + i];
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+                acc[y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[buf][kk][16 * y + i], acc[y], 0, 0, 0);
+        }
+        if (more) stage(buf ^ 1, na, nb);
+        __syncthreads();
+    }
+    // epilogue: operands first, then TF1 LSTMCell (cell_fwd_kernel's arithmetic)
+    const int u = u0 + i;
+    float zx[4][4], cpv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + 16 * wave + 4 * gq + r;
+        const bool ok = row < B && u < U;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) zx[y][r] = ok ? Zx[row * G4 + y * U + u] : 0.0f;
+        cpv[r] = ok ? cprev[row * U + u] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + 16 * wave + 4 * gq + r;
+        if (row >= B || u >= U) continue;
+        const float gi = sigm((acc[0][r] + 0.0f) + zx[0][r]), gj = tanhf((acc[1][r] + 0.0f) + zx[1][r]);
+        const float gf = sigm((acc[2][r] + 0.0f) + zx[2][r] + 1.0f), go = sigm((acc[3][r] + 0.0f) + zx[3][r]);
+        const float c = fmaf(gf, cpv[r], gi * gj);
+        float* g = Gs + row * G4;
+        g[u] = gi; g[U + u] = gj; g[2 * U + u] = gf; g[3 * U + u] = go;
+        cs[row * U + u] = c;
+        hs[row * U + u] = go * tanhf(c);
+    }
+}
+
+// BPTT through one cell (dh = dh_head + dh_next; dc carried in place).  The fused backward
+// runs this only for the last step; the others ride in the dh GEMM's epilogue
+// (rdg::EPI_LSTM_BWD, the same arithmetic)
 __global__ __launch_bounds__(256) void cell_bwd_kernel(const float* dh_head, const float* dh_next, int add_next,
                                                        const float* G, const float* c_t, const float* c_prev,
                                                        float* dc, float* dZ, int64_t B) {
@@ -349,16 +434,23 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     }
     // input half of the gate pre-activations for all steps: Z = X[:, :43] Wl[0:43] + bl
     RDL_CK(mm(t, (int)R, G4, XI, t->X, XLD, 0, P + OFF_WL, G4, 0, t->Z, G4, P + OFF_BL), "rdl gemm Zx");
-    const unsigned cb = (unsigned)((B * U + 255) / 256);
     for (int s = 0; s < T; ++s) {
         float* Zs = t->Z + (int64_t)s * B * G4;
+#ifdef RD_LSTM_UNFUSED   // diagnostic build: the recurrent GEMM and the cell as two launches
         RDL_CK(mm(t, (int)B, G4, U, t->H + (int64_t)s * B * U, U, 0, P + OFF_WL + XI * G4, G4, 0, Zs, G4, nullptr,
                   rdg::EPI_NONE, nullptr, 0, 1),
                "rdl gemm recurrent");
-        hipLaunchKernelGGL(cell_fwd_kernel, dim3(cb), dim3(256), 0, t->stream, (const float*)Zs,
-                           (const float*)(t->Cs + (int64_t)s * B * U), t->G + (int64_t)s * B * G4,
+        hipLaunchKernelGGL(cell_fwd_kernel, dim3((unsigned)((B * U + 255) / 256)), dim3(256), 0, t->stream,
+                           (const float*)Zs, (const float*)(t->Cs + (int64_t)s * B * U), t->G + (int64_t)s * B * G4,
                            t->Cs + (int64_t)(s + 1) * B * U, t->H + (int64_t)(s + 1) * B * U, B);
         RDL_CK(hipGetLastError(), "rdl cell_fwd_kernel");
+#else
+        hipLaunchKernelGGL(lstm_rec_fwd_kernel, dim3((U + RF_UNITS - 1) / RF_UNITS, (unsigned)((B + RF_ROWS - 1) / RF_ROWS)),
+                           dim3(256), 0, t->stream, (const float*)(t->H + (int64_t)s * B * U), P + OFF_WL + XI * G4,
+                           (const float*)Zs, (const float*)(t->Cs + (int64_t)s * B * U), t->G + (int64_t)s * B * G4,
+                           t->Cs + (int64_t)(s + 1) * B * U, t->H + (int64_t)(s + 1) * B * U, B);
+        RDL_CK(hipGetLastError(), "rdl lstm_rec_fwd_kernel");
+#endif
     }
     // head over all T x B rows (student_nn.py:42-46)
     const float* Hc = t->H + B * U;
@@ -403,6 +495,7 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     float* dZl = t->Z;
     RDL_CK(hipMemsetAsync(t->dc, 0, sizeof(float) * B * U, t->stream), "rdl bptt");
     const unsigned cb = (unsigned)((B * U + 255) / 256);
+#ifdef RD_LSTM_UNFUSED   // diagnostic build: dh GEMM and cell backward as two launches per step
     for (int s = T - 1; s >= 0; --s) {
         hipLaunchKernelGGL(cell_bwd_kernel, dim3(cb), dim3(256), 0, t->stream, (const float*)(t->dHh + (int64_t)s * B * U),
                            (const float*)t->dhn, s < T - 1 ? 1 : 0, (const float*)(t->G + (int64_t)s * B * G4),
@@ -413,6 +506,30 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
             RDL_CK(mm(t, (int)B, U, G4, dZl + (int64_t)s * B * G4, G4, 0, P + OFF_WL + XI * G4, G4, 1, t->dhn, U),
                    "rdl gemm dh");
     }
+#else
+    // the last step's cell alone; then per step s the GEMM dh_{s-1} = dz_s . Wr^T whose
+    // epilogue (or split-K reduce) runs the cell backward of step s-1 -> dz_{s-1}, dc
+    hipLaunchKernelGGL(cell_bwd_kernel, dim3(cb), dim3(256), 0, t->stream,
+                       (const float*)(t->dHh + (int64_t)(T - 1) * B * U), (const float*)t->dhn, 0,
+                       (const float*)(t->G + (int64_t)(T - 1) * B * G4), (const float*)(t->Cs + (int64_t)T * B * U),
+                       (const float*)(t->Cs + (int64_t)(T - 1) * B * U), t->dc, dZl + (int64_t)(T - 1) * B * G4, B);
+    RDL_CK(hipGetLastError(), "rdl cell_bwd_kernel");
+    for (int s = T - 1; s > 0; --s) {
+        rdg::GemmArgs g{};
+        g.M = (int)B; g.N = U; g.K = G4;
+        g.A = dZl + (int64_t)s * B * G4; g.lda = G4; g.ta = 0;
+        g.B = P + OFF_WL + XI * G4; g.ldb = G4; g.tb = 1;
+        g.C = t->dhn; g.ldc = U;
+        g.epi = rdg::EPI_LSTM_BWD;
+        g.aux = t->dHh + (int64_t)(s - 1) * B * U; g.ldaux = U;
+        g.lg = t->G + (int64_t)(s - 1) * B * G4;
+        g.lct = t->Cs + (int64_t)s * B * U;
+        g.lcp = t->Cs + (int64_t)(s - 1) * B * U;
+        g.lcc = t->dc;
+        g.lz = dZl + (int64_t)(s - 1) * B * G4;
+        RDL_CK(rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus), "rdl gemm dh + cell");
+    }
+#endif
     // LSTM weights: dWl = [x | h_prev]^T dz over all rows; dbl; then dp -> dWp, dbp
     RDL_CK(mm(t, XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4), "rdl dWl x");
     RDL_CK(mm(t, U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4), "rdl dWl h");
