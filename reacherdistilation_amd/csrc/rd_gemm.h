@@ -104,6 +104,10 @@ __device__ __forceinline__ f32x4 load4(const float* p, int valid) {
     return v;
 }
 
+template <int BT>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[BT / 32][BT / 32], int m0, int n0,
+                                              int wm, int wn, int i, int gq);
+
 // BT x BT C tile per workgroup (BT = 64 or 128); 4 waves in 2 x 2, each (BT/2)^2 =
 // (BT/32)^2 16x16 blocks.  LDS rows are BT + 16 floats: the 4 k-rows of one MFMA operand
 // start 16 banks apart, so 16 consecutive m (or n) x 4 k hit 64 distinct banks.
@@ -207,7 +211,15 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
         }
         __syncthreads();
     }
+    gemm_epilogue<BT>(g, acc, m0, n0, wm, wn, i, gq);
+}
 
+// The C tile's epilogue (every kernel of this file): acc[x][y][r] = C[m0 + (BT/2) wm + 16x +
+// 4gq + r][n0 + (BT/2) wn + 16y + i].
+template <int BT>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[BT / 32][BT / 32], int m0, int n0,
+                                              int wm, int wn, int i, int gq) {
+    constexpr int FB = BT / 32;
     if (g.epi == EPI_LSTM_BWD && g.splits <= 1) {   // (uniform) the cell backward per output
 #pragma unroll
         for (int x = 0; x < FB; ++x)
@@ -421,14 +433,16 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
     // 16x16x4 128-tile variant and the 32x32x2 128 x 128 x 32 kernel (BT 129), which are kept
     // for diagnostic builds (scripts/gemm_tile_compare.sh): the LSTM's GEMMs
     // are short-K (recurrent, K = 200) or weight gradients whose operands stream from HBM,
-    // where 8 resident 64-tile workgroups per CU keep more loads in flight than 2 big ones
+    // where 8 resident 64-tile workgroups per CU keep more loads in flight than 2 big ones.
+    // Also measured slower: the 64 tile with k-contiguous LDS staging read by
+    // ds_read_b128, 16 or 32 deep
     const int BT = 64;
 #endif
     const int TILE = BT == 129 ? 128 : BT;
     const int tm = (g.M + TILE - 1) / TILE, tn = (g.N + TILE - 1) / TILE;
     const int tiles = tm * tn;
-    // split K when the tile grid cannot fill the chip (~8 workgroups per CU, so the loads of
-    // one tile's K-loop hide behind the others' MFMAs) and K is long
+    // split K when the tile grid cannot fill the chip (the resident workgroups per CU, so the
+    // loads of one tile's K-loop hide behind the others' MFMAs) and K is long
     int splits = 1;
     const int target = (BT == 129 ? 2 : 8) * cus;   // the big kernel's 80 KB of LDS: 2 per CU
     if (part && tiles < target && g.K >= 512) {
