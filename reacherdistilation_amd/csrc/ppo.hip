@@ -543,6 +543,28 @@ hipError_t mm(rdp_trainer* t, int M, int N, int K, const float* A, int64_t lda, 
     return rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus);
 }
 
+rdg::GemmArgs gm(int M, int N, int K, const float* A, int64_t lda, int ta, const float* B, int64_t ldb, int tb,
+                 float* C, int64_t ldc, const float* bias = nullptr, int epi = rdg::EPI_NONE,
+                 const float* aux = nullptr, int64_t ldaux = 0) {
+    rdg::GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.lda = lda; g.ta = ta;
+    g.B = B; g.ldb = ldb; g.tb = tb;
+    g.C = C; g.ldc = ldc;
+    g.bias = bias; g.epi = epi; g.aux = aux; g.ldaux = ldaux;
+    return g;
+}
+
+// the policy's and the value net's GEMM of one layer as one grouped launch (rdg::gemm2)
+hipError_t mm2(rdp_trainer* t, const rdg::GemmArgs& pol, const rdg::GemmArgs& vf) {
+#ifdef RD_PPO_UNGROUPED   // diagnostic build: one launch per net (A/B of the grouping)
+    if (hipError_t e = rdg::gemm(t->stream, pol, t->split, SPLIT_FLOATS, t->cus)) return e;
+    return rdg::gemm(t->stream, vf, t->split, SPLIT_FLOATS, t->cus);
+#else
+    return rdg::gemm2(t->stream, pol, vf, t->split, SPLIT_FLOATS, t->cus);
+#endif
+}
+
 
 #define RDP_CK(call, what) RD_HIP((call), what)
 
@@ -588,13 +610,16 @@ int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
                        (const float*)t->rms, (const float*)t->ob, (const float*)t->ac, (const float*)t->lpo,
                        (const float*)t->atarg, (const float*)t->ret, t->Z, t->A, t->LPO, t->ATG, t->RET);
     RDP_CK(hipGetLastError(), "rdp gather");
-    // forward (pol, vf)
-    RDP_CK(mm(t, mb, HID, OBD, t->Z, ZLD, 0, P + PW1, HID, 0, t->H1, HLD, P + PB1, rdg::EPI_TANH), "rdp pol1");
-    RDP_CK(mm(t, mb, HID, HID, t->H1, HLD, 0, P + PW2, HID, 0, t->H2, HLD, P + PB2, rdg::EPI_TANH), "rdp pol2");
-    RDP_CK(mm(t, mb, 2, HID, t->H2, HLD, 0, P + PW3, 2, 0, t->MEAN, 2, P + PB3), "rdp pol3");
-    RDP_CK(mm(t, mb, HID, OBD, t->Z, ZLD, 0, Pv + VW1, HID, 0, t->G1, HLD, Pv + VC1, rdg::EPI_TANH), "rdp vf1");
-    RDP_CK(mm(t, mb, HID, HID, t->G1, HLD, 0, Pv + VW2, HID, 0, t->G2, HLD, Pv + VC2, rdg::EPI_TANH), "rdp vf2");
-    RDP_CK(mm(t, mb, 1, HID, t->G2, HLD, 0, Pv + VW3, 1, 0, t->V, 1, Pv + VC3), "rdp vf3");
+    // forward: layer k of the policy and of the value net in one launch
+    RDP_CK(mm2(t, gm(mb, HID, OBD, t->Z, ZLD, 0, P + PW1, HID, 0, t->H1, HLD, P + PB1, rdg::EPI_TANH),
+               gm(mb, HID, OBD, t->Z, ZLD, 0, Pv + VW1, HID, 0, t->G1, HLD, Pv + VC1, rdg::EPI_TANH)),
+           "rdp pol1 vf1");
+    RDP_CK(mm2(t, gm(mb, HID, HID, t->H1, HLD, 0, P + PW2, HID, 0, t->H2, HLD, P + PB2, rdg::EPI_TANH),
+               gm(mb, HID, HID, t->G1, HLD, 0, Pv + VW2, HID, 0, t->G2, HLD, Pv + VC2, rdg::EPI_TANH)),
+           "rdp pol2 vf2");
+    RDP_CK(mm2(t, gm(mb, 2, HID, t->H2, HLD, 0, P + PW3, 2, 0, t->MEAN, 2, P + PB3),
+               gm(mb, 1, HID, t->G2, HLD, 0, Pv + VW3, 1, 0, t->V, 1, Pv + VC3)),
+           "rdp pol3 vf3");
     const int lblk = (mb + RB - 1) / RB;
     hipLaunchKernelGGL(ppo_loss_kernel, dim3(lblk), dim3(RB), 0, t->stream, mb, P, (const float*)t->MEAN,
                        (const float*)t->V, (const float*)t->A, (const float*)t->LPO, (const float*)t->ATG,
@@ -602,20 +627,23 @@ int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
     hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, t->stream, (const double*)t->part, lblk, g, t->acc,
                        last_epoch ? 1 : 0, t->ctl);
     RDP_CK(hipGetLastError(), "rdp loss");
-    // policy backward: [dW; db] of a layer in one GEMM (the ones column of its input)
-    RDP_CK(mm(t, HID + 1, 2, mb, t->H2, HLD, 1, t->dMEAN, 2, 0, g + PW3, 2), "rdp gW3 gb3");
-    RDP_CK(mm(t, mb, HID, 2, t->dMEAN, 2, 0, P + PW3, 2, 1, t->D2, HID, nullptr, rdg::EPI_DTANH, t->H2, HLD), "rdp d2");
-    RDP_CK(mm(t, HID + 1, HID, mb, t->H1, HLD, 1, t->D2, HID, 0, g + PW2, HID), "rdp gW2 gb2");
-    RDP_CK(mm(t, mb, HID, HID, t->D2, HID, 0, P + PW2, HID, 1, t->D1, HID, nullptr, rdg::EPI_DTANH, t->H1, HLD),
-           "rdp d1");
-    RDP_CK(mm(t, OBD + 1, HID, mb, t->Z, ZLD, 1, t->D1, HID, 0, g + PW1, HID), "rdp gW1 gb1");
-    // value backward
-    RDP_CK(mm(t, HID + 1, 1, mb, t->G2, HLD, 1, t->dV, 1, 0, gv + VW3, 1), "rdp gV3 gc3");
-    RDP_CK(mm(t, mb, HID, 1, t->dV, 1, 0, Pv + VW3, 1, 1, t->E2, HID, nullptr, rdg::EPI_DTANH, t->G2, HLD), "rdp e2");
-    RDP_CK(mm(t, HID + 1, HID, mb, t->G1, HLD, 1, t->E2, HID, 0, gv + VW2, HID), "rdp gV2 gc2");
-    RDP_CK(mm(t, mb, HID, HID, t->E2, HID, 0, Pv + VW2, HID, 1, t->E1, HID, nullptr, rdg::EPI_DTANH, t->G1, HLD),
-           "rdp e1");
-    RDP_CK(mm(t, OBD + 1, HID, mb, t->Z, ZLD, 1, t->E1, HID, 0, gv + VW1, HID), "rdp gV1 gc1");
+    // backward, policy and value side by side: [dW; db] of a layer in one GEMM (the ones
+    // column of its input), then the data gradient with tanh' fused
+    RDP_CK(mm2(t, gm(HID + 1, 2, mb, t->H2, HLD, 1, t->dMEAN, 2, 0, g + PW3, 2),
+               gm(HID + 1, 1, mb, t->G2, HLD, 1, t->dV, 1, 0, gv + VW3, 1)),
+           "rdp gW3 gV3");
+    RDP_CK(mm2(t, gm(mb, HID, 2, t->dMEAN, 2, 0, P + PW3, 2, 1, t->D2, HID, nullptr, rdg::EPI_DTANH, t->H2, HLD),
+               gm(mb, HID, 1, t->dV, 1, 0, Pv + VW3, 1, 1, t->E2, HID, nullptr, rdg::EPI_DTANH, t->G2, HLD)),
+           "rdp d2 e2");
+    RDP_CK(mm2(t, gm(HID + 1, HID, mb, t->H1, HLD, 1, t->D2, HID, 0, g + PW2, HID),
+               gm(HID + 1, HID, mb, t->G1, HLD, 1, t->E2, HID, 0, gv + VW2, HID)),
+           "rdp gW2 gV2");
+    RDP_CK(mm2(t, gm(mb, HID, HID, t->D2, HID, 0, P + PW2, HID, 1, t->D1, HID, nullptr, rdg::EPI_DTANH, t->H1, HLD),
+               gm(mb, HID, HID, t->E2, HID, 0, Pv + VW2, HID, 1, t->E1, HID, nullptr, rdg::EPI_DTANH, t->G1, HLD)),
+           "rdp d1 e1");
+    RDP_CK(mm2(t, gm(OBD + 1, HID, mb, t->Z, ZLD, 1, t->D1, HID, 0, g + PW1, HID),
+               gm(OBD + 1, HID, mb, t->Z, ZLD, 1, t->E1, HID, 0, gv + VW1, HID)),
+           "rdp gW1 gV1");
     AdamArgs aa{t->grad, t->params, t->m, t->v, t->ctl, t->cfg.optim_stepsize * t->lrmult, 0.9f, 0.999f, 1e-8f};
     hipLaunchKernelGGL(adam_kernel, dim3((P_ALL + 255) / 256), dim3(256), 0, t->stream, aa);
     RDP_CK(hipGetLastError(), "rdp adam");

@@ -106,20 +106,21 @@ __device__ __forceinline__ f32x4 load4(const float* p, int valid) {
 
 template <int BT>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[BT / 32][BT / 32], int m0, int n0,
-                                              int wm, int wn, int i, int gq);
+                                              int wm, int wn, int i, int gq, int bz);
 
 // BT x BT C tile per workgroup (BT = 64 or 128); 4 waves in 2 x 2, each (BT/2)^2 =
 // (BT/32)^2 16x16 blocks.  LDS rows are BT + 16 floats: the 4 k-rows of one MFMA operand
 // start 16 banks apart, so 16 consecutive m (or n) x 4 k hit 64 distinct banks.
+// The tile (bx, by) of K split bz; gemm_kernel and the grouped gemm_kernel_g2 run it.
 template <int BT, bool TA, bool TB, bool VEC>
-__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz) {
     constexpr int LS = BT + 16, FB = BT / 32, NQ = BT / 64;   // blocks per wave dim, loads per thread
     __shared__ __attribute__((aligned(16))) float As[2][TK][LS];
     __shared__ __attribute__((aligned(16))) float Bs[2][TK][LS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int wm = wave >> 1, wn = wave & 1;
-    const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT;
-    const int kbeg = blockIdx.z * g.kchunk;
+    const int m0 = by * BT, n0 = bx * BT;
+    const int kbeg = bz * g.kchunk;
     const int kend = min(g.K, kbeg + g.kchunk);
 
     // quad q of a tile: [row][4 quads of k] (k-contiguous) or [k][BT/4 quads] (k-strided)
@@ -211,14 +212,31 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
         }
         __syncthreads();
     }
-    gemm_epilogue<BT>(g, acc, m0, n0, wm, wn, i, gq);
+    gemm_epilogue<BT>(g, acc, m0, n0, wm, wn, i, gq, bz);
+}
+
+template <int BT, bool TA, bool TB, bool VEC>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
+    gemm_tile<BT, TA, TB, VEC>(g, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Two independent problems of one orientation in one launch (the PPO policy and value nets'
+// layers): grid z = g0's K splits then g1's; x, y cover the larger tile grid and the blocks
+// beyond a problem's own grid exit.
+template <int BT, bool TA, bool TB, bool VEC>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel_g2(GemmArgs g0, GemmArgs g1) {
+    const bool first = (int)blockIdx.z < g0.splits;
+    const GemmArgs& g = first ? g0 : g1;
+    const int bz = first ? (int)blockIdx.z : (int)blockIdx.z - g0.splits;
+    if ((int)blockIdx.x * BT >= g.N || (int)blockIdx.y * BT >= g.M) return;
+    gemm_tile<BT, TA, TB, VEC>(g, blockIdx.x, blockIdx.y, bz);
 }
 
 // The C tile's epilogue (every kernel of this file): acc[x][y][r] = C[m0 + (BT/2) wm + 16x +
 // 4gq + r][n0 + (BT/2) wn + 16y + i].
 template <int BT>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[BT / 32][BT / 32], int m0, int n0,
-                                              int wm, int wn, int i, int gq) {
+                                              int wm, int wn, int i, int gq, int bz) {
     constexpr int FB = BT / 32;
     if (g.epi == EPI_LSTM_BWD && g.splits <= 1) {   // (uniform) the cell backward per output
 #pragma unroll
@@ -259,7 +277,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[BT
                 const int row = m0 + (BT / 2) * wm + 16 * x + 4 * gq + r, col = n0 + (BT / 2) * wn + 16 * y + i;
                 if (row >= g.M || col >= g.N) continue;
                 if (g.splits > 1)
-                    g.part[((int64_t)blockIdx.z * g.M + row) * g.N + col] = acc[x][y][r];
+                    g.part[((int64_t)bz * g.M + row) * g.N + col] = acc[x][y][r];
                 else
                     g.C[(int64_t)row * g.ldc + col] = epi_value(g, acc[x][y][r], in_b[x][y], in_a[x][y][r],
                                                                in_c[x][y][r]);
@@ -394,11 +412,10 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel_big(GemmArgs g) {
 
 // split-K: C = epi(sum_z part[z]) in a fixed order.  64 outputs per block, 4 interleaved
 // split phases per output (summed in a fixed order at the end).
-template <int = 0>   // a template: one definition per translation unit that includes this header
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
+__device__ __forceinline__ void splitk_reduce_block(const GemmArgs& g, int64_t blk) {
     __shared__ float s[4][64];
     const int64_t MN = (int64_t)g.M * g.N;
-    const int64_t idx = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int64_t idx = blk * 64 + (threadIdx.x & 63);
     const int ph = threadIdx.x >> 6;
     float a = 0.f, b = 0.f;
     if (idx < MN) {
@@ -421,6 +438,40 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
     }
 }
 
+template <int = 0>   // a template: one definition per translation unit that includes this header
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
+    splitk_reduce_block(g, blockIdx.x);
+}
+
+// grouped: blocks [0, nb0) reduce g0 (when it is split), the rest g1
+template <int = 0>
+__global__ __launch_bounds__(256) void splitk_reduce_g2(GemmArgs g0, GemmArgs g1, int nb0) {
+    if ((int)blockIdx.x < nb0) splitk_reduce_block(g0, blockIdx.x);
+    else splitk_reduce_block(g1, (int)blockIdx.x - nb0);
+}
+
+// Split K when the tile grid cannot fill the chip (`per_cu` resident workgroups per CU, so
+// the loads of one tile's K-loop hide behind the others' MFMAs) and K is long.
+inline void gemm_plan(GemmArgs& g, int tile, int per_cu, float* part, int64_t part_floats, int cus) {
+    const int tiles = ((g.M + tile - 1) / tile) * ((g.N + tile - 1) / tile);
+    int splits = 1;
+    const int target = per_cu * cus;
+    if (part && tiles < target && g.K >= 512) {
+        splits = (target + tiles - 1) / tiles;
+        const int maxs = g.K / 256 < 256 ? g.K / 256 : 256;   // >= 16 k-tiles per split, <= 256 partials
+        if (splits > maxs) splits = maxs;
+        while (splits > 1 && (int64_t)splits * g.M * g.N > part_floats) --splits;
+    }
+    g.splits = splits;
+    g.part = part;
+    g.kchunk = splits > 1 ? (((g.K + splits - 1) / splits + 31) / 32) * 32 : g.K;   // multiple of both K tiles
+    if (splits > 1) g.splits = (g.K + g.kchunk - 1) / g.kchunk;
+}
+
+inline bool gemm_vec(const GemmArgs& g) {
+    return ((uintptr_t)g.A % 16 == 0) && ((uintptr_t)g.B % 16 == 0) && g.lda % 4 == 0 && g.ldb % 4 == 0;
+}
+
 // Launch; `part`/`part_floats` = split-K workspace (may be null: no split).  Returns a hip error.
 inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_floats, int cus) {
     if (g.M <= 0 || g.N <= 0) return hipSuccess;
@@ -440,22 +491,8 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
 #endif
     const int TILE = BT == 129 ? 128 : BT;
     const int tm = (g.M + TILE - 1) / TILE, tn = (g.N + TILE - 1) / TILE;
-    const int tiles = tm * tn;
-    // split K when the tile grid cannot fill the chip (the resident workgroups per CU, so the
-    // loads of one tile's K-loop hide behind the others' MFMAs) and K is long
-    int splits = 1;
-    const int target = (BT == 129 ? 2 : 8) * cus;   // the big kernel's 80 KB of LDS: 2 per CU
-    if (part && tiles < target && g.K >= 512) {
-        splits = (target + tiles - 1) / tiles;
-        const int maxs = g.K / 256 < 256 ? g.K / 256 : 256;   // >= 16 k-tiles per split, <= 256 partials
-        if (splits > maxs) splits = maxs;
-        while (splits > 1 && (int64_t)splits * g.M * g.N > part_floats) --splits;
-    }
-    g.splits = splits;
-    g.part = part;
-    g.kchunk = splits > 1 ? (((g.K + splits - 1) / splits + 31) / 32) * 32 : g.K;   // multiple of both K tiles
-    if (splits > 1) g.splits = (g.K + g.kchunk - 1) / g.kchunk;
-    const bool vec = ((uintptr_t)g.A % 16 == 0) && ((uintptr_t)g.B % 16 == 0) && g.lda % 4 == 0 && g.ldb % 4 == 0;
+    gemm_plan(g, TILE, BT == 129 ? 2 : 8, part, part_floats, cus);   // the big kernel's 80 KB of LDS: 2 per CU
+    const bool vec = gemm_vec(g);
     dim3 grid(tn, tm, g.splits);
 #define RDG_LAUNCH(BT_, TA_, TB_, V_) \
     hipLaunchKernelGGL((gemm_kernel<BT_, TA_, TB_, V_>), grid, dim3(GEMM_THREADS), 0, st, g)
@@ -498,6 +535,52 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
     const int64_t MN = (int64_t)g.M * g.N;
     hipLaunchKernelGGL(splitk_reduce_kernel<0>, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, g);
     return hipGetLastError();
+}
+
+// Two independent problems of one orientation (same ta, tb) as ONE launch of the 64 tile, plus
+// one grouped split-K reduce when either is split: the PPO policy and value nets run their
+// layers side by side (half the dependent launches of a minibatch).  The split-K workspace is
+// halved between them.  Problems that do not pair (orientation, 16-B alignment) and the
+// diagnostic tile builds run as two gemm() calls.  Same tiles, splits and k order as gemm().
+inline hipError_t gemm2(hipStream_t st, GemmArgs g0, GemmArgs g1, float* part, int64_t part_floats, int cus) {
+#ifndef RD_GEMM_BT
+    const bool pair = g0.M > 0 && g0.N > 0 && g1.M > 0 && g1.N > 0 && g0.ta == g1.ta && g0.tb == g1.tb &&
+                      gemm_vec(g0) == gemm_vec(g1);
+    if (pair) {
+        const int64_t half = part_floats / 2;
+        gemm_plan(g0, 64, 8, part, half, cus);
+        gemm_plan(g1, 64, 8, part ? part + half : nullptr, half, cus);
+        const int tn = ((g0.N > g1.N ? g0.N : g1.N) + 63) / 64, tm = ((g0.M > g1.M ? g0.M : g1.M) + 63) / 64;
+        dim3 grid(tn, tm, g0.splits + g1.splits);
+#define RDG_LAUNCH2(TA_, TB_, V_) \
+    hipLaunchKernelGGL((gemm_kernel_g2<64, TA_, TB_, V_>), grid, dim3(GEMM_THREADS), 0, st, g0, g1)
+        if (gemm_vec(g0)) {
+            if (!g0.ta && !g0.tb) RDG_LAUNCH2(false, false, true);
+            else if (!g0.ta && g0.tb) RDG_LAUNCH2(false, true, true);
+            else if (g0.ta && !g0.tb) RDG_LAUNCH2(true, false, true);
+            else RDG_LAUNCH2(true, true, true);
+        } else {
+            if (!g0.ta && !g0.tb) RDG_LAUNCH2(false, false, false);
+            else if (!g0.ta && g0.tb) RDG_LAUNCH2(false, true, false);
+            else if (g0.ta && !g0.tb) RDG_LAUNCH2(true, false, false);
+            else RDG_LAUNCH2(true, true, false);
+        }
+#undef RDG_LAUNCH2
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess || (g0.splits <= 1 && g1.splits <= 1)) return e;
+        const int nb0 = g0.splits > 1 ? (int)(((int64_t)g0.M * g0.N + 63) / 64) : 0;
+        const int nb1 = g1.splits > 1 ? (int)(((int64_t)g1.M * g1.N + 63) / 64) : 0;
+        // an unsplit problem contributes no reduce blocks: give the grouped kernel g1 first
+        if (nb0 == 0)
+            hipLaunchKernelGGL(splitk_reduce_g2<0>, dim3((unsigned)nb1), dim3(256), 0, st, g1, g1, nb1);
+        else
+            hipLaunchKernelGGL(splitk_reduce_g2<0>, dim3((unsigned)(nb0 + nb1)), dim3(256), 0, st, g0, g1, nb0);
+        return hipGetLastError();
+    }
+#endif
+    hipError_t e = gemm(st, g0, part, part_floats, cus);
+    if (e != hipSuccess) return e;
+    return gemm(st, g1, part, part_floats, cus);
 }
 
 }  // namespace rdg
