@@ -111,12 +111,19 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[BT
 // BT x BT C tile per workgroup (BT = 64 or 128); 4 waves in 2 x 2, each (BT/2)^2 =
 // (BT/32)^2 16x16 blocks.  LDS rows are BT + 16 floats: the 4 k-rows of one MFMA operand
 // start 16 banks apart, so 16 consecutive m (or n) x 4 k hit 64 distinct banks.
-// The tile (bx, by) of K split bz; gemm_kernel and the grouped gemm_kernel_g2 run it.
+// The tile (bx, by) of K split bz; gemm_kernel and the grouped kernels run it on the LDS
+// staging buffers the kernel declares ([2][TK][BT + 16] floats each).
+template <int BT>
+struct TileLds {
+    float A[2][TK][BT + 16];
+    float B[2][TK][BT + 16];
+};
+
 template <int BT, bool TA, bool TB, bool VEC>
-__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz) {
-    constexpr int LS = BT + 16, FB = BT / 32, NQ = BT / 64;   // blocks per wave dim, loads per thread
-    __shared__ __attribute__((aligned(16))) float As[2][TK][LS];
-    __shared__ __attribute__((aligned(16))) float Bs[2][TK][LS];
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz, TileLds<BT>& lds) {
+    constexpr int FB = BT / 32, NQ = BT / 64;   // blocks per wave dim, loads per thread
+    auto& As = lds.A;
+    auto& Bs = lds.B;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int wm = wave >> 1, wn = wave & 1;
     const int m0 = by * BT, n0 = bx * BT;
@@ -217,19 +224,43 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
 
 template <int BT, bool TA, bool TB, bool VEC>
 __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs g) {
-    gemm_tile<BT, TA, TB, VEC>(g, blockIdx.x, blockIdx.y, blockIdx.z);
+    __shared__ __attribute__((aligned(16))) TileLds<BT> lds;
+    gemm_tile<BT, TA, TB, VEC>(g, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
-// Two independent problems of one orientation in one launch (the PPO policy and value nets'
-// layers): grid z = g0's K splits then g1's; x, y cover the larger tile grid and the blocks
-// beyond a problem's own grid exit.
+// Two independent problems in one launch (the PPO policy and value nets' layers; a head
+// layer's weight and data gradients): a 1-D grid, blocks [0, n0) = g0's tiles x K splits, the
+// rest g1's, so two very different shapes cost no empty blocks.
+struct Group2 {
+    int tn0, tm0, n0, tn1, tm1;
+};
+
+__device__ __forceinline__ void group2_decode(const Group2& q, int bid, int& which, int& bx, int& by, int& bz) {
+    which = bid >= q.n0;
+    const int b = which ? bid - q.n0 : bid;
+    const int tn = which ? q.tn1 : q.tn0, tm = which ? q.tm1 : q.tm0;
+    bx = b % tn;
+    by = (b / tn) % tm;
+    bz = b / (tn * tm);
+}
+
 template <int BT, bool TA, bool TB, bool VEC>
-__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel_g2(GemmArgs g0, GemmArgs g1) {
-    const bool first = (int)blockIdx.z < g0.splits;
-    const GemmArgs& g = first ? g0 : g1;
-    const int bz = first ? (int)blockIdx.z : (int)blockIdx.z - g0.splits;
-    if ((int)blockIdx.x * BT >= g.N || (int)blockIdx.y * BT >= g.M) return;
-    gemm_tile<BT, TA, TB, VEC>(g, blockIdx.x, blockIdx.y, bz);
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel_g2(GemmArgs g0, GemmArgs g1, Group2 q) {
+    int which, bx, by, bz;
+    group2_decode(q, blockIdx.x, which, bx, by, bz);
+    __shared__ __attribute__((aligned(16))) TileLds<BT> lds;
+    gemm_tile<BT, TA, TB, VEC>(which ? g1 : g0, bx, by, bz, lds);
+}
+
+// the same for two problems of DIFFERENT orientations (a weight gradient Hᵀ·dZ beside a data
+// gradient dZ·Wᵀ): one LDS buffer set, the orientation chosen per block
+template <bool TA0, bool TB0, bool TA1, bool TB1>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel_g2m(GemmArgs g0, GemmArgs g1, Group2 q) {
+    int which, bx, by, bz;
+    group2_decode(q, blockIdx.x, which, bx, by, bz);
+    __shared__ __attribute__((aligned(16))) TileLds<64> lds;
+    if (!which) gemm_tile<64, TA0, TB0, true>(g0, bx, by, bz, lds);
+    else gemm_tile<64, TA1, TB1, true>(g1, bx, by, bz, lds);
 }
 
 // The C tile's epilogue (every kernel of this file): acc[x][y][r] = C[m0 + (BT/2) wm + 16x +
@@ -537,11 +568,22 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
     return hipGetLastError();
 }
 
-// Two independent problems of one orientation (same ta, tb) as ONE launch of the 64 tile, plus
+// Two independent problems of one orientation (same ta, tb) -- or a weight gradient (1, 0)
+// beside a data gradient (0, 1) -- as ONE launch of the 64 tile, plus
 // one grouped split-K reduce when either is split: the PPO policy and value nets run their
 // layers side by side (half the dependent launches of a minibatch).  The split-K workspace is
 // halved between them.  Problems that do not pair (orientation, 16-B alignment) and the
 // diagnostic tile builds run as two gemm() calls.  Same tiles, splits and k order as gemm().
+inline Group2 group2(const GemmArgs& g0, const GemmArgs& g1) {
+    Group2 q;
+    q.tn0 = (g0.N + 63) / 64;
+    q.tm0 = (g0.M + 63) / 64;
+    q.n0 = q.tn0 * q.tm0 * g0.splits;
+    q.tn1 = (g1.N + 63) / 64;
+    q.tm1 = (g1.M + 63) / 64;
+    return q;
+}
+
 inline hipError_t gemm2(hipStream_t st, GemmArgs g0, GemmArgs g1, float* part, int64_t part_floats, int cus) {
 #ifndef RD_GEMM_BT
     const bool pair = g0.M > 0 && g0.N > 0 && g1.M > 0 && g1.N > 0 && g0.ta == g1.ta && g0.tb == g1.tb &&
@@ -550,10 +592,10 @@ inline hipError_t gemm2(hipStream_t st, GemmArgs g0, GemmArgs g1, float* part, i
         const int64_t half = part_floats / 2;
         gemm_plan(g0, 64, 8, part, half, cus);
         gemm_plan(g1, 64, 8, part ? part + half : nullptr, half, cus);
-        const int tn = ((g0.N > g1.N ? g0.N : g1.N) + 63) / 64, tm = ((g0.M > g1.M ? g0.M : g1.M) + 63) / 64;
-        dim3 grid(tn, tm, g0.splits + g1.splits);
+        const Group2 q = group2(g0, g1);
+        dim3 grid((unsigned)(q.n0 + q.tn1 * q.tm1 * g1.splits));
 #define RDG_LAUNCH2(TA_, TB_, V_) \
-    hipLaunchKernelGGL((gemm_kernel_g2<64, TA_, TB_, V_>), grid, dim3(GEMM_THREADS), 0, st, g0, g1)
+    hipLaunchKernelGGL((gemm_kernel_g2<64, TA_, TB_, V_>), grid, dim3(GEMM_THREADS), 0, st, g0, g1, q)
         if (gemm_vec(g0)) {
             if (!g0.ta && !g0.tb) RDG_LAUNCH2(false, false, true);
             else if (!g0.ta && g0.tb) RDG_LAUNCH2(false, true, true);
@@ -571,6 +613,27 @@ inline hipError_t gemm2(hipStream_t st, GemmArgs g0, GemmArgs g1, float* part, i
         const int nb0 = g0.splits > 1 ? (int)(((int64_t)g0.M * g0.N + 63) / 64) : 0;
         const int nb1 = g1.splits > 1 ? (int)(((int64_t)g1.M * g1.N + 63) / 64) : 0;
         // an unsplit problem contributes no reduce blocks: give the grouped kernel g1 first
+        if (nb0 == 0)
+            hipLaunchKernelGGL(splitk_reduce_g2<0>, dim3((unsigned)nb1), dim3(256), 0, st, g1, g1, nb1);
+        else
+            hipLaunchKernelGGL(splitk_reduce_g2<0>, dim3((unsigned)(nb0 + nb1)), dim3(256), 0, st, g0, g1, nb0);
+        return hipGetLastError();
+    }
+    // a layer's weight gradient (ta, tb) = (1, 0) beside its data gradient (0, 1), both 16-B
+    // aligned: one launch of the mixed kernel
+    const bool mixed = g0.M > 0 && g0.N > 0 && g1.M > 0 && g1.N > 0 && g0.ta == 1 && g0.tb == 0 && g1.ta == 0 &&
+                       g1.tb == 1 && gemm_vec(g0) && gemm_vec(g1);
+    if (mixed) {
+        const int64_t half = part_floats / 2;
+        gemm_plan(g0, 64, 8, part, half, cus);
+        gemm_plan(g1, 64, 8, part ? part + half : nullptr, half, cus);
+        const Group2 q = group2(g0, g1);
+        hipLaunchKernelGGL((gemm_kernel_g2m<true, false, false, true>), dim3((unsigned)(q.n0 + q.tn1 * q.tm1 * g1.splits)),
+                           dim3(GEMM_THREADS), 0, st, g0, g1, q);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess || (g0.splits <= 1 && g1.splits <= 1)) return e;
+        const int nb0 = g0.splits > 1 ? (int)(((int64_t)g0.M * g0.N + 63) / 64) : 0;
+        const int nb1 = g1.splits > 1 ? (int)(((int64_t)g1.M * g1.N + 63) / 64) : 0;
         if (nb0 == 0)
             hipLaunchKernelGGL(splitk_reduce_g2<0>, dim3((unsigned)nb1), dim3(256), 0, st, g1, g1, nb1);
         else

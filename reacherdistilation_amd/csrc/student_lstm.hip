@@ -7,12 +7,13 @@
 // MI355X mapping.  Rows = (t, window) pairs, t-major, so every per-step slice is contiguous.
 // All GEMM-shaped work runs on one MFMA GEMM (csrc/rd_gemm.h) with fused epilogues:
 //  * the input half of the gate GEMM, [x_t] . Wl[0:43], is ONE GEMM over all T x B rows
-//    (bias fused); only the recurrent half h_{t-1} . Wl[43:243] is per step (accumulating
-//    into the same gate buffer), followed by the elementwise cell kernel;
+//    (bias fused); only the recurrent half h_{t-1} . Wl[43:243] is per step, with the cell
+//    fused into its epilogue (lstm_rec_fwd_kernel);
 //  * the head runs once over all T x B rows after the recurrence (bias + tanh fused);
-//  * backward: the head's data gradients fuse the tanh derivative of the stored activation
-//    into the GEMM epilogue; BPTT is per step (cell kernel, then dh_{t-1} = dz_t Wr^T); the
-//    LSTM weight gradients are two GEMMs over all T x B rows at the end ([x | h_prev]^T dz),
+//  * backward: each head layer's weight gradient and data gradient (tanh' of the stored
+//    activation fused) run as one grouped launch (rdg::gemm2); BPTT is one launch per step,
+//    dh_{t-1} = dz_t Wr^T with the cell backward of step t-1 in its epilogue; the LSTM weight
+//    gradients ([x | h_prev]^T dz over all T x B rows) are one grouped launch at the end,
 //    split-K with a fixed-order reduction when the output tile grid is small;
 //  * bias gradients are deterministic two-level column sums; no atomics anywhere.
 // Activations of all steps stay resident in HBM (sized at create for max_windows).
@@ -395,6 +396,28 @@ hipError_t mm(rdl_trainer* t, int M, int N, int K, const float* A, int64_t lda, 
     return rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus);
 }
 
+rdg::GemmArgs ga(int M, int N, int K, const float* A, int64_t lda, int ta, const float* B, int64_t ldb, int tb,
+                 float* C, int64_t ldc, int epi = rdg::EPI_NONE, const float* aux = nullptr, int64_t ldaux = 0) {
+    rdg::GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.lda = lda; g.ta = ta;
+    g.B = B; g.ldb = ldb; g.tb = tb;
+    g.C = C; g.ldc = ldc;
+    g.epi = epi; g.aux = aux; g.ldaux = ldaux;
+    return g;
+}
+
+// two independent GEMMs as one grouped launch (rdg::gemm2): a head layer's weight gradient
+// beside its data gradient, the two halves of the LSTM weight gradient
+hipError_t mm2(rdl_trainer* t, const rdg::GemmArgs& g0, const rdg::GemmArgs& g1) {
+#ifdef RD_LSTM_UNGROUPED   // diagnostic build: one launch per GEMM
+    if (hipError_t e = rdg::gemm(t->stream, g0, t->split, SPLIT_FLOATS, t->cus)) return e;
+    return rdg::gemm(t->stream, g1, t->split, SPLIT_FLOATS, t->cus);
+#else
+    return rdg::gemm2(t->stream, g0, g1, t->split, SPLIT_FLOATS, t->cus);
+#endif
+}
+
 hipError_t colsum(rdl_trainer* t, const float* src, int64_t M, int N, int64_t ld, float* out) {
     const unsigned gx = (unsigned)((N + 63) / 64);
     if (M <= COLSUM_CHUNK) {
@@ -476,21 +499,24 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
                        t->ctl, t->hist, t->cfg.metrics_len);
     RDL_CK(hipGetLastError(), "rdl metrics_kernel");
     // head backward (weight gradients over all rows; data gradients with the tanh derivative fused)
-    RDL_CK(mm(t, H4 + 1, 4, Ri, t->A4, L4, 1, t->dY, 4, 0, g + OFF_W5, 4), "rdl dW5 db5");
-    RDL_CK(mm(t, Ri, H4, 4, t->dY, 4, 0, P + OFF_W5, 4, 1, t->D32, H4, nullptr, rdg::EPI_DTANH, t->A4, L4), "rdl dZ4");
-    RDL_CK(mm(t, H3 + 1, H4, Ri, t->A3, L3, 1, t->D32, H4, 0, g + OFF_W4, H4), "rdl dW4 db4");
-    RDL_CK(mm(t, Ri, H3, H4, t->D32, H4, 0, P + OFF_W4, H4, 1, t->D64a, H3, nullptr, rdg::EPI_DTANH, t->A3, L3),
-           "rdl dZ3");
-    RDL_CK(mm(t, H2 + 1, H3, Ri, t->A2, L2, 1, t->D64a, H3, 0, g + OFF_W3, H3), "rdl dW3 db3");
-    RDL_CK(mm(t, Ri, H2, H3, t->D64a, H3, 0, P + OFF_W3, H3, 1, t->D128, H2, nullptr, rdg::EPI_DTANH, t->A2, L2),
-           "rdl dZ2");
-    RDL_CK(mm(t, H1 + 1, H2, Ri, t->A1, L1, 1, t->D128, H2, 0, g + OFF_W2, H2), "rdl dW2 db2");
-    RDL_CK(mm(t, Ri, H1, H2, t->D128, H2, 0, P + OFF_W2, H2, 1, t->D64b, H1, nullptr, rdg::EPI_DTANH, t->A1, L1),
-           "rdl dZ1");
+    // per layer, [dW; db] (weight gradient, ones column) beside the data gradient with tanh'
+    RDL_CK(mm2(t, ga(H4 + 1, 4, Ri, t->A4, L4, 1, t->dY, 4, 0, g + OFF_W5, 4),
+               ga(Ri, H4, 4, t->dY, 4, 0, P + OFF_W5, 4, 1, t->D32, H4, rdg::EPI_DTANH, t->A4, L4)),
+           "rdl dW5 db5 | dZ4");
+    RDL_CK(mm2(t, ga(H3 + 1, H4, Ri, t->A3, L3, 1, t->D32, H4, 0, g + OFF_W4, H4),
+               ga(Ri, H3, H4, t->D32, H4, 0, P + OFF_W4, H4, 1, t->D64a, H3, rdg::EPI_DTANH, t->A3, L3)),
+           "rdl dW4 db4 | dZ3");
+    RDL_CK(mm2(t, ga(H2 + 1, H3, Ri, t->A2, L2, 1, t->D64a, H3, 0, g + OFF_W3, H3),
+               ga(Ri, H2, H3, t->D64a, H3, 0, P + OFF_W3, H3, 1, t->D128, H2, rdg::EPI_DTANH, t->A2, L2)),
+           "rdl dW3 db3 | dZ2");
+    RDL_CK(mm2(t, ga(H1 + 1, H2, Ri, t->A1, L1, 1, t->D128, H2, 0, g + OFF_W2, H2),
+               ga(Ri, H1, H2, t->D128, H2, 0, P + OFF_W2, H2, 1, t->D64b, H1, rdg::EPI_DTANH, t->A1, L1)),
+           "rdl dW2 db2 | dZ1");
     const float* Hc = t->H + B * U;
-    RDL_CK(mm(t, U, H1, Ri, Hc, U, 1, t->D64b, H1, 0, g + OFF_W1, H1), "rdl dW1");
+    RDL_CK(mm2(t, ga(U, H1, Ri, Hc, U, 1, t->D64b, H1, 0, g + OFF_W1, H1),
+               ga(Ri, U, H1, t->D64b, H1, 0, P + OFF_W1, H1, 1, t->dHh, U)),
+           "rdl dW1 | dHhead");
     RDL_CK(colsum(t, t->D64b, R, H1, H1, g + OFF_B1), "rdl db1");
-    RDL_CK(mm(t, Ri, U, H1, t->D64b, H1, 0, P + OFF_W1, H1, 1, t->dHh, U), "rdl dHhead");
     // BPTT (the gate buffer Z is reused for dz: the forward keeps activations in G)
     float* dZl = t->Z;
     RDL_CK(hipMemsetAsync(t->dc, 0, sizeof(float) * B * U, t->stream), "rdl bptt");
@@ -531,8 +557,9 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     }
 #endif
     // LSTM weights: dWl = [x | h_prev]^T dz over all rows; dbl; then dp -> dWp, dbp
-    RDL_CK(mm(t, XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4), "rdl dWl x");
-    RDL_CK(mm(t, U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4), "rdl dWl h");
+    RDL_CK(mm2(t, ga(XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4),
+               ga(U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4)),
+           "rdl dWl x | h");
     RDL_CK(colsum(t, dZl, R, G4, G4, g + OFF_BL), "rdl dbl");
     RDL_CK(mm(t, Ri, 32, G4, dZl, G4, 0, P + OFF_WL + 11 * G4, G4, 1, t->dP, 32), "rdl dP");
     RDL_CK(mm(t, 4, 32, Ri, prev, 4, 1, t->dP, 32, 0, g + OFF_WP, 32), "rdl dWp");
