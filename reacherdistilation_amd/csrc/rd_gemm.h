@@ -70,6 +70,15 @@ __device__ __forceinline__ void lstm_bwd_point(const GemmArgs& g, int64_t row, i
 }
 
 constexpr int TK = 16, GEMM_THREADS = 256;
+// K tiles of global loads kept in flight by the 64/128-tile kernels (register ring).  1: tile
+// t+2's loads issue right after tile t+1 is written to LDS, so they span a barrier and a whole
+// MFMA phase.  Measured (LSTM 20 / 1,024 / 16,384 windows, PPO iteration): depth 1 0.467 /
+// 0.679 / 4.31 ms, 63.1 ms; depth 3 0.474 / 0.691 / 4.37, 64.9; depth 5 0.472 / 0.693 / 4.41,
+// 65.6; the previous loop (next tile loaded at the top of the step) 0.485 / 0.709 / 4.42, 70.0.
+#ifndef RDG_PF
+#define RDG_PF 1
+#endif
+constexpr int PF = RDG_PF;
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, int row, int col, float v) {
     if (g.bias) v += g.bias[col];
@@ -176,7 +185,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
 #pragma unroll
         for (int y = 0; y < FB; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // K loop: tile kt is in LDS buffer kt & 1; the global loads of the next PF tiles are in
+    // flight in a register ring (slot = tile % PF), so a step waits for a load issued PF
+    // steps earlier rather than one (small-M GEMMs are a chain of load latencies otherwise)
     const int ntiles = kend > kbeg ? (kend - kbeg + TK - 1) / TK : 0;
+    f32x4 ra[PF][NQ], rb[PF][NQ];
     if (ntiles > 0) {
 #pragma unroll
         for (int u = 0; u < NQ; ++u) {
@@ -184,40 +197,51 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
             store_b(0, tid + GEMM_THREADS * u, load_b(kbeg, tid + GEMM_THREADS * u));
         }
     }
+#pragma unroll
+    for (int p = 1; p <= PF; ++p)
+        if (p < ntiles)
+#pragma unroll
+            for (int u = 0; u < NQ; ++u) {
+                ra[p % PF][u] = load_a(kbeg + p * TK, tid + GEMM_THREADS * u);
+                rb[p % PF][u] = load_b(kbeg + p * TK, tid + GEMM_THREADS * u);
+            }
     __syncthreads();
-    for (int kt = 0; kt < ntiles; ++kt) {
-        const int buf = kt & 1;
-        f32x4 na[NQ], nb[NQ];
-        const bool more = kt + 1 < ntiles;
-        if (more) {
+    for (int kt0 = 0; kt0 < ntiles; kt0 += PF) {
 #pragma unroll
-            for (int u = 0; u < NQ; ++u) {
-                na[u] = load_a(kbeg + (kt + 1) * TK, tid + GEMM_THREADS * u);
-                nb[u] = load_b(kbeg + (kt + 1) * TK, tid + GEMM_THREADS * u);
+        for (int j = 0; j < PF; ++j) {
+            const int kt = kt0 + j;
+            if (kt >= ntiles) break;
+            const int buf = kt & 1;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int kk = 4 * s + gq;
+                float a[FB], b[FB];
+#pragma unroll
+                for (int x = 0; x < FB; ++x) a[x] = As[buf][kk][(BT / 2) * wm + 16 * x + i];
+#pragma unroll
+                for (int y = 0; y < FB; ++y) b[y] = Bs[buf][kk][(BT / 2) * wn + 16 * y + i];
+#pragma unroll
+                for (int x = 0; x < FB; ++x)
+#pragma unroll
+                    for (int y = 0; y < FB; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x], b[y], acc[x][y], 0, 0, 0);
             }
-        }
+            const int SL = (j + 1) % PF;   // the slot of tile kt + 1 (kt0 is a multiple of PF; unrolled)
+            if (kt + 1 < ntiles) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int kk = 4 * s + gq;
-            float a[FB], b[FB];
+                for (int u = 0; u < NQ; ++u) {
+                    store_a(buf ^ 1, tid + GEMM_THREADS * u, ra[SL][u]);
+                    store_b(buf ^ 1, tid + GEMM_THREADS * u, rb[SL][u]);
+                }
+                if (kt + 1 + PF < ntiles)   // refill the slot with tile kt + 1 + PF
 #pragma unroll
-            for (int x = 0; x < FB; ++x) a[x] = As[buf][kk][(BT / 2) * wm + 16 * x + i];
-#pragma unroll
-            for (int y = 0; y < FB; ++y) b[y] = Bs[buf][kk][(BT / 2) * wn + 16 * y + i];
-#pragma unroll
-            for (int x = 0; x < FB; ++x)
-#pragma unroll
-                for (int y = 0; y < FB; ++y)
-                    acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x], b[y], acc[x][y], 0, 0, 0);
-        }
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < NQ; ++u) {
-                store_a(buf ^ 1, tid + GEMM_THREADS * u, na[u]);
-                store_b(buf ^ 1, tid + GEMM_THREADS * u, nb[u]);
+                    for (int u = 0; u < NQ; ++u) {
+                        ra[SL][u] = load_a(kbeg + (kt + 1 + PF) * TK, tid + GEMM_THREADS * u);
+                        rb[SL][u] = load_b(kbeg + (kt + 1 + PF) * TK, tid + GEMM_THREADS * u);
+                    }
             }
+            __syncthreads();
         }
-        __syncthreads();
     }
     gemm_epilogue<BT>(g, acc, m0, n0, wm, wn, i, gq, bz);
 }
