@@ -147,17 +147,14 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
     rdg::f32x4 acc[4];
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[y] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+    // load pipeline of rd_gemm.h: tile t+2's loads issue right after tile t+1 is staged, so
+    // they stay in flight across the barrier and the next MFMA phase
     constexpr int NT = (U + RF_TK - 1) / RF_TK;
     stage(0, load_a(0), load_b(0));
+    rdg::f32x4 na = load_a(RF_TK), nb = load_b(RF_TK);
     __syncthreads();
     for (int kt = 0; kt < NT; ++kt) {
         const int buf = kt & 1;
-        const bool more = kt + 1 < NT;
-        rdg::f32x4 na, nb;
-        if (more) {
-            na = load_a((kt + 1) * RF_TK);
-            nb = load_b((kt + 1) * RF_TK);
-        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int kk = 4 * s + gq;
@@ -166,7 +163,13 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
             for (int y = 0; y < 4; ++y)
                 acc[y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[buf][kk][16 * y + i], acc[y], 0, 0, 0);
         }
-        if (more) stage(buf ^ 1, na, nb);
+        if (kt + 1 < NT) {
+            stage(buf ^ 1, na, nb);
+            if (kt + 2 < NT) {
+                na = load_a((kt + 2) * RF_TK);
+                nb = load_b((kt + 2) * RF_TK);
+            }
+        }
         __syncthreads();
     }
     // epilogue: operands first, then TF1 LSTMCell (cell_fwd_kernel's arithmetic)
