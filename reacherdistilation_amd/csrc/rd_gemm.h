@@ -1,4 +1,5 @@
-// f32 GEMM on gfx950 MFMA for the LSTM student (csrc/student_lstm.hip):
+// f32 GEMM on gfx950 MFMA for the LSTM student and the PPO teacher (csrc/student_lstm.hip,
+// csrc/ppo.hip):
 //   C[M x N] (+)= epi( op(A)[M x K] . op(B)[K x N] + bias[N] )
 // op(A) = A stored [M][lda] (ta = 0) or [K][lda] (ta = 1, A^T); likewise B [K][ldb] / [N][ldb].
 // Epilogues: none, tanh, or x (1 - aux^2) (the tanh derivative of a stored activation);
@@ -7,12 +8,14 @@
 // a store (csrc/student_lstm.hip).  Deterministic: fixed tiling, split-K partials summed in a
 // fixed order by a second kernel (no atomics).
 //
-// Tiling: 256-thread workgroups own a 128 x 128 (or, for thin problems, 64 x 64) C tile; 4
-// waves in 2 x 2, each 4 x 4 (2 x 2) blocks of v_mfma_f32_16x16x4_f32 (exact f32 products).
+// Tiling: 256-thread workgroups own a 64 x 64 C tile (128 x 128 in diagnostic builds); 4
+// waves in 2 x 2, each 2 x 2 (4 x 4) blocks of v_mfma_f32_16x16x4_f32 (exact f32 products).
 // K advances 16 at a time through double-buffered LDS tiles stored [k][m] / [k][n] with row
 // stride BT + 16 floats, so the 64 lanes of an MFMA operand read (16 consecutive m or n) x
-// (4 k rows) hit 64 distinct banks; the next tile's global loads (16-B loads when aligned)
-// are in flight while the current tile's MFMAs issue.
+// (4 k rows) hit 64 distinct banks; global loads (16-B when aligned) of the tile after next
+// issue as soon as the next one is staged, so they span a barrier and an MFMA phase.
+// gemm2() runs two independent problems (same or weight-/data-gradient orientations) as one
+// launch over a 1-D grid, with one grouped split-K reduce.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
