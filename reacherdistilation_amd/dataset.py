@@ -51,7 +51,7 @@ class DeviceDataset:
             raise RuntimeError(f"episode already holds {EPISODE_STEPS} steps; flush() first")
         r = self.curr[self.curr_len]
         r[F_OB:F_REW] = torch.as_tensor(ob, dtype=torch.float32).reshape(-1)[:OBSPACE_SHAPE].to(self.device)
-        r[F_REW] = float(reward)
+        r[F_REW] = reward.reshape(()) if torch.is_tensor(reward) else float(reward)   # device reward: no sync
         z = torch.zeros(PDFLAT_SHAPE)
         r[F_T:F_S] = torch.as_tensor(t_pdflat if t_pdflat is not None else z, dtype=torch.float32).reshape(-1).to(
             self.device)

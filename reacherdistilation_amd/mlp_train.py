@@ -38,11 +38,22 @@ from .student_mlp import StudentMlpConfig, StudentMlpTrainer, rows
 def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPISODE_BUDGET,
           loss: str = "kl", lr: float = 1e-4, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
           warmup_episodes: int = 2 * MLP_BATCH_SIZE, student: str = "policy", keep_prob: float = 1.0,
-          log=print):
+          log=print, gym_env: bool = False):
     """Returns (trainer, dataset, per-episode summed training loss); the trainer is the
-    DistillTrainer (student="policy") or the StudentMlpTrainer (student="mlp")."""
+    DistillTrainer (student="policy") or the StudentMlpTrainer (student="mlp").
+
+    By default the loop never waits on the GPU inside an episode: observations, rewards and
+    actions stay device tensors from the env kernel to the dataset and the policy queries,
+    `done` is the TimeLimit count the host already keeps, and the per-window losses are read
+    from the trainer's metrics ring once per episode.  gym_env=True runs the same loop through
+    the gym-API env (numpy round trips every step, as the reference does); both give the
+    same records bit for bit (tests/test_c1_gpu.py)."""
     if student not in ("policy", "mlp"):
         raise ValueError(f"unknown student {student!r}")
+    if not gym_env:
+        return _train_device(train, restore, episodes=episodes, loss=loss, lr=lr, seed=seed, device=device,
+                             teacher_path=teacher_path, warmup_episodes=warmup_episodes, student=student,
+                             keep_prob=keep_prob, log=log)
     env = make_mujoco_env("Reacher-v2", seed, device=device)
     teacher = TeacherAgent(restore=restore, path=teacher_path)
     tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr), device=device, teacher=teacher.pi)
@@ -91,6 +102,71 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
             log("recent loss: %f " % total_loss)
             losses.append(total_loss)
             total_loss = 0.0
+            dataset.flush()
+            if dataset.num_episodes() >= episodes:
+                break
+    return (sm or tr), dataset, losses
+
+
+def _train_device(train, restore, *, episodes, loss, lr, seed, device, teacher_path, warmup_episodes, student,
+                  keep_prob, log):
+    """train() with device-resident env I/O (see train's docstring)."""
+    from .env import BatchedReacher
+    env = BatchedReacher(1, seed=seed, device=device, reset="gym")   # = make_mujoco_env's env
+    teacher = TeacherAgent(restore=restore, path=teacher_path)
+    tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr), device=device, teacher=teacher.pi)
+    sm = StudentMlpTrainer(StudentMlpConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed),
+                           device=device) if student == "mlp" else None
+    dataset = DeviceDataset(device=device, seed=seed)
+    ob = env.reset()                                  # [1, 11], the env's persistent buffer
+    reward = torch.zeros(1, device=env.device)
+    losses = []
+    if not train:
+        return (sm or tr), dataset, losses
+
+    def query(o):
+        t, s = tr.forward(o)
+        if sm is not None:   # the reference student: row = ob | prev_pdflat | prev_rew
+            prev, prew = dataset.current_prev()
+            s = sm.forward(rows(o.view(OBSPACE_SHAPE), prev, prew))
+        return t[0], s[0]
+
+    def env_step(a):
+        """env.step on the device: the kernel auto-resets at the TimeLimit, so after `done`
+        the returned observation is already the reset one (what the reference's env.reset()
+        hands back next)."""
+        o, r, _, _ = env.step(a[:2].reshape(1, 2).contiguous())
+        return o, r, env._step == 0
+
+    log("Begin Training! First Accumulate observation with teacher")
+    while dataset.num_episodes() <= warmup_episodes:
+        t_pdflat, _ = query(ob)
+        dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, stepped_with="t")
+        ob, reward, new = env_step(t_pdflat)
+        if new:
+            dataset.flush()
+    log("Accumulated sufficient data points from teacher. now train")
+
+    opt_steps = 0   # optimiser steps of the open episode (their losses are read at its end)
+    while True:
+        for ob_batch, t_batch, prev_batch, prew_batch in dataset.training_batches():
+            if sm is not None:
+                sm.step(rows(ob_batch, prev_batch, prew_batch), t_batch.reshape(-1, 4))
+            else:
+                tr.step_obs(ob_batch.reshape(-1, OBSPACE_SHAPE))
+            opt_steps += 1
+        t_pdflat, s_pdflat = query(ob)
+        dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, s_pdflat=s_pdflat, stepped_with="s")
+        ob, reward, new = env_step(s_pdflat)
+        if new:
+            log("************** Episode {0} ****************".format(dataset.num_episodes()))
+            m = (sm.metrics(opt_steps)[:, 0] if sm is not None else tr.metrics(opt_steps)[:, 1]) if opt_steps else []
+            total_loss = 0.0
+            for v in m:   # the reference's running float sum, in step order
+                total_loss += float(v)
+            log("recent loss: %f " % total_loss)
+            losses.append(total_loss)
+            opt_steps = 0
             dataset.flush()
             if dataset.num_episodes() >= episodes:
                 break

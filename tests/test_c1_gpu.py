@@ -93,3 +93,21 @@ def test_reference_shaped_lstm_driver_runs():
     assert st.counter() == 50
     m = st.metrics(50)
     assert np.all(m[:, 2] == 200) and np.all(np.isfinite(m[:, 0]))
+
+
+@pytest.mark.parametrize("student", ["policy", "mlp"])
+def test_device_resident_driver_equals_the_gym_api_loop(student):
+    """mlp_train.train's default loop (env I/O kept on the device, `done` from the TimeLimit
+    count, losses read once per episode) writes the same records, trains the same student
+    and logs the same losses as the loop through the gym-API env (numpy every step)."""
+    from reacherdistilation_amd import mlp_train
+    kw = dict(episodes=5, warmup_episodes=2, loss="kl", lr=1e-3, student=student, log=lambda *a: None)
+    a, da, la = mlp_train.train(**kw)
+    b, db, lb = mlp_train.train(gym_env=True, **kw)
+    torch.cuda.synchronize()
+    assert da.num_episodes() == db.num_episodes() == 5
+    assert torch.equal(da.ring, db.ring)
+    assert la == lb and len(la) == 2
+    pa = a.params() if student == "mlp" else a.student_params()
+    pb = b.params() if student == "mlp" else b.student_params()
+    assert torch.equal(pa, pb)
