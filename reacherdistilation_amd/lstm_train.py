@@ -20,13 +20,12 @@ from __future__ import annotations
 
 import os
 
-import numpy as np
 import torch
 
-from .config import LSTM_BATCH_SIZE, OBSPACE_SHAPE, STEPS_UNROLLED, TOTAL_EPISODES
+from .config import LSTM_BATCH_SIZE, STEPS_UNROLLED, TOTAL_EPISODES
 from .dataset import DeviceDataset
 from .distill import DistillConfig, DistillTrainer
-from .env import make_mujoco_env
+from .driver_env import DriverEnv, episode_loss
 from .policy import TeacherAgent
 from .student_lstm import StudentLstmConfig, StudentLstmTrainer
 
@@ -44,11 +43,14 @@ def _restore(st, restore: bool, path: str | None, log):
 
 def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EPISODES, loss: str = "kl",
           lr: float = 1e-3, keep_prob: float = 1.0, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
-          warmup_episodes: int = 2 * LSTM_BATCH_SIZE, student_path: str | None = None, log=print):
+          warmup_episodes: int = 2 * LSTM_BATCH_SIZE, student_path: str | None = None, log=print,
+          gym_env: bool = False):
     """Returns (student trainer, dataset, per-episode summed training loss).  With
     ``student_path`` the student (params + Adam slots) is restored from it when ``restore``
-    (lstm_train.py:102-107) and saved to it after every episode (:199)."""
-    env = make_mujoco_env("Reacher-v2", seed, device=device)
+    (lstm_train.py:102-107) and saved to it after every episode (:199).  Env I/O on the device
+    (driver_env.DriverEnv; gym_env=True through the gym-API env), window losses read once per
+    episode."""
+    env = DriverEnv(seed, device, gym_api=gym_env)
     teacher = TeacherAgent(restore=restore, path=teacher_path)
     tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
     st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
@@ -59,40 +61,39 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
     if not train:
         return st, dataset, losses
     ob = env.reset()
-    reward = 0.0
+    reward = torch.zeros(1, device=env.device)
 
     def teacher_query(o):
-        t, _ = tq.forward(torch.as_tensor(np.asarray(o, np.float32)).view(1, OBSPACE_SHAPE), student=False)
-        return t[0].cpu().numpy()
+        t, _ = tq.forward(o, student=False)
+        return t[0]
 
     log("Begin Training! First Accumulate observation with teacher")
     while dataset.num_episodes() <= warmup_episodes:
         t_pdflat = teacher_query(ob)
         dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, stepped_with="t")
-        ob, reward, new, _ = env.step(t_pdflat[:2])
+        ob, reward, new = env.step(t_pdflat)
         if new:
-            ob = env.reset()
             dataset.flush()
     log("Accumulated sufficient data points from teacher. now train")
 
     state = None   # curr_state_batch: zero at the start (lstm_train.py:88-89)
-    total_loss = 0.0
+    opt_steps = 0
     while True:
         for ob_b, t_b, prev_b, _prew_b in dataset.training_batches():
             st.step(ob_b, prev_b, t_b)          # zero initial state (lstm_train.py:159)
-            total_loss += float(st.metrics(1)[0, 0])
+            opt_steps += 1
         t_pdflat = teacher_query(ob)
         ob_w, prev_w, _ = dataset.test_windows(ob)
         out, state = st.forward(ob_w, prev_w, state)
-        s_pdflat = out[STEPS_UNROLLED - 1, LSTM_BATCH_SIZE - 1].cpu().numpy()
+        s_pdflat = out[STEPS_UNROLLED - 1, LSTM_BATCH_SIZE - 1].clone()
         dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, s_pdflat=s_pdflat, stepped_with="s")
-        ob, reward, new, _ = env.step(s_pdflat[:2])
+        ob, reward, new = env.step(s_pdflat)
         if new:
             log("************** Episode {0} ****************".format(dataset.num_episodes()))
-            ob = env.reset()
+            total_loss = episode_loss(st.metrics(opt_steps)[:, 0] if opt_steps else [])
             log("recent loss: %f " % total_loss)
             losses.append(total_loss)
-            total_loss = 0.0
+            opt_steps = 0
             dataset.flush()
             if student_path:
                 st.save(student_path)   # saver.save every episode (lstm_train.py:199)
@@ -103,7 +104,8 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
 
 def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EPISODES, loss: str = "kl",
                lr: float = 1e-3, keep_prob: float = 1.0, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
-               warmup_episodes: int = 2 * LSTM_BATCH_SIZE, student_path: str | None = None, log=print):
+               warmup_episodes: int = 2 * LSTM_BATCH_SIZE, student_path: str | None = None, log=print,
+               gym_env: bool = False):
     """The truncated-BPTT variant of the driver (reference backup/lstm_bbpt.py:18-208), same
     graph, loss and Adam.  After the teacher warm-up (:115-139) each round is
       * one BPTT pass (:141-158): ``dataset.bptt_batches()`` -- LSTM_BATCH_SIZE episodes, the
@@ -112,8 +114,9 @@ def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOT
         initial_state_batch; zero at the start of the pass);
       * then one whole episode stepped by the student (:160-205): teacher relabel, the test
         window's query with the carried query state, record with 's', env.step(student mean).
-    Returns (student trainer, dataset, per-episode summed training loss)."""
-    env = make_mujoco_env("Reacher-v2", seed, device=device)
+    Returns (student trainer, dataset, per-episode summed training loss).  Env I/O as in
+    train()."""
+    env = DriverEnv(seed, device, gym_api=gym_env)
     teacher = TeacherAgent(restore=restore, path=teacher_path)
     tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
     st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
@@ -124,40 +127,39 @@ def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOT
     if not train:
         return st, dataset, losses
     ob = env.reset()
-    reward = 0.0
+    reward = torch.zeros(1, device=env.device)
 
     def teacher_query(o):
-        t, _ = tq.forward(torch.as_tensor(np.asarray(o, np.float32)).view(1, OBSPACE_SHAPE), student=False)
-        return t[0].cpu().numpy()
+        t, _ = tq.forward(o, student=False)
+        return t[0]
 
     log("Begin Training! First Accumulate observation with teacher")
     while dataset.num_episodes() <= warmup_episodes:
         t_pdflat = teacher_query(ob)
         dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, stepped_with="t")
-        ob, reward, new, _ = env.step(t_pdflat[:2])
+        ob, reward, new = env.step(t_pdflat)
         if new:
-            ob = env.reset()
             dataset.flush()
     log("Accumulated sufficient data points from teacher. now train")
 
     query_state = None   # curr_state_batch (lstm_bbpt.py:94)
     while True:
-        total_loss = 0.0
         s = None         # zero_state_batch at the start of each pass (:142)
+        opt_steps = 0
         for ob_b, t_b, prev_b, _prew_b in dataset.bptt_batches():
             st.step(ob_b, prev_b, t_b, state0=s)
             s = st.final_state(LSTM_BATCH_SIZE)
-            total_loss += float(st.metrics(1)[0, 0])
+            opt_steps += 1
+        total_loss = episode_loss(st.metrics(opt_steps)[:, 0] if opt_steps else [])
         new = False
         while not new:
             t_pdflat = teacher_query(ob)
             ob_w, prev_w, _ = dataset.test_windows(ob)
             out, query_state = st.forward(ob_w, prev_w, query_state)
-            s_pdflat = out[STEPS_UNROLLED - 1, LSTM_BATCH_SIZE - 1].cpu().numpy()
+            s_pdflat = out[STEPS_UNROLLED - 1, LSTM_BATCH_SIZE - 1].clone()
             dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, s_pdflat=s_pdflat, stepped_with="s")
-            ob, reward, new, _ = env.step(s_pdflat[:2])
+            ob, reward, new = env.step(s_pdflat)
         log("************** Episode {0} ****************".format(dataset.num_episodes()))
-        ob = env.reset()
         log("recent loss: %f " % total_loss)
         losses.append(total_loss)
         dataset.flush()

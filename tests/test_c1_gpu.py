@@ -111,3 +111,18 @@ def test_device_resident_driver_equals_the_gym_api_loop(student):
     pa = a.params() if student == "mlp" else a.student_params()
     pb = b.params() if student == "mlp" else b.student_params()
     assert torch.equal(pa, pb)
+
+
+@pytest.mark.parametrize("fn", ["train", "train_bptt"])
+def test_device_resident_lstm_drivers_equal_the_gym_api_loop(fn):
+    """lstm_train.train / train_bptt with the env I/O on the device write the same records,
+    train the same student and log the same losses as through the gym-API env."""
+    from reacherdistilation_amd import lstm_train
+    kw = dict(episodes=4, warmup_episodes=2, keep_prob=0.5, log=lambda *a: None)
+    a, da, la = getattr(lstm_train, fn)(**kw)
+    b, db, lb = getattr(lstm_train, fn)(gym_env=True, **kw)
+    torch.cuda.synchronize()
+    assert da.num_episodes() == db.num_episodes() == 4
+    assert torch.equal(da.ring, db.ring)
+    assert la == lb and len(la) >= 1
+    assert torch.equal(a.params(), b.params())
