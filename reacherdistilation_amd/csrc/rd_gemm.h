@@ -516,7 +516,11 @@ inline void gemm_plan(GemmArgs& g, int tile, int per_cu, float* part, int64_t pa
     const int target = per_cu * cus;
     if (part && tiles < target && g.K >= 512) {
         splits = (target + tiles - 1) / tiles;
-        const int maxs = g.K / 256 < 256 ? g.K / 256 : 256;   // >= 16 k-tiles per split, <= 256 partials
+        // >= 16 k-tiles per split, <= 256 partials; a grid of a few tiles (small M and N: the
+        // LSTM's dh GEMM at the reference's 20 windows) goes down to 4 k-tiles per split, since
+        // each split's K loop is a chain of load latencies
+        const int kmin = tiles <= 16 ? 64 : 256;
+        const int maxs = g.K / kmin < 256 ? g.K / kmin : 256;
         if (splits > maxs) splits = maxs;
         while (splits > 1 && (int64_t)splits * g.M * g.N > part_floats) --splits;
     }
