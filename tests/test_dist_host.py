@@ -120,3 +120,29 @@ def test_replica_checksum_detects_one_ulp():
     for r in range(world):
         assert out[r][0] is True and out[r][1] is False
     assert out[0][2] == out[1][2]
+
+
+def test_native_comm_host_contract():
+    """include/reacher_comm.h without a GPU: the RCCL unique id comes back (128 bytes, not
+    all zero); argument errors and a communicator on a missing device fail with a message
+    (rc != 0, rd_last_error set) instead of crashing -- the error path on which bench.py
+    falls back to torch's collective."""
+    import ctypes
+
+    from reacherdistilation_amd import _native as nat
+    lib = nat.load()
+    idb = (ctypes.c_uint8 * 128)()
+    rc = lib.rd_comm_unique_id(idb)
+    if rc != 0:   # no RCCL on this host: the failure is reported, not raised from C
+        assert lib.rd_last_error()
+        return
+    assert any(bytes(idb))
+    h = ctypes.c_void_p()
+    assert lib.rd_comm_create(ctypes.byref(h), idb, 0, 0, 0) != 0          # nranks 0
+    assert b"bad argument" in lib.rd_last_error()
+    assert lib.rd_comm_create(ctypes.byref(h), idb, 2, 2, 0) != 0          # rank out of range
+    assert lib.rd_comm_allreduce_f32(None, None, 4, None) != 0
+    assert lib.rd_comm_nranks(None) == 0 and lib.rd_comm_destroy(None) == 0
+    if not torch.cuda.is_available():
+        assert lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0) != 0      # no HIP device here
+        assert lib.rd_last_error()
