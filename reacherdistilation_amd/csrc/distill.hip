@@ -1032,8 +1032,12 @@ struct ReduceArgs {
     int bf16;
 };
 
-constexpr int RED_COLS = 64;                        // params per reduce block
-constexpr int RED_ROWS = 16;                        // partial rows summed in parallel
+#ifndef RDD_RED_COLS   // diagnostic builds may change the reduce blocking (A/B)
+#define RDD_RED_COLS 64
+#define RDD_RED_ROWS 16
+#endif
+constexpr int RED_COLS = RDD_RED_COLS;              // params per reduce block
+constexpr int RED_ROWS = RDD_RED_ROWS;              // partial rows summed in parallel
 constexpr int RED_BLOCK = RED_COLS * RED_ROWS;
 constexpr int RED_GRID = (P_PAD + RED_COLS - 1) / RED_COLS;
 
