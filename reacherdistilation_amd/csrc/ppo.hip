@@ -336,22 +336,27 @@ __global__ __launch_bounds__(64) void logp_old_kernel(const float* params, const
     lpo[r] = -0.5f * (d0 * d0 + d1 * d1) - (ls0 + ls1) - LOG2PI;
 }
 
-// minibatch rows perm[i] -> Z (filtered obs, 12-wide), A, LPO, ATG, RET
+// minibatch rows perm[i] -> Z (filtered obs, 12-wide), A, LPO, ATG, RET.  16 lanes per row,
+// one gathered value each (one lane per row left the random-row loads of a 4,096-row
+// minibatch on 16 workgroups: a chain of load latencies)
+constexpr int GATHER_LANES = 16;
 __global__ __launch_bounds__(256) void gather_kernel(const int* perm, int mb, const float* rms, const float* ob,
                                                      const float* ac, const float* lpo, const float* atarg,
                                                      const float* ret, float* Z, float* A, float* LPO, float* ATG,
                                                      float* RET) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int i = (int)(t / GATHER_LANES), j = (int)(t % GATHER_LANES);
     if (i >= mb) return;
     const int64_t r = perm[i];
-#pragma unroll
-    for (int k = 0; k < OBD; ++k) Z[i * ZLD + k] = clip5((ob[r * OBD + k] - rms[k]) / rms[OBD + k]);
-    Z[i * ZLD + OBD] = 1.0f;   // the bias input of the layer-1 gradient GEMM
-    A[2 * i] = ac[2 * r];
-    A[2 * i + 1] = ac[2 * r + 1];
-    LPO[i] = lpo[r];
-    ATG[i] = atarg[r];
-    RET[i] = ret[r];
+    if (j < OBD) Z[i * ZLD + j] = clip5((ob[r * OBD + j] - rms[j]) / rms[OBD + j]);
+    else if (j == OBD) Z[i * ZLD + OBD] = 1.0f;   // the bias input of the layer-1 gradient GEMM
+    else if (j == 12) A[2 * i] = ac[2 * r];
+    else if (j == 13) A[2 * i + 1] = ac[2 * r + 1];
+    else if (j == 14) LPO[i] = lpo[r];
+    else {
+        ATG[i] = atarg[r];
+        RET[i] = ret[r];
+    }
 }
 
 // clipped surrogate + value loss per row: dMEAN, dV, and per-block sums of
@@ -606,7 +611,8 @@ int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
     const float* Pv = P + VB;
     float* gv = g + VB;
     const float eps = t->cfg.clip_param * t->lrmult;
-    hipLaunchKernelGGL(gather_kernel, dim3((mb + 255) / 256), dim3(256), 0, t->stream, perm, mb,
+    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(((int64_t)mb * GATHER_LANES + 255) / 256)), dim3(256), 0,
+                       t->stream, perm, mb,
                        (const float*)t->rms, (const float*)t->ob, (const float*)t->ac, (const float*)t->lpo,
                        (const float*)t->atarg, (const float*)t->ret, t->Z, t->A, t->LPO, t->ATG, t->RET);
     RDP_CK(hipGetLastError(), "rdp gather");
