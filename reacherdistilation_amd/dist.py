@@ -71,14 +71,20 @@ class RcclComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         idb = (ctypes.c_uint8 * 128)()
-        if self.rank == 0:
-            nat.check(self._lib.rd_comm_unique_id(idb), "rd_comm_unique_id")
-        t = torch.tensor(list(bytes(idb)), dtype=torch.uint8)
+        ok, why = 1, ""
+        if self.rank == 0:   # rank 0 always takes part in the broadcast, success or not, so a
+            rc = self._lib.rd_comm_unique_id(idb)   # failure reaches every rank (no one-sided hang)
+            if rc != 0:
+                ok, why = 0, self._lib.rd_last_error().decode(errors="replace")
+        t = torch.tensor(list(bytes(idb)) + [ok], dtype=torch.uint8)
         if dist.get_backend(group) == "nccl":
             t = t.to(self.device)
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast(t, src=src, group=group)
-        idb = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+        t = t.cpu()
+        if int(t[-1]) != 1:
+            raise nat.NativeError(f"rd_comm_unique_id failed on rank 0{': ' + why if why else ''}")
+        idb = (ctypes.c_uint8 * 128)(*t[:128].tolist())
         h = ctypes.c_void_p()
         nat.check(self._lib.rd_comm_create(ctypes.byref(h), idb, self.world, self.rank, self.device.index or 0),
                   "rd_comm_create")

@@ -146,3 +146,31 @@ def test_native_comm_host_contract():
     if not torch.cuda.is_available():
         assert lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0) != 0      # no HIP device here
         assert lib.rd_last_error()
+
+
+def _comm_rank(rank, world, port, out):
+    import torch.distributed as dist
+
+    from reacherdistilation_amd.dist import RcclComm
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        RcclComm(torch.device("cpu"))
+        out[rank] = "created"
+    except Exception as e:  # noqa: BLE001
+        out[rank] = type(e).__name__
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="the no-device failure path is exercised on CPU hosts")
+def test_native_comm_failure_reaches_every_rank():
+    """Two gloo ranks build dist.RcclComm on a host without a HIP device: the id broadcast
+    completes, every rank's rd_comm_create fails, and each raises NativeError -- no rank is
+    left waiting in a collective (the bench then uses torch's collective)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = mp.get_context("spawn").Manager().dict()
+    mp.start_processes(_comm_rank, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    assert out[0] == out[1] == "NativeError"
