@@ -67,6 +67,8 @@ def parse():
                     help="also time K env-steps per optimiser step (SURVEY §8d: K = 50 = one episode); 0 = skip")
     ap.add_argument("--conv-steps", type=int, default=5000,
                     help="convergence leg: optimiser steps allowed to reach student action-MSE < 1e-3; 0 = skip")
+    ap.add_argument("--conv-small-envs", type=int, default=256,
+                    help="env count of the second convergence run (the env-step reading of the budget)")
     return ap.parse_args()
 
 
@@ -175,13 +177,13 @@ def copy_bandwidth(dev, gib=1.0, iters=40):
     return 2 * 4 * n * iters / (s.elapsed_time(e) * 1e-3) / 1e9
 
 
-def cpu_baseline(workload, seconds, threads):
-    """Time the oracle's C f32 rollout+distill step (OpenMP) on a bounded sample."""
+def cpu_baseline(workload, seconds, threads, n):
+    """Time the oracle's C f32 rollout+distill step (OpenMP) at the workload's own env count
+    (the same per-GPU batch as the timed GPU step), for a bounded number of steps."""
     import numpy as np
 
     from oracle import ref_c
     from reacherdistilation_amd.policy import student_init, synthetic_teacher
-    n = 4096
     t, s = synthetic_teacher(1), student_init(2)
     state = ref_c.philox_reset(n, 0, 0, 0)
     threads = threads or min(16, os.cpu_count() or 1)
@@ -199,10 +201,11 @@ def cpu_baseline(workload, seconds, threads):
         b1p *= 0.9; b2p *= 0.999
         steps += 1
         el = time.perf_counter() - t0
-        if el >= seconds:
+        if el >= seconds and steps >= 2:
             break
-    return dict(value=n * steps / el, unit="env-steps/s", cores=threads, kind="port",
-                sample=f"{n} envs x {steps} steps ({el:.1f} s), same step (env + teacher + student fwd/bwd "
+    return dict(value=n * steps / el, unit="env-steps/s", cores=threads, kind="port", envs=n,
+                sample=f"{n} envs (the workload's per-GPU batch) x {steps} steps ({el:.1f} s), same step "
+                       f"(env + teacher + student fwd/bwd "
                        f"+ {workload['loss']} + TF1 Adam), C f32 restatement oracle/reacher_ref.c, "
                        f"OpenMP {threads} threads")
 
@@ -234,10 +237,14 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
             break
     el = time.perf_counter() - t0
     tr.close()
-    return {"target_mse": target, "lr": lr, "loss": wl["loss"], "steps_checked_every": chunk,
-            "opt_steps_to_target": hit, "env_steps_to_target": None if hit is None else hit * n * world,
-            "reference_budget_opt_steps": 5000 * 50, "student_mse_final": mse, "opt_steps_run": steps,
-            "seconds": el}
+    env_steps = None if hit is None else hit * n * world
+    budget = 5000 * 50   # mlp_train.py:143-204: 5000 episodes x 50 steps, one Adam step per env step
+    return {"target_mse": target, "lr": lr, "loss": wl["loss"], "envs_total": n * world,
+            "steps_checked_every": chunk, "opt_steps_to_target": hit, "env_steps_to_target": env_steps,
+            "reference_budget_opt_steps": budget, "reference_budget_env_steps": budget,
+            "within_opt_step_budget": hit is not None and hit <= budget,
+            "within_env_step_budget": env_steps is not None and env_steps <= budget,
+            "student_mse_final": mse, "opt_steps_run": steps, "seconds": el}
 
 
 def main():
@@ -288,6 +295,17 @@ def main():
     wl = WORKLOADS[args.workload]
     n = args.envs_per_gpu or wl["envs"]
     sdt = wl.get("student_dtype", "f32")
+
+    # The convergence leg runs first, on trainers of its own: it is the north star's student
+    # action-MSE check, and its ~1,000 back-to-back steps also take the GPU out of its idle
+    # clocks, so the short timed region below (the driver runs 20 steps of ~0.12 ms) measures
+    # the kernels rather than the clock ramp.
+    conv = conv_small = None
+    if args.conv_steps > 0:
+        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm)
+        # the same check at a small per-GPU batch: the env-step reading of the reference's budget
+        conv_small = convergence(wl, args.conv_small_envs, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm)
+
     cfg = DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr, student_dtype=sdt)
     tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world, comm=comm)
 
@@ -302,36 +320,40 @@ def main():
             ev[1].record()
         if world == 1:
             tr.launch(tr.STAGE_REDUCE_APPLY)
-        else:
+        else:   # the bound communicator's or torch's all-reduce, between reduce and Adam
             tr.launch(tr.STAGE_REDUCE)
             tr.allreduce_grad()
             tr.launch(tr.STAGE_APPLY)
 
     for _ in range(args.warmup):
         one_step()
-    # rollout_kernel's launch time for the roofline: HIP events around every `every`-th launch
-    # of the timed region (a timing event costs the stream a few us, so bracketing every step
-    # would slow the very loop being timed: 122 vs 113 us per c4 step)
-    every = max(1, args.steps // 20)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range((args.steps + every - 1) // every)]
+    # the timed region: exactly `steps` steps, nothing else on the stream (no timing events)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        one_step(evs[k // every] if k % every == 0 else None)
+    for _ in range(args.steps):
+        one_step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+
+    # rollout_kernel's launch time for the roofline: a separate pass right after the timed
+    # region, HIP events on the trainer's stream around every rollout launch (an event pair
+    # costs the stream a few us per step, so it is kept out of the timed region)
+    npass = max(20, min(args.steps, 200))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(npass)]
+    for k in range(npass):
+        one_step(evs[k])
+    torch.cuda.synchronize(dev)
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
 
     replicas = tr.replicas_identical() if world > 1 else True   # SURVEY §8e checksum
 
@@ -362,10 +384,6 @@ def main():
                  "replicas_identical": tk.replicas_identical() if world > 1 else True}
         tk.close()
 
-    conv = None
-    if args.conv_steps > 0:
-        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm)
-
     # student action-MSE vs teacher over the last steps (all ranks)
     met = tr.metrics(min(10, tr.counter()))
     mt = torch.tensor(met.sum(0), dtype=torch.float64, device=dev)
@@ -383,11 +401,18 @@ def main():
             f_s = FLOP_PER_ENV_STEP - FLOP_TEACHER
             peak = FLOP_PER_ENV_STEP / (FLOP_TEACHER / PEAK_F32_TFLOPS + f_s / PEAK_BF16_TFLOPS)
         copy_gbs = copy_bandwidth(dev)
-        traffic = None
+        # HBM bytes per rollout launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
+        # MI355X_MICROARCH.md §HBM); counters cannot be read from inside this process, so the
+        # committed profile of this workload is used and named in traffic_source
+        traffic, traffic_src = None, None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}.json")
         if os.path.exists(pmc):
             with open(pmc) as fh:
-                traffic = json.load(fh).get("hbm_bytes_per_launch")
+                pj = json.load(fh)
+            traffic = pj.get("hbm_bytes_per_launch")
+            traffic_src = {"file": os.path.relpath(pmc, ROOT), "measured": pj.get("measured", "round 1 (r01i/r01q)"),
+                           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes "
+                                     "(scripts/profile_workload.sh, scripts/pmc_traffic.py)"}
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
@@ -405,8 +430,10 @@ def main():
             "student_mse_timed_run": mse,
             "roofline": {"kernel": "rollout_kernel", "bound": "mfma", "achieved": achieved,
                          "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": traffic, "flop_per_env_step": FLOP_PER_ENV_STEP,
-                         "launch_us": kern_ms * 1e3,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "flop_per_env_step": FLOP_PER_ENV_STEP, "launch_us": kern_ms * 1e3,
+                         "launch_timing": f"HIP events around each of {npass} rollout launches, a pass after "
+                                          "the timed region",
                          "hbm_gbs_algorithmic": BYTES_PER_ENV_STEP * n / launch_s / 1e9,
                          "hbm_peak_gbs": PEAK_HBM_GBS, "hbm_copy_gbs_measured": copy_gbs},
             "replicas_identical": replicas,
@@ -415,10 +442,11 @@ def main():
             out["accum"] = accum
         if conv is not None:
             out["convergence"] = conv
+            out["convergence_small_batch"] = conv_small
         out["roofline_env"] = env_roofline(dev)
         out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / copy_gbs
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads, n)
             out["cpu_baseline"]["ref_loop"] = cpu_ref_loop(min(4.0, args.cpu_seconds))
             out["cpu_baseline"]["batched_env"] = cpu_batched_env(min(4.0, args.cpu_seconds))
         # at N > 1 a communication library may have written to stdout without a newline

@@ -16,9 +16,14 @@
  *
  * RCCL is resolved at run time (dlopen of librccl.so.1, reusing the copy torch loaded), so
  * the library loads on hosts without RCCL; rd_comm_* then fail with RD_EINVAL and a message.
- * Usage (one process per GPU): rank 0 calls rd_comm_unique_id() and broadcasts the 128
- * bytes (e.g. over the torch.distributed group); every rank calls rd_comm_create() with
- * them; bind with rdd_bind_comm() (reacher_distill.h).  Conventions as in reacher.h.
+ * Usage (one process per GPU): every rank calls rd_comm_probe() and the ranks agree on the
+ * result (e.g. an all-reduce over the torch.distributed group), so a rank that cannot take
+ * part stops everyone before any RCCL collective starts; rank 0 calls rd_comm_unique_id()
+ * and broadcasts the 128 bytes; every rank calls rd_comm_create() with them; bind with
+ * rdd_bind_comm() (reacher_distill.h).  The communicator is non-blocking underneath: its
+ * creation (and a first collective's connection setup) is awaited with a deadline, and a
+ * rank whose peers do not arrive within timeout_s aborts the communicator and returns an
+ * error instead of hanging.  Conventions as in reacher.h.
  */
 #ifndef REACHER_COMM_H
 #define REACHER_COMM_H
@@ -35,8 +40,12 @@ typedef struct rd_comm rd_comm;
 /* A fresh RCCL unique id (rank 0 only); id: host buffer of RD_COMM_ID_BYTES. */
 int rd_comm_unique_id(uint8_t* id);
 
-/* Collective over all ranks: an RCCL communicator of nranks ranks on HIP device `device`. */
-int rd_comm_create(rd_comm** out, const uint8_t* id, int nranks, int rank, int device);
+/* 0 iff this rank can join: RCCL resolvable and HIP device `device` selectable. */
+int rd_comm_probe(int device);
+
+/* Collective over all ranks: an RCCL communicator of nranks ranks on HIP device `device`;
+ * fails (communicator aborted) if the other ranks have not joined within timeout_s. */
+int rd_comm_create(rd_comm** out, const uint8_t* id, int nranks, int rank, int device, double timeout_s);
 
 /* In-place SUM all-reduce of n floats of device memory, asynchronous on hip_stream. */
 int rd_comm_allreduce_f32(rd_comm* c, float* buf, int64_t n, void* hip_stream);

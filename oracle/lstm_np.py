@@ -85,6 +85,20 @@ def sig(x):
     return 1.0 / (1.0 + np.exp(-x))
 
 
+FORGET_BIAS = 1.0   # TF1 LSTMCell default (LSTM/unique_lstm_cell/add/y in the reference graph)
+
+
+def cell(x, c, h, Wl, bl):
+    """One TF1 LSTMCell step: z = [x, h] Wl + bl split (i, j, f, o);
+    c' = sig(f + forget_bias) c + sig(i) tanh(j); h' = sig(o) tanh(c').  Returns
+    (c', h', (sig i, tanh j, sig(f + 1), sig o))."""
+    z = np.concatenate([x, h], 1) @ Wl + bl
+    i, j, f, o = np.split(z, 4, axis=1)
+    gi, gj, gf, go = sig(i), np.tanh(j), sig(f + FORGET_BIAS), sig(o)
+    c = gf * c + gi * gj
+    return c, go * np.tanh(c), (gi, gj, gf, go)
+
+
 def forward(p, ob, prev, state0=None):
     """ob [T,B,11] (already dropped), prev [T,B,4] -> dict with pdflat [T,B,4] and caches."""
     W = unpack(p)
@@ -98,12 +112,8 @@ def forward(p, ob, prev, state0=None):
     for t in range(T):
         pt = prev[t] @ W["Wp"] + W["bp"]
         x = np.concatenate([ob[t], pt], 1)
-        z = np.concatenate([x, h], 1) @ W["Wl"] + W["bl"]
-        i, j, f, o = np.split(z, 4, axis=1)
-        gi, gj, gf, go = sig(i), np.tanh(j), sig(f + 1.0), sig(o)
         cache["x"].append(x); cache["hprev"].append(h); cache["cprev"].append(c)
-        c = gf * c + gi * gj
-        h = go * np.tanh(c)
+        c, h, (gi, gj, gf, go) = cell(x, c, h, W["Wl"], W["bl"])
         for k, v in (("gi", gi), ("gj", gj), ("gf", gf), ("go", go), ("c", c), ("h", h)):
             cache[k].append(v)
         a = [h]

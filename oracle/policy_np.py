@@ -14,9 +14,13 @@
                  var -= m * lr*sqrt(1 - b2^t)/(1 - b1^t) / (sqrt(v) + eps), with
                  beta1_power/beta2_power float32 variables multiplied once per step.
 
-Parity status: UNPINNED beyond the formulas -- TensorFlow/baselines are not installed and
-the reference has no test for this math.  Gradients are checked against
-finite differences in tests/test_policy_oracle.py.
+Parity status: PINNED to the reference's own GraphDefs (src/~/reacher/data/viz/1 event
+files, parsed and evaluated by oracle/tfgraph.py; goldens tests/golden/graph_golden.npz):
+the MlpPolicy forward incl. the observation filter (pi/pol/concat on the teacher's own
+initial weights and on seeded weights), the kl loss and TF's gradient of it, the Adam
+constants and beta-power schedule (tests/test_graph_pins.py).  The backward is pinned
+through the forward: it is checked against finite differences of the pinned forward
+(tests/test_policy_oracle.py).  TensorFlow/baselines themselves are not installed.
 """
 from __future__ import annotations
 
@@ -34,6 +38,20 @@ P_LS = P_B3 + ACD
 P_TOT = P_LS + ACD  # 5060
 
 
+# baselines RunningMeanStd as the reference's GraphDef computes it (pi/obfilter: count and
+# runningsumsq start at 1e-2, runningsum at 0, sums in f64; the floor is on the VARIANCE,
+# Maximum/y = 1e-2); pinned by tests/test_graph_pins.py against the graph itself
+OBF_COUNT0, OBF_SUMSQ0, OB_CLIP = 1e-2, 1e-2, 5.0
+OBF_VAR_FLOOR = float(np.float32(1e-2))   # a float32 Const in the graph
+
+
+def obfilter(runningsum, runningsumsq, count):
+    """(mean, std) of the observation filter from its running sums (pi/obfilter/*)."""
+    mean = np.asarray(runningsum, np.float64) / count
+    var = np.asarray(runningsumsq, np.float64) / count - mean ** 2
+    return mean, np.sqrt(np.maximum(var, OBF_VAR_FLOOR))
+
+
 def unpack(p):
     return dict(W1=p[P_W1:P_B1].reshape(OBD, HID), b1=p[P_B1:P_W2], W2=p[P_W2:P_B2].reshape(HID, HID),
                 b2=p[P_B2:P_W3], W3=p[P_W3:P_B3].reshape(HID, ACD), b3=p[P_B3:P_LS], ls=p[P_LS:P_TOT])
@@ -46,7 +64,7 @@ def pack(W1, b1, W2, b2, W3, b3, ls):
 def forward(p, obmu, obsd, ob):
     """ob [N,11] -> dict(z, h1, h2, mean [N,2], logstd [2])."""
     q = unpack(p)
-    z = np.clip((ob - obmu) / obsd, -5.0, 5.0)
+    z = np.clip((ob - obmu) / obsd, -OB_CLIP, OB_CLIP)
     h1 = np.tanh(z @ q["W1"] + q["b1"])
     h2 = np.tanh(h1 @ q["W2"] + q["b2"])
     mean = h2 @ q["W3"] + q["b3"]

@@ -70,6 +70,13 @@ def philox4x32_10(c, k0, k1):
     return np.stack(c).astype(np.uint32)
 
 
+def apply_mask(x, u, kp):
+    """tf.nn.dropout's scale with our keep rule: x / kp where u < kp, else 0.  TF keeps
+    where floor(kp + U) = 1, i.e. U >= 1 - kp: the same rule with u = 1 - U (pinned
+    against the reference graph's LSTM/dropout ops by tests/test_graph_pins.py)."""
+    return np.where(u < kp, x / kp, np.float32(0.0)).astype(np.float32)
+
+
 def dropout(x, keep_prob, seed, step, row_base=0):
     """Training-time input dropout of rows x [n,16] (f32), columns 0..10 only."""
     x = np.array(x, np.float32)
@@ -85,7 +92,7 @@ def dropout(x, keep_prob, seed, step, row_base=0):
         for k in range(4):
             col = 4 * q + k
             if col < 11:
-                x[:, col] = np.where(u[k] < kp, x[:, col] / kp, np.float32(0.0))
+                x[:, col] = apply_mask(x[:, col], u[k], kp)
     return x
 
 

@@ -42,7 +42,8 @@ SIGNATURES = {
     "rd_last_error": (ctypes.c_char_p, []),
     # reacher_comm.h
     "rd_comm_unique_id": (INT, [P]),
-    "rd_comm_create": (INT, [ctypes.POINTER(P), P, INT, INT, INT]),
+    "rd_comm_probe": (INT, [INT]),
+    "rd_comm_create": (INT, [ctypes.POINTER(P), P, INT, INT, INT, ctypes.c_double]),
     "rd_comm_allreduce_f32": (INT, [P, P, I64, P]),
     "rd_comm_nranks": (INT, [P]),
     "rd_comm_destroy": (INT, [P]),

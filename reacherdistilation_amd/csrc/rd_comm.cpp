@@ -10,8 +10,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
 #include <new>
+#include <thread>
 
 #include "../../include/reacher.h"
 #include "../../include/reacher_comm.h"
@@ -21,7 +23,9 @@ namespace {
 
 struct Rccl {
     decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommInitRankConfig) init_rank_config = nullptr;
+    decltype(&ncclCommGetAsyncError) async_error = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
@@ -40,11 +44,14 @@ const Rccl& rccl() {
             return;
         }
         r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
-        r.init_rank = (decltype(r.init_rank))dlsym(h, "ncclCommInitRank");
+        r.init_rank_config = (decltype(r.init_rank_config))dlsym(h, "ncclCommInitRankConfig");
+        r.async_error = (decltype(r.async_error))dlsym(h, "ncclCommGetAsyncError");
+        r.abort = (decltype(r.abort))dlsym(h, "ncclCommAbort");
         r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
         r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
         r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-        r.ok = r.get_unique_id && r.init_rank && r.all_reduce && r.destroy && r.error_string;
+        r.ok = r.get_unique_id && r.init_rank_config && r.async_error && r.abort && r.all_reduce && r.destroy &&
+               r.error_string;
         if (!r.ok) snprintf(r.why, sizeof r.why, "librccl.so.1 lacks an nccl* entry point");
     });
     return r;
@@ -59,7 +66,31 @@ int nccl_fail(ncclResult_t e, const char* what) {
 struct rd_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
+    double timeout_s = 60.0;
 };
+
+namespace {
+
+// The communicator is non-blocking (ncclConfig_t.blocking = 0): its creation, and a
+// collective that still has connections to set up, return ncclInProgress and complete in
+// the background.  Wait for that with a deadline; past it the communicator is aborted, so a
+// rank whose peers never arrive fails with a message instead of hanging in RCCL.
+int wait_ready(rd_comm* c, const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclInProgress;
+        if (ncclResult_t e = rccl().async_error(c->comm, &st); e != ncclSuccess) return nccl_fail(e, what);
+        if (st == ncclSuccess) return RD_OK;
+        if (st != ncclInProgress) return nccl_fail(st, what);
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (dt > c->timeout_s)
+            return rd::set_error(RD_EINVAL, "%s: rank %d of %d: the other ranks did not join within %.0f s", what,
+                                 c->rank, c->nranks, c->timeout_s);
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -74,8 +105,19 @@ int rd_comm_unique_id(uint8_t* id) {
     return RD_OK;
 }
 
-int rd_comm_create(rd_comm** out, const uint8_t* id, int nranks, int rank, int device) {
-    if (!out || !id || nranks <= 0 || rank < 0 || rank >= nranks)
+int rd_comm_probe(int device) {
+    const Rccl& r = rccl();
+    if (!r.ok) return rd::set_error(RD_EINVAL, "rd_comm_probe: %s", r.why);
+    int n = 0;
+    RD_HIP(hipGetDeviceCount(&n), "rd_comm_probe: hipGetDeviceCount");
+    if (device < 0 || device >= n) return rd::set_error(RD_EINVAL, "rd_comm_probe: no HIP device %d (%d visible)", device, n);
+    rd::DeviceGuard g(device);
+    RD_HIP(g.err, "rd_comm_probe: hipSetDevice");
+    return RD_OK;
+}
+
+int rd_comm_create(rd_comm** out, const uint8_t* id, int nranks, int rank, int device, double timeout_s) {
+    if (!out || !id || nranks <= 0 || rank < 0 || rank >= nranks || !(timeout_s > 0))
         return rd::set_error(RD_EINVAL, "rd_comm_create: bad argument");
     const Rccl& r = rccl();
     if (!r.ok) return rd::set_error(RD_EINVAL, "rd_comm_create: %s", r.why);
@@ -85,13 +127,20 @@ int rd_comm_create(rd_comm** out, const uint8_t* id, int nranks, int rank, int d
     memcpy(&u, id, sizeof(u));
     rd_comm* c = new (std::nothrow) rd_comm();
     if (!c) return rd::set_error(RD_EINVAL, "rd_comm_create: out of host memory");
-    if (ncclResult_t e = r.init_rank(&c->comm, nranks, u, rank); e != ncclSuccess) {
-        delete c;
-        return nccl_fail(e, "ncclCommInitRank");
-    }
     c->nranks = nranks;
     c->rank = rank;
     c->device = device;
+    c->timeout_s = timeout_s;
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t e = r.init_rank_config(&c->comm, nranks, u, rank, &cfg);
+    int rc = (e == ncclSuccess || e == ncclInProgress) ? wait_ready(c, "ncclCommInitRankConfig")
+                                                       : nccl_fail(e, "ncclCommInitRankConfig");
+    if (rc != RD_OK) {
+        if (c->comm) (void)r.abort(c->comm);
+        delete c;
+        return rc;
+    }
     *out = c;
     return RD_OK;
 }
@@ -100,9 +149,9 @@ int rd_comm_allreduce_f32(rd_comm* c, float* buf, int64_t n, void* hip_stream) {
     if (!c || !buf || n <= 0) return rd::set_error(RD_EINVAL, "rd_comm_allreduce_f32: bad argument");
     rd::DeviceGuard g(c->device);
     RD_HIP(g.err, "rd_comm_allreduce_f32: hipSetDevice");
-    if (ncclResult_t e = rccl().all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, (hipStream_t)hip_stream);
-        e != ncclSuccess)
-        return nccl_fail(e, "ncclAllReduce");
+    ncclResult_t e = rccl().all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, (hipStream_t)hip_stream);
+    if (e == ncclInProgress) return wait_ready(c, "ncclAllReduce");   // first use: connection setup
+    if (e != ncclSuccess) return nccl_fail(e, "ncclAllReduce");
     return RD_OK;
 }
 
@@ -111,7 +160,10 @@ int rd_comm_nranks(const rd_comm* c) { return c ? c->nranks : 0; }
 int rd_comm_destroy(rd_comm* c) {
     if (!c) return RD_OK;
     rd::DeviceGuard g(c->device);
-    if (c->comm) (void)rccl().destroy(c->comm);
+    if (c->comm) {
+        if (wait_ready(c, "rd_comm_destroy") == RD_OK) (void)rccl().destroy(c->comm);
+        else (void)rccl().abort(c->comm);
+    }
     delete c;
     return RD_OK;
 }

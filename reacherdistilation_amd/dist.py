@@ -56,10 +56,20 @@ def allreduce_sum_(t, group=None):
 
 class RcclComm:
     """This rank's RCCL communicator (include/reacher_comm.h), created collectively over a
-    torch.distributed group: rank 0 draws the RCCL unique id, the group broadcasts it, every
-    rank joins.  Bind it to a trainer (`DistillTrainer(..., comm=...)`)."""
+    torch.distributed group in three steps, each of which every rank reaches whatever the
+    others did, so a failure anywhere raises on every rank instead of leaving one waiting:
 
-    def __init__(self, device, group=None):
+      1. every rank probes whether it can join (RCCL resolvable, its HIP device selectable)
+         and the group sums a one-hot vector of the answers: if any rank cannot, every rank
+         raises NativeError naming it, before any RCCL call;
+      2. rank 0 draws the RCCL unique id and the group broadcasts it with a success flag (rank
+         0 joins the broadcast even when the draw failed);
+      3. every rank creates the communicator; RCCL's init runs non-blocking with a deadline
+         (`timeout` seconds), so a rank whose peers never arrive aborts and raises.
+
+    Bind it to a trainer (`DistillTrainer(..., comm=...)`)."""
+
+    def __init__(self, device, group=None, timeout: float = 60.0):
         import ctypes
 
         import torch
@@ -67,27 +77,44 @@ class RcclComm:
 
         from . import _native as nat
         self._lib = nat.load()
-        self.device = torch.device(device)
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:   # a bare "cuda" is the current device
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        on_dev = dist.get_backend(group) == "nccl"
+        # 1. can every rank take part?
+        rc = self._lib.rd_comm_probe(device.index if device.type == "cuda" else -1)
+        why = "" if rc == 0 else self._lib.rd_last_error().decode(errors="replace")
+        ok = torch.zeros(self.world, dtype=torch.int32)
+        ok[self.rank] = 1 if rc == 0 else 0
+        if on_dev:
+            ok = ok.to(device)
+        dist.all_reduce(ok, group=group)
+        bad = [r for r, v in enumerate(ok.cpu().tolist()) if v != 1]
+        if bad:
+            raise nat.NativeError(f"RCCL communicator: rank(s) {bad} cannot join"
+                                  f"{' (this rank: ' + why + ')' if why else ''}")
+        # 2. the unique id, from rank 0, with its success flag
         idb = (ctypes.c_uint8 * 128)()
-        ok, why = 1, ""
-        if self.rank == 0:   # rank 0 always takes part in the broadcast, success or not, so a
-            rc = self._lib.rd_comm_unique_id(idb)   # failure reaches every rank (no one-sided hang)
-            if rc != 0:
-                ok, why = 0, self._lib.rd_last_error().decode(errors="replace")
-        t = torch.tensor(list(bytes(idb)) + [ok], dtype=torch.uint8)
-        if dist.get_backend(group) == "nccl":
-            t = t.to(self.device)
+        ok0, why = 1, ""
+        if self.rank == 0:
+            if self._lib.rd_comm_unique_id(idb) != 0:
+                ok0, why = 0, self._lib.rd_last_error().decode(errors="replace")
+        t = torch.tensor(list(bytes(idb)) + [ok0], dtype=torch.uint8)
+        if on_dev:
+            t = t.to(device)
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast(t, src=src, group=group)
         t = t.cpu()
         if int(t[-1]) != 1:
             raise nat.NativeError(f"rd_comm_unique_id failed on rank 0{': ' + why if why else ''}")
         idb = (ctypes.c_uint8 * 128)(*t[:128].tolist())
+        # 3. every rank joins (bounded by `timeout`)
         h = ctypes.c_void_p()
-        nat.check(self._lib.rd_comm_create(ctypes.byref(h), idb, self.world, self.rank, self.device.index or 0),
-                  "rd_comm_create")
+        nat.check(self._lib.rd_comm_create(ctypes.byref(h), idb, self.world, self.rank, device.index,
+                                           float(timeout)), "rd_comm_create")
         self.handle = h
 
     def allreduce_(self, t):

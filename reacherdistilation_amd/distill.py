@@ -94,6 +94,8 @@ class DistillTrainer:
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("DistillTrainer runs on a GPU (HIP) device only; there is no CPU path")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.rank, self.world = rank, world_size
         self.pg = process_group
         self._lib = nat.load()
@@ -131,8 +133,12 @@ class DistillTrainer:
             self.bind_comm(comm)
 
     def bind_comm(self, comm):
-        if comm is not None and comm.world != self.world:
-            raise ValueError(f"communicator of {comm.world} ranks for a trainer of {self.world}")
+        if comm is not None:
+            if comm.world != self.world or comm.rank != self.rank:
+                raise ValueError(f"communicator rank {comm.rank} of {comm.world} for a trainer at rank "
+                                 f"{self.rank} of {self.world}")
+            if comm.device != self.device:   # RCCL would run on the wrong device's context
+                raise ValueError(f"communicator on {comm.device} for a trainer on {self.device}")
         nat.check(self._lib.rdd_bind_comm(self._h, comm.handle if comm is not None else None), "rdd_bind_comm")
         self.comm = comm
 

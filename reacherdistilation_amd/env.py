@@ -145,7 +145,13 @@ class BatchedReacher:
 
 
 class ReacherEnv:
-    """Single Reacher-v2 env with the gym 0.10.5 API (numpy float64 out), on the GPU kernel."""
+    """Single Reacher-v2 env with the gym 0.10.5 API (numpy float64 out), on the GPU kernel.
+
+    step() returns the TERMINAL observation on the step that ends the episode (done=True),
+    as gym's TimeLimit does; the following reset() returns the next episode's first
+    observation.  The kernel auto-resets at that step, so the terminal observation comes from
+    a one-env shadow handle stepped from the same state with the episode clock at 0 (the same
+    kernel and arithmetic, no reset)."""
 
     class _Box:
         def __init__(self, shape, low, high):
@@ -157,6 +163,7 @@ class ReacherEnv:
         self.action_space = self._Box((ACSPACE_SHAPE,), -1.0, 1.0)
         self._needs_reset = True
         self._pending = None
+        self._shadow = None
 
     def seed(self, seed=None):
         dev = self._env.device
@@ -181,17 +188,26 @@ class ReacherEnv:
         act = torch.from_numpy(a32).view(1, ACSPACE_SHAPE).to(self._env.device)
         if self._env._episode < 0:
             self._env.reset()
+        terminal = None
+        if self._env._step + 1 >= EPISODE_STEPS:   # this step ends the episode
+            if self._shadow is None:
+                self._shadow = BatchedReacher(1, seed=0, device=self._env.device)
+            st, _, _ = self._env.get_state()
+            self._shadow.set_state(st, step=0, episode=0)
+            terminal = self._shadow.step(act)[0][0].double().cpu().numpy()
         ob, r, d, _ = self._env.step(act)
         done = bool(d[0].item())
+        ob = ob[0].double().cpu().numpy()
         if done:
             self._needs_reset = True
             # the kernel already auto-reset; the reference calls env.reset() next, which
             # must hand out that same reset observation (not draw another one)
-            self._pending = ob[0].double().cpu().numpy()
+            self._pending = ob
+            ob = terminal
         reward_ctrl = -float(np.square(a32).sum())
         rew = float(r[0].item())
         info = dict(reward_dist=rew - reward_ctrl, reward_ctrl=reward_ctrl)
-        return ob[0].double().cpu().numpy(), rew, done, info
+        return ob, rew, done, info
 
 
 def make_mujoco_env(env_id: str, seed: int, device="cuda:0"):

@@ -67,7 +67,7 @@ class _Comm1:
         idb = (ctypes.c_uint8 * 128)()
         nat.check(self._lib.rd_comm_unique_id(idb), "rd_comm_unique_id")
         h = ctypes.c_void_p()
-        nat.check(self._lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0), "rd_comm_create")
+        nat.check(self._lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0, 60.0), "rd_comm_create")
         self.handle, self.world = h, 1
 
     def close(self):

@@ -138,39 +138,66 @@ def test_native_comm_host_contract():
         return
     assert any(bytes(idb))
     h = ctypes.c_void_p()
-    assert lib.rd_comm_create(ctypes.byref(h), idb, 0, 0, 0) != 0          # nranks 0
+    assert lib.rd_comm_create(ctypes.byref(h), idb, 0, 0, 0, 60.0) != 0    # nranks 0
     assert b"bad argument" in lib.rd_last_error()
-    assert lib.rd_comm_create(ctypes.byref(h), idb, 2, 2, 0) != 0          # rank out of range
+    assert lib.rd_comm_create(ctypes.byref(h), idb, 2, 2, 0, 60.0) != 0    # rank out of range
+    assert lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0, 0.0) != 0     # no deadline
     assert lib.rd_comm_allreduce_f32(None, None, 4, None) != 0
     assert lib.rd_comm_nranks(None) == 0 and lib.rd_comm_destroy(None) == 0
     if not torch.cuda.is_available():
-        assert lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0) != 0      # no HIP device here
+        assert lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0, 60.0) != 0   # no HIP device here
         assert lib.rd_last_error()
+        assert lib.rd_comm_probe(0) != 0 and b"rd_comm_probe" in lib.rd_last_error()
 
 
-def _comm_rank(rank, world, port, out):
+def _comm_rank(rank, world, port, out, inject=None):
+    import datetime
+
     import torch.distributed as dist
 
+    from reacherdistilation_amd import _native as nat
     from reacherdistilation_amd.dist import RcclComm
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a short collective timeout: a regression that leaves a rank waiting fails fast
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=30))
+    if inject == "rank0_id":   # every rank passes the probe; rank 0 cannot draw the id
+        lib = nat.load()
+        lib.rd_comm_probe = lambda device: 0
+        if rank == 0:
+            lib.rd_comm_unique_id = lambda buf: 1
+            lib.rd_last_error = lambda: b"injected failure"
     try:
         RcclComm(torch.device("cpu"))
-        out[rank] = "created"
+        out[rank] = ("created", "")
     except Exception as e:  # noqa: BLE001
-        out[rank] = type(e).__name__
+        out[rank] = (type(e).__name__, str(e))
     dist.destroy_process_group()
 
 
-@pytest.mark.skipif(torch.cuda.is_available(), reason="the no-device failure path is exercised on CPU hosts")
-def test_native_comm_failure_reaches_every_rank():
-    """Two gloo ranks build dist.RcclComm on a host without a HIP device: the id broadcast
-    completes, every rank's rd_comm_create fails, and each raises NativeError -- no rank is
-    left waiting in a collective (the bench then uses torch's collective)."""
+def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    return port
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="the no-device failure path is exercised on CPU hosts")
+def test_native_comm_failure_reaches_every_rank():
+    """Two gloo ranks build dist.RcclComm on a host without a HIP device: both fail the
+    probe, the group agrees on it, and each raises NativeError naming the ranks that cannot
+    join -- before any RCCL call, with no rank left waiting in a collective."""
     out = mp.get_context("spawn").Manager().dict()
-    mp.start_processes(_comm_rank, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
-    assert out[0] == out[1] == "NativeError"
+    mp.start_processes(_comm_rank, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    assert out[0][0] == out[1][0] == "NativeError"
+    assert "[0, 1] cannot join" in out[0][1] and "[0, 1] cannot join" in out[1][1]
+
+
+def test_rank0_id_failure_reaches_every_rank():
+    """Rank 0 fails to draw the RCCL unique id (injected); rank 1 must not wait for it: both
+    raise, and rank 1's message names rank 0."""
+    out = mp.get_context("spawn").Manager().dict()
+    mp.start_processes(_comm_rank, args=(2, _free_port(), out, "rank0_id"), nprocs=2, join=True,
+                       start_method="spawn")
+    assert out[0][0] == out[1][0] == "NativeError"
+    assert "failed on rank 0" in out[1][1] and "injected failure" in out[0][1]

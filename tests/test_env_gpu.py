@@ -55,11 +55,20 @@ def test_single_env_gym_api_fixture(golden):
         assert o.dtype == np.float64 and o.shape == (11,)
         np.testing.assert_allclose(o, ob[e, 0], atol=1e-6, rtol=0)
         for k in range(50):
+            o_in = o
             o, r, done, info = env.step(act[e, k][None])
             assert done == (k == 49)
             if k < 49:
                 np.testing.assert_allclose(o, ob[e, k + 1], atol=OB_ATOL, rtol=OB_RTOL)
                 assert abs(r - rew[e, k + 1]) < R_ATOL
+            else:   # gym's terminal observation: the f64 oracle's step from the last state
+                st = np.array([[np.arctan2(o_in[2], o_in[0])], [np.arctan2(o_in[3], o_in[1])], [o_in[6]], [o_in[7]],
+                               [o_in[4]], [o_in[5]], [o_in[8]], [o_in[9]]])
+                want, _ = __import__("oracle.ref_c", fromlist=["x"]).step(st, act[e, k][None].astype(np.float32),
+                                                                         np.float64)
+                np.testing.assert_allclose(o, want[0], atol=OB_ATOL, rtol=OB_RTOL)
+                if e < 24:
+                    assert not np.allclose(o, ob[e + 1, 0], atol=1e-3)   # not the next reset
             assert set(info) == {"reward_dist", "reward_ctrl"}
     with pytest.raises(RuntimeError):
         env.step(np.zeros(2))

@@ -61,3 +61,38 @@ def test_c5_global_batch_equals_eight_shards():
     assert rel < 1e-5, rel
     assert torch.equal(torch.cat(states, dim=1), s_full)
     assert np.isfinite(g_full.cpu().numpy()).all()
+
+
+def test_c4_full_size_gradient_matches_oracle():
+    """c4 at its full per-GPU size (262,144 envs, teacher-driven, staggered, MSE): the rollout
+    gradient vs the f64 numpy oracle (policy_np, pinned to the reference graph) within
+    2e-4 x max|g|, and every env's transition vs the f64 C oracle (tests/test_distill_gpu.py
+    _grad_check)."""
+    from tests.test_distill_gpu import _grad_check, _trainer
+    tr = _trainer(262144, loss="mse")
+    assert tr.cfg.stagger
+    _grad_check(tr, "mse", "teacher")
+
+
+@pytest.mark.parametrize("loss", ["mse", "kl"])
+def test_c5_shard_gradient_matches_bf16_oracle(loss):
+    """A c5 shard (rank 5 of 8: 131,072 of 1,048,576 envs, DAgger, bf16 student) vs the bf16
+    oracle (policy_np.forward_bf16 / backward_bf16, MSE normalised by the global N), with the
+    tolerances of tests/test_distill_gpu.py's bf16 tests."""
+    from oracle import policy_np as pn
+    from tests.test_distill_gpu import _np_params, _obs_from_state
+    N, rank = 8 * 131072, 5
+    tr = _tr(n_envs_global=N, rank=rank, world_size=8, loss=loss, act_with="student", student_dtype="bf16")
+    assert tr.n_local == 131072 and tr.env_base == rank * 131072
+    st0 = tr.env_state().cpu().numpy()
+    sp = tr.student_params().cpu().numpy().astype(np.float64)
+    tr.rollout()
+    g = tr.grad().cpu().numpy()
+    ob = _obs_from_state(st0).astype(np.float32)
+    fs = pn.forward_bf16(sp, *_np_params(tr.student)[1:], ob)
+    ft = pn.forward(*_np_params(tr.teacher), ob.astype(np.float64))
+    # MSE is normalised by the global N; the KL is a sum, so dlogstd is over this shard's rows
+    L, dmean, dls, sq = pn.loss_and_dmean(fs, ft, loss, N)
+    gb = pn.backward_bf16(sp, fs, dmean, dls)
+    err = np.abs(g - gb).max() / np.abs(gb).max()
+    assert err < 1e-2, err
