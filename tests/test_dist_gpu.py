@@ -68,7 +68,7 @@ class _Comm1:
         nat.check(self._lib.rd_comm_unique_id(idb), "rd_comm_unique_id")
         h = ctypes.c_void_p()
         nat.check(self._lib.rd_comm_create(ctypes.byref(h), idb, 1, 0, 0, 60.0), "rd_comm_create")
-        self.handle, self.world = h, 1
+        self.handle, self.world, self.rank, self.device = h, 1, 0, torch.device("cuda:0")
 
     def close(self):
         self._lib.rd_comm_destroy(self.handle)
@@ -114,3 +114,44 @@ def test_bound_comm_step_is_bitwise_the_single_rank_step(accum):
         b.close()
     finally:
         c.close()
+
+
+def _rccl_rank(rank, world, port, out):
+    import torch.distributed as dist
+
+    from reacherdistilation_amd.dist import RcclComm
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dev = torch.device("cuda", rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    comm = RcclComm(dev, timeout=60.0)
+    assert comm.self_check()
+    tr = DistillTrainer(DistillConfig(n_envs_global=N_GLOBAL, seed=7, lr=1e-3), device=dev,
+                        rank=rank, world_size=world, comm=comm)
+    for _ in range(STEPS):
+        tr.step()
+    out[rank] = (tr.student_params().cpu().numpy(), tr.env_state().cpu().numpy(), tr.metrics(STEPS),
+                 tr.replicas_identical())
+    tr.close()
+    comm.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two HIP devices (one per rank)")
+def test_two_devices_native_rccl_match_single_rank():
+    """Two ranks on two devices, the native RCCL communicator bound (the multi-GPU bench's
+    path): the same student as one rank over the whole batch (within f32 summation order),
+    bitwise-identical replicas."""
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    out = mp.get_context("spawn").Manager().dict()
+    mp.start_processes(_rccl_rank, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
+    ref = DistillTrainer(DistillConfig(n_envs=N_GLOBAL, seed=7, lr=1e-3), device="cuda:0")
+    for _ in range(STEPS):
+        ref.step()
+    p_ref, st_ref = ref.student_params().cpu().numpy(), ref.env_state().cpu().numpy()
+    (p0, st0, m0, same0), (p1, st1, m1, same1) = out[0], out[1]
+    assert same0 and same1 and np.array_equal(p0, p1)
+    np.testing.assert_allclose(p0, p_ref, atol=1e-5)
+    np.testing.assert_allclose(np.concatenate([st0, st1], axis=1), st_ref, atol=1e-4)
+    np.testing.assert_allclose(m0[:, 3] + m1[:, 3], ref.metrics(STEPS)[:, 3])
