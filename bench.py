@@ -67,6 +67,9 @@ def parse():
                     help="also time K env-steps per optimiser step (SURVEY §8d: K = 50 = one episode); 0 = skip")
     ap.add_argument("--conv-steps", type=int, default=5000,
                     help="convergence leg: optimiser steps allowed to reach student action-MSE < 1e-3; 0 = skip")
+    ap.add_argument("--f32-mode", default="exact", choices=["exact", "split"],
+                    help="f32 hidden-layer products: exact f32 MFMA, or f32 emulated on bf16 MFMAs by exact "
+                         "3-piece operand splits (include/reacher_distill.h f32_split)")
     ap.add_argument("--conv-small-envs", type=int, default=256,
                     help="env count of the second convergence run (the env-step reading of the budget)")
     return ap.parse_args()
@@ -210,7 +213,7 @@ def cpu_baseline(workload, seconds, threads, n):
                        f"OpenMP {threads} threads")
 
 
-def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=100, comm=None):
+def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=100, comm=None, split=False):
     """North-star check: optimiser steps (one per env step, the reference's lr 1e-4 TF1 Adam)
     until the student's action-MSE vs the teacher, averaged over the last 10 steps and all
     ranks, falls below 1e-3 -- against the reference's budget of 5000 episodes x 50 steps =
@@ -220,7 +223,8 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
 
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
     tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
-                                      student_dtype=sdt), device=dev, rank=rank, world_size=world, comm=comm)
+                                      student_dtype=sdt, f32_split=split), device=dev, rank=rank, world_size=world,
+                        comm=comm)
     t0 = time.perf_counter()
     steps, mse, hit = 0, float("nan"), None
     while steps < max_steps:
@@ -295,6 +299,7 @@ def main():
     wl = WORKLOADS[args.workload]
     n = args.envs_per_gpu or wl["envs"]
     sdt = wl.get("student_dtype", "f32")
+    split = args.f32_mode == "split"
 
     # The convergence leg runs first, on trainers of its own: it is the north star's student
     # action-MSE check, and its ~1,000 back-to-back steps also take the GPU out of its idle
@@ -302,11 +307,13 @@ def main():
     # the kernels rather than the clock ramp.
     conv = conv_small = None
     if args.conv_steps > 0:
-        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm)
+        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm, split=split)
         # the same check at a small per-GPU batch: the env-step reading of the reference's budget
-        conv_small = convergence(wl, args.conv_small_envs, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm)
+        conv_small = convergence(wl, args.conv_small_envs, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm,
+                                 split=split)
 
-    cfg = DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr, student_dtype=sdt)
+    cfg = DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr, student_dtype=sdt,
+                        f32_split=split)
     tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world, comm=comm)
 
     def one_step(ev=None):
@@ -360,7 +367,7 @@ def main():
     accum = None
     if args.accum > 1:   # secondary line: one optimiser step (+ all-reduce) per K env-steps
         tk = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr,
-                                          student_dtype=sdt, accum_steps=args.accum),
+                                          student_dtype=sdt, accum_steps=args.accum, f32_split=split),
                             device=dev, rank=rank, world_size=world, comm=comm)
         ksteps = 2 * args.accum
         for _ in range(args.accum):
@@ -423,7 +430,7 @@ def main():
                        "envs_total": n * world, "student": f"MlpPolicy 2x64 tanh (5060 params, {sdt})",
                        "teacher": "MlpPolicy 2x64 tanh", "loss": wl["loss"], "act_with": wl["act_with"],
                        "optimizer": f"TF1 Adam lr {args.lr}, 1 step per env-step",
-                       "parallelism": f"dp{world}", "collective": collective},
+                       "parallelism": f"dp{world}", "collective": collective, "f32_mode": args.f32_mode},
             # the north star's student action-MSE: after the convergence leg (< 1e-3 within its
             # budget); the timed run's own value (220 steps from init) is kept beside it
             "student_mse": conv["student_mse_final"] if conv is not None else mse,

@@ -58,6 +58,10 @@ typedef struct {
     int32_t accum_steps;     /* K env steps (rollouts) per optimiser step; 0 or 1 = the
                                 reference's one Adam step per env step.  Scales the MSE
                                 normalisation to 1 / (K n_envs_global)                  */
+    int32_t f32_split;       /* 0: every f32 product on v_mfma_f32_16x16x4_f32 (exact f32);
+                                1: the K = 64 hidden-layer products of the f32 nets (both
+                                layer 2s; the f32 student's dH1) as f32 emulated on bf16
+                                MFMAs with three-piece operand splits (see below)        */
 } rdd_config;
 
 /* Student precision.  RDD_DTYPE_F32: every product exact f32 (v_mfma_f32_16x16x4_f32).
@@ -68,6 +72,13 @@ typedef struct {
  * either way.  oracle/policy_np.py forward_bf16/backward_bf16 define the arithmetic. */
 #define RDD_DTYPE_F32 0
 #define RDD_DTYPE_BF16 1
+
+/* f32_split = 1 keeps f32 accuracy on gfx950's 16x faster bf16 matrix path: each f32
+ * operand is split EXACTLY into three bf16 pieces (x = x0 + x1 + x2: x truncated to bf16,
+ * the remainder truncated, the rest, which has at most 8 significant bits), and a product
+ * sums the six partial products x2y0 + x1y1 + x0y2 + x1y0 + x0y1 + x0y0 (each exact in the
+ * MFMA) into the f32 accumulator; the three dropped terms are below 2^-24 |x||y|.  Layer 1
+ * (K = 12), the weight gradients, biases, tanh, the loss and Adam are unchanged f32. */
 
 /* Staggered episodes.  The reference steps ONE env and trains on random windows drawn
  * from past episodes (dataset.py:179-194), so a training batch mixes episode phases.  N

@@ -441,14 +441,266 @@ __device__ void load_net_bf16(float* L, const float* g, int nthreads) {
     }
 }
 
+// ---------------------------------------------------------------- f32 on bf16 MFMAs (split images)
+// gfx950 runs f32 MFMAs at 1/16 of the bf16 rate, and beside them VALU work serialises on
+// the SIMD's issue.  With rdd_config.f32_split the hidden-layer products
+// (K = 64: both nets' layer 2 and the student's dH1 = W2 dZ2) run as f32 EMULATED on
+// v_mfma_f32_16x16x32_bf16: each operand is split exactly into three bf16 pieces
+//   x = x0 + x1 + x2,  x0 = x truncated to bf16, x1 = (x - x0) truncated, x2 = the rest,
+// (x2 has at most 8 significant bits, so the split loses nothing) and a K = 32 step sums
+// the six partial products of order >= 2^-16 (x2y0, x1y1, x0y2, x1y0, x0y1, x0y0, smallest
+// first), each exact in the MFMA, into the f32 accumulator.  The dropped terms are below
+// 2^-24 of |x||y|: f32 accuracy (scripts/micro/split_layer.hip: max error 1.5e-7 of
+// sum|terms| vs 1.3e-7 for the exact f32 MFMA form; 1.54x its throughput).  Weight pieces
+// are prepacked (pack_param); activation pieces are made per tile (split8).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split1(float x, unsigned short (&h)[3]) {
+    const uint32_t u = __float_as_uint(x);
+    const float r = x - __uint_as_float(u & 0xffff0000u);
+    const uint32_t ur = __float_as_uint(r);
+    const float l = r - __uint_as_float(ur & 0xffff0000u);
+    h[0] = (unsigned short)(u >> 16);
+    h[1] = (unsigned short)(ur >> 16);
+    h[2] = (unsigned short)(__float_as_uint(l) >> 16);
+}
+
+// lo = features k-slots jj 0..3, hi = jj 4..7 (the B operand order of the permuted images)
+__device__ __forceinline__ void split8(f32x4 lo, f32x4 hi, bf16x8 (&p)[3]) {
+    const float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    uint32_t u0[8], u1[8], u2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t u = __float_as_uint(x[i]);
+        const float r = x[i] - __uint_as_float(u & 0xffff0000u);
+        const uint32_t ur = __float_as_uint(r);
+        u0[i] = u;
+        u1[i] = ur;
+        u2[i] = __float_as_uint(r - __uint_as_float(ur & 0xffff0000u));
+    }
+    u32x4 q0, q1, q2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // high halves of two words -> one packed pair
+        q0[i] = __builtin_amdgcn_perm(u0[2 * i + 1], u0[2 * i], 0x07060302u);
+        q1[i] = __builtin_amdgcn_perm(u1[2 * i + 1], u1[2 * i], 0x07060302u);
+        q2[i] = __builtin_amdgcn_perm(u2[2 * i + 1], u2[2 * i], 0x07060302u);
+    }
+    p[0] = __builtin_bit_cast(bf16x8, q0);
+    p[1] = __builtin_bit_cast(bf16x8, q1);
+    p[2] = __builtin_bit_cast(bf16x8, q2);
+}
+
+// acc += W . X over one K = 32 step from split pieces w[3] (A) and x[3] (B)
+__device__ __forceinline__ f32x4 mfma_split(const bf16x8 (&w)[3], const bf16x8 (&x)[3], f32x4 c) {
+    c = mfma_k32(w[2], x[0], c);
+    c = mfma_k32(w[1], x[1], c);
+    c = mfma_k32(w[0], x[2], c);
+    c = mfma_k32(w[1], x[0], c);
+    c = mfma_k32(w[0], x[1], c);
+    return mfma_k32(w[0], x[0], c);
+}
+
+// Split-mode image of a net (offsets in floats): W1 [12][16][4] f32 (as N_W1, scaled) and the
+// small vectors first, then the three pieces of the scaled W2 in the bf16 student's permuted
+// forward order [q][s 2][g 4][fb 4][i 16][jj 8] = piece q of kTanhScale W2[kperm(s,g,jj)][16fb+i];
+// the student adds the pieces of the unscaled W2 for dH1 in the NB_W2B order.
+constexpr int SP_PIECE = 2 * 4 * 4 * 16 * 8;      // bf16 elements per piece
+constexpr int NX_W1 = 0;
+constexpr int NX_B2 = NX_W1 + 12 * HID;           // 768
+constexpr int NX_W3 = NX_B2 + HID;                // 832
+constexpr int NX_B3 = NX_W3 + HID * ACD;          // 960
+constexpr int NX_LS = NX_B3 + ACD;
+constexpr int NX_MU = NX_LS + ACD;
+constexpr int NX_RS = NX_MU + 12;
+constexpr int NX_W2F = NX_RS + 12;                // 988
+constexpr int NETX = NX_W2F + 3 * SP_PIECE / 2;   // 7132
+constexpr int NX_W2B = NETX;                      // student only
+constexpr int NETX_S = NX_W2B + 3 * SP_PIECE / 2; // 13276
+static_assert(NX_W3 % 4 == 0 && NX_B2 % 4 == 0 && NX_W2F % 4 == 0 && NETX % 4 == 0 && NETX_S % 4 == 0,
+              "16-B aligned split images");
+
+// the student image's W3 / filter offsets by kind: exact f32 (N_*), split (NX_*), bf16 (NB_*)
+template <int K> struct Off;
+template <> struct Off<0> { static constexpr int W3 = N_W3, MU = N_MU, RS = N_RS; };
+template <> struct Off<1> { static constexpr int W3 = NX_W3, MU = NX_MU, RS = NX_RS; };
+template <> struct Off<2> { static constexpr int W3 = NB_W3, MU = NB_MU, RS = NB_RS; };
+
+__device__ __forceinline__ void ld_pieces(const float* L, int base, int o, bf16x8 (&w)[3]) {
+    const unsigned short* h = reinterpret_cast<const unsigned short*>(L + base);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) w[q] = *reinterpret_cast<const bf16x8*>(h + q * SP_PIECE + o);
+}
+
+// Teacher and student forwards of one tile with split images (both nets, interleaved):
+// layer 1 exact f32 (K = 12, as mlp_forward_pair), layer 2 on split bf16 MFMAs.
+__device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const float* LS, const float* ob, int j, int g,
+                                                       f32x4 (&H1)[4], f32x4 (&H2)[4], float& mt0, float& mt1,
+                                                       float& ms0, float& ms1) {
+    f32x4 at[4], as[4];
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) at[fb] = as[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        const int k = 4 * s + g;
+        const float x = ob[j * SOS + k];
+        const float zt = fminf(fmaxf((x - LT[NX_MU + k]) * LT[NX_RS + k], -5.0f), 5.0f);
+        const float zs = fminf(fmaxf((x - LS[NX_MU + k]) * LS[NX_RS + k], -5.0f), 5.0f);
+        const f32x4 wt = ld4(LT + NX_W1 + k * HID + 4 * j);
+        const f32x4 ws = ld4(LS + NX_W1 + k * HID + 4 * j);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            at[fb] = mfma(wt[fb], zt, at[fb]);
+            as[fb] = mfma(ws[fb], zs, as[fb]);
+        }
+    }
+    f32x4 T1[4];
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            T1[fb][r] = tanh_pre(at[fb][r]);
+            H1[fb][r] = tanh_pre(as[fb][r]);
+        }
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) {
+        at[fb] = ld4(LT + NX_B2 + 16 * fb + 4 * g);
+        as[fb] = ld4(LS + NX_B2 + 16 * fb + 4 * g);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
+        bf16x8 tp[3], sp[3];
+        split8(T1[2 * s], T1[2 * s + 1], tp);
+        split8(H1[2 * s], H1[2 * s + 1], sp);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            const int o = (((s * 4 + g) * 4 + fb) * 16 + j) * 8;
+            bf16x8 wt[3], ws[3];
+            ld_pieces(LT, NX_W2F, o, wt);
+            ld_pieces(LS, NX_W2F, o, ws);
+            at[fb] = mfma_split(wt, tp, at[fb]);
+            as[fb] = mfma_split(ws, sp, as[fb]);
+        }
+    }
+    float pt0 = 0.0f, pt1 = 0.0f, ps0 = 0.0f, ps1 = 0.0f;
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) {
+        const f32x4 ta = ld4(LT + NX_W3 + (16 * fb + 4 * g) * 2), tb = ld4(LT + NX_W3 + (16 * fb + 4 * g) * 2 + 4);
+        const f32x4 sa = ld4(LS + NX_W3 + (16 * fb + 4 * g) * 2), sb = ld4(LS + NX_W3 + (16 * fb + 4 * g) * 2 + 4);
+        f32x4 t2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            t2[r] = tanh_pre(at[fb][r]);
+            H2[fb][r] = tanh_pre(as[fb][r]);
+        }
+        pt0 = fmaf(t2[0], ta[0], pt0); pt1 = fmaf(t2[0], ta[1], pt1);
+        pt0 = fmaf(t2[1], ta[2], pt0); pt1 = fmaf(t2[1], ta[3], pt1);
+        pt0 = fmaf(t2[2], tb[0], pt0); pt1 = fmaf(t2[2], tb[1], pt1);
+        pt0 = fmaf(t2[3], tb[2], pt0); pt1 = fmaf(t2[3], tb[3], pt1);
+        ps0 = fmaf(H2[fb][0], sa[0], ps0); ps1 = fmaf(H2[fb][0], sa[1], ps1);
+        ps0 = fmaf(H2[fb][1], sa[2], ps0); ps1 = fmaf(H2[fb][1], sa[3], ps1);
+        ps0 = fmaf(H2[fb][2], sb[0], ps0); ps1 = fmaf(H2[fb][2], sb[1], ps1);
+        ps0 = fmaf(H2[fb][3], sb[2], ps0); ps1 = fmaf(H2[fb][3], sb[3], ps1);
+    }
+    mt0 = xsum32(xsum16(pt0)) + LT[NX_B3];
+    mt1 = xsum32(xsum16(pt1)) + LT[NX_B3 + 1];
+    ms0 = xsum32(xsum16(ps0)) + LS[NX_B3];
+    ms1 = xsum32(xsum16(ps1)) + LS[NX_B3 + 1];
+}
+
+// One net's forward with a split image (the teacher beside the bf16 student).
+__device__ __forceinline__ void mlp_forward_split(const float* L, const float* ob, int j, int g, float& m0, float& m1) {
+    f32x4 acc[4];
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) acc[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        const int k = 4 * s + g;
+        const float z = fminf(fmaxf((ob[j * SOS + k] - L[NX_MU + k]) * L[NX_RS + k], -5.0f), 5.0f);
+        const f32x4 w = ld4(L + NX_W1 + k * HID + 4 * j);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], z, acc[fb]);
+    }
+    f32x4 H1[4];
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) H1[fb][r] = tanh_pre(acc[fb][r]);
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NX_B2 + 16 * fb + 4 * g);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        bf16x8 hp[3];
+        split8(H1[2 * s], H1[2 * s + 1], hp);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            bf16x8 w[3];
+            ld_pieces(L, NX_W2F, (((s * 4 + g) * 4 + fb) * 16 + j) * 8, w);
+            acc[fb] = mfma_split(w, hp, acc[fb]);
+        }
+    }
+    float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) {
+        const f32x4 wa = ld4(L + NX_W3 + (16 * fb + 4 * g) * 2);
+        const f32x4 wb = ld4(L + NX_W3 + (16 * fb + 4 * g) * 2 + 4);
+        f32x4 h2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h2[r] = tanh_pre(acc[fb][r]);
+        p0 = fmaf(h2[0], wa[0], p0); p1 = fmaf(h2[0], wa[1], p1);
+        p0 = fmaf(h2[1], wa[2], p0); p1 = fmaf(h2[1], wa[3], p1);
+        p0 = fmaf(h2[2], wb[0], p0); p1 = fmaf(h2[2], wb[1], p1);
+        p0 = fmaf(h2[3], wb[2], p0); p1 = fmaf(h2[3], wb[3], p1);
+    }
+    m0 = xsum32(xsum16(p0)) + L[NX_B3];
+    m1 = xsum32(xsum16(p1)) + L[NX_B3 + 1];
+}
+
 // ---------------------------------------------------------------- prepacked LDS images
 // The rollout's LDS images (teacher NET floats, student NET_S floats) are kept ready in
 // HBM: pack_param() writes one parameter's value into every image slot it occupies.  The
 // images are built once by pack_net_kernel (rdd_set_teacher / rdd_set_student) and the
 // student's is refreshed by reduce_adam_kernel as it updates each parameter, so a rollout's
 // prologue is a plain 16-B copy instead of a gather with index arithmetic.
-__device__ __forceinline__ void pack_param(float* img, int p, float v, bool student, bool bf16) {
-    if (!bf16) {
+// image kinds: IMG_F32 (N_* layout), IMG_SPLIT (NX_*), IMG_BF16 (NB_*, student only)
+constexpr int IMG_F32 = 0, IMG_SPLIT = 1, IMG_BF16 = 2;
+
+__device__ __forceinline__ void pack_param(float* img, int p, float v, bool student, int kind) {
+    if (kind == IMG_SPLIT) {
+        unsigned short* h = reinterpret_cast<unsigned short*>(img);
+        unsigned short q[3];
+        if (p < P_B1) {
+            const int k = p >> 6, f = p & 63;
+            img[NX_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+        } else if (p < P_W2) {
+            const int f = p - P_B1;
+            img[NX_W1 + OBD * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+        } else if (p < P_B2) {
+            const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
+            {   // forward: k is the permuted K index (as NB_W2F), pieces of the scaled weight
+                const int s = k >> 5, r = k & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
+                const int o = 2 * NX_W2F + (((s * 4 + gg) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + jj;
+                split1(kTanhScale * v, q);
+                h[o] = q[0]; h[o + SP_PIECE] = q[1]; h[o + 2 * SP_PIECE] = q[2];
+            }
+            if (student) {   // dH1: f is the permuted K index (as NB_W2B), unscaled
+                const int s = f >> 5, r = f & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
+                const int o = 2 * NX_W2B + (((s * 4 + gg) * 4 + (k >> 4)) * 16 + (k & 15)) * 8 + jj;
+                split1(v, q);
+                h[o] = q[0]; h[o + SP_PIECE] = q[1]; h[o + 2 * SP_PIECE] = q[2];
+            }
+        } else if (p < P_W3) {
+            img[NX_B2 + (p - P_B2)] = kTanhScale * v;
+        } else if (p < P_B3) {
+            img[NX_W3 + (p - P_W3)] = v;
+        } else if (p < P_LS) {
+            img[NX_B3 + (p - P_B3)] = v;
+        } else if (p < P_TOT) {
+            img[NX_LS + (p - P_LS)] = v;
+        }
+        return;
+    }
+    if (kind == IMG_F32) {
         if (p < P_B1) {
             const int k = p >> 6, f = p & 63;
             img[N_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
@@ -501,17 +753,18 @@ __device__ __forceinline__ void pack_param(float* img, int p, float v, bool stud
 
 // net = params[P] | mu[11] | sd[11] -> image (every slot, including zero padding and filter)
 __global__ __launch_bounds__(256) void pack_net_kernel(const float* net, float* img, int img_floats, int student,
-                                                       int bf16) {
+                                                       int kind) {
     const int x = blockIdx.x * 256 + threadIdx.x;
     // phase 1 (one launch): zero the image, then the filter words, then every parameter
     for (int i = x; i < img_floats; i += gridDim.x * 256) img[i] = 0.0f;
     __syncthreads();   // (single-block launch: see rdd host code)
     if (x < 12) {
-        const int mu = bf16 ? NB_MU : N_MU, rs = bf16 ? NB_RS : N_RS;
+        const int mu = kind == IMG_BF16 ? NB_MU : kind == IMG_SPLIT ? NX_MU : N_MU;
+        const int rs = kind == IMG_BF16 ? NB_RS : kind == IMG_SPLIT ? NX_RS : N_RS;
         img[mu + x] = x < OBD ? net[P_TOT + x] : 0.0f;
         img[rs + x] = x < OBD ? 1.0f / net[P_TOT + OBD + x] : 1.0f;
     }
-    for (int p = x; p < P_TOT; p += gridDim.x * 256) pack_param(img, p, net[p], student != 0, bf16 != 0);
+    for (int p = x; p < P_TOT; p += gridDim.x * 256) pack_param(img, p, net[p], student != 0, kind);
 }
 
 // Both rollout images (contiguous in LDS: teacher then student) with every 16-B load of a
@@ -630,17 +883,24 @@ __device__ __forceinline__ float env_step_group(const RolloutArgs& a, uint32_t C
     return rew;
 }
 
-template <bool BS>   // BS: bf16 student (RDD_DTYPE_BF16)
+// LDS floats of the teacher / student images of a rollout instance
+constexpr int img_t(bool SPL) { return SPL ? NETX : NET; }
+constexpr int img_s(bool BS, bool SPL) { return BS ? NET_S : (SPL ? NETX_S : NET_S); }
+static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NET_S + PAIRS * PSCR) * 4 <= 160 * 1024,
+              "LDS budget (split images)");
+
+template <bool BS, bool SPL>   // BS: bf16 student (RDD_DTYPE_BF16); SPL: split-bf16 f32 hidden layers
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
-    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+    constexpr int TN = img_t(SPL), SN = img_s(BS, SPL);
+    __shared__ __attribute__((aligned(16))) float lds[TN + SN + PAIRS * PSCR];
     float* LT = lds;
-    float* LS = lds + NET;
+    float* LS = lds + TN;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const int pair = wave & (PAIRS - 1);
     const bool producer = wave < PAIRS;
-    float* PS = lds + NET + NET_S + pair * PSCR;
-    uint32_t* flags = reinterpret_cast<uint32_t*>(lds + NET + NET_S + pair * PSCR + P_FLAGS);
+    float* PS = lds + TN + SN + pair * PSCR;
+    uint32_t* flags = reinterpret_cast<uint32_t*>(lds + TN + SN + pair * PSCR + P_FLAGS);
     uint32_t* err = a.ctl + 8;
 
     RTSTAMP(16);
@@ -655,10 +915,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     if (producer && !a.obs_in && gfirst < ngroups && lane < gs && gfirst * gs + lane < a.n)
         load_state(a.state, a.n, (uint32_t)(gfirst * gs + lane), st0);
     static_assert(NET % 4 == 0 && NET_S % 4 == 0, "16-B images");
-    copy_images<NET / 4, NET_S / 4, BLOCK>(LT, a.timg, a.simg);   // LS = LT + NET
-    constexpr int SW3 = BS ? NB_W3 : N_W3, SMU = BS ? NB_MU : N_MU, SRS = BS ? NB_RS : N_RS;
+    copy_images<TN / 4, SN / 4, BLOCK>(LT, a.timg, a.simg);   // LS = LT + TN
+    using SO = Off<BS ? IMG_BF16 : (SPL ? IMG_SPLIT : IMG_F32)>;
+    constexpr int SW3 = SO::W3, SMU = SO::MU, SRS = SO::RS;
     if (threadIdx.x < PAIRS * 4)
-        reinterpret_cast<uint32_t*>(lds + NET + NET_S + (threadIdx.x >> 2) * PSCR + P_FLAGS)[threadIdx.x & 3] = 0u;
+        reinterpret_cast<uint32_t*>(lds + TN + SN + (threadIdx.x >> 2) * PSCR + P_FLAGS)[threadIdx.x & 3] = 0u;
 
     const uint32_t C = a.ctl[0];
     // snapshot of the step words for reduce_adam_kernel, which rewrites ctl[0..3]; ctl[12]
@@ -717,10 +978,12 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 float mt0, mt1, ms0, ms1;
                 STAMP(10);
                 if constexpr (BS) {
-                    mlp_forward(LT, obt, j, g, H1, H2, mt0, mt1);
+                    if constexpr (SPL) mlp_forward_split(LT, obt, j, g, mt0, mt1);
+                    else mlp_forward(LT, obt, j, g, H1, H2, mt0, mt1);
                     mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
                 } else {
-                    mlp_forward_pair(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                    if constexpr (SPL) mlp_forward_pair_split(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                    else mlp_forward_pair(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
                 }
                 STAMP(12);
                 // loss
@@ -915,6 +1178,20 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     // dH1 = W2 . dZ2 (A = W2^T image)
 #pragma unroll
                     for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if constexpr (SPL) {   // two K = 32 steps on split pieces (dZ2 in accumulator layout = B)
+#pragma unroll
+                        for (int s = 0; s < 2; ++s) {
+                            __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
+                            bf16x8 dp[3];
+                            split8(dZ[2 * s], dZ[2 * s + 1], dp);
+#pragma unroll
+                            for (int mb = 0; mb < 4; ++mb) {
+                                bf16x8 w[3];
+                                ld_pieces(LS, NX_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8, w);
+                                acc[mb] = mfma_split(w, dp, acc[mb]);
+                            }
+                        }
+                    } else {
                     f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
 #pragma unroll
                     for (int fb = 0; fb < 4; ++fb)
@@ -928,6 +1205,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
 #pragma unroll
                             for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
                         }
+                    }
                 }
                 STAMP(14);
                 float* sa = PS + P_SA;
@@ -1029,7 +1307,7 @@ struct ReduceArgs {
     int bump_env, bump_opt;    // advance the env clock (after a reduce) / the optimiser step
     float lr, b1, b2, eps;
     float* simg;       // student LDS image, refreshed with every updated parameter
-    int bf16;
+    int img_kind;      // IMG_F32 / IMG_SPLIT / IMG_BF16
 };
 
 #ifndef RDD_RED_COLS   // diagnostic builds may change the reduce blocking (A/B)
@@ -1099,7 +1377,7 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
             a.v[p] = v;
             const float w = w_p - (m * alpha) / (sqrtf(v) + a.eps);
             a.params[p] = w;
-            pack_param(a.simg, p, w, true, a.bf16 != 0);
+            pack_param(a.simg, p, w, true, a.img_kind);
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1228,6 +1506,16 @@ int group_envs(int64_t n, int pairs_total) {
     return 16;
 }
 
+// LDS image kinds and sizes (floats) of a trainer's teacher and student
+int teacher_kind(const rdd_trainer* t) { return t->cfg.f32_split ? IMG_SPLIT : IMG_F32; }
+int student_kind(const rdd_trainer* t) {
+    return t->cfg.student_dtype == RDD_DTYPE_BF16 ? IMG_BF16 : (t->cfg.f32_split ? IMG_SPLIT : IMG_F32);
+}
+int image_floats(int kind, bool student) {
+    if (kind == IMG_SPLIT) return student ? NETX_S : NETX;
+    return student ? NET_S : NET;
+}
+
 int grid_for(int64_t n, int gs, int cap) {
     const int64_t want = ((n + gs - 1) / gs + PAIRS - 1) / PAIRS;   // one group per pair at least
     return (int)(want < cap ? want : cap);
@@ -1259,10 +1547,11 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
         grid = grid_for(n_obs, a.gs, t->ws_rows);
     }
     t->last_grid = grid;
-    if (t->cfg.student_dtype == RDD_DTYPE_BF16)
-        hipLaunchKernelGGL(rollout_kernel<true>, dim3(grid), dim3(BLOCK), 0, t->stream, a);
-    else
-        hipLaunchKernelGGL(rollout_kernel<false>, dim3(grid), dim3(BLOCK), 0, t->stream, a);
+    const bool bs = t->cfg.student_dtype == RDD_DTYPE_BF16, spl = t->cfg.f32_split != 0;
+    if (bs && spl) hipLaunchKernelGGL((rollout_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
+    else if (bs) hipLaunchKernelGGL((rollout_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
+    else if (spl) hipLaunchKernelGGL((rollout_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
+    else hipLaunchKernelGGL((rollout_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
     return RD_OK;
 }
@@ -1290,7 +1579,7 @@ int launch_reduce(rdd_trainer* t, int reduce, int adam, int accum = 0) {
     a.b2 = t->cfg.beta2;
     a.eps = t->cfg.eps;
     a.simg = t->simg;
-    a.bf16 = t->cfg.student_dtype == RDD_DTYPE_BF16;
+    a.img_kind = student_kind(t);
     hipLaunchKernelGGL(reduce_adam_kernel, dim3(RED_GRID), dim3(RED_BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "reduce_adam_kernel launch");
     return RD_OK;
@@ -1314,7 +1603,8 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
         cfg->n_envs > ((int64_t)1 << 31) || (cfg->loss != RDD_LOSS_MSE && cfg->loss != RDD_LOSS_KL) ||
         (cfg->act_with != RDD_ACT_TEACHER && cfg->act_with != RDD_ACT_STUDENT) || !(cfg->lr > 0) ||
         cfg->grid < 0 || cfg->metrics_len < 0 || (cfg->stagger != 0 && cfg->stagger != 1) ||
-        (cfg->student_dtype != RDD_DTYPE_F32 && cfg->student_dtype != RDD_DTYPE_BF16) || cfg->accum_steps < 0)
+        (cfg->student_dtype != RDD_DTYPE_F32 && cfg->student_dtype != RDD_DTYPE_BF16) || cfg->accum_steps < 0 ||
+        (cfg->f32_split != 0 && cfg->f32_split != 1))
         return rd::set_error(RD_EINVAL, "rdd_create: bad config");
     rd::DeviceGuard g(device);
     RD_HIP(g.err, "rdd_create: hipSetDevice");
@@ -1339,8 +1629,8 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     alloc((void**)&t->state, sizeof(float) * 8 * cfg->n_envs);
     alloc((void**)&t->tnet, sizeof(float) * netf);
     alloc((void**)&t->snet, sizeof(float) * netf);
-    alloc((void**)&t->timg, sizeof(float) * NET);
-    alloc((void**)&t->simg, sizeof(float) * NET_S);
+    alloc((void**)&t->timg, sizeof(float) * image_floats(teacher_kind(t), false));
+    alloc((void**)&t->simg, sizeof(float) * image_floats(student_kind(t), true));
     alloc((void**)&t->m, sizeof(float) * P_TOT);
     alloc((void**)&t->v, sizeof(float) * P_TOT);
     alloc((void**)&t->own_grad, sizeof(float) * P_TOT);
@@ -1378,9 +1668,9 @@ static int set_net(rdd_trainer* t, float* dst, const float* params, const float*
     RD_HIP(hipMemcpyAsync(dst + P_TOT, mu, sizeof(float) * OBD, hipMemcpyDeviceToDevice, t->stream), what);
     RD_HIP(hipMemcpyAsync(dst + P_TOT + OBD, sd, sizeof(float) * OBD, hipMemcpyDeviceToDevice, t->stream), what);
     const bool student = dst == t->snet;
-    const bool bf16 = student && t->cfg.student_dtype == RDD_DTYPE_BF16;
+    const int kind = student ? student_kind(t) : teacher_kind(t);
     hipLaunchKernelGGL(pack_net_kernel, dim3(1), dim3(256), 0, t->stream, dst, student ? t->simg : t->timg,
-                       student ? NET_S : NET, student ? 1 : 0, bf16 ? 1 : 0);
+                       image_floats(kind, student), student ? 1 : 0, kind);
     RD_HIP(hipGetLastError(), what);
     return RD_OK;
 }

@@ -35,7 +35,7 @@ class RddConfig(ctypes.Structure):
     _fields_ = [("n_envs", I64), ("n_envs_global", I64), ("env_base", I64), ("seed", U64),
                 ("loss", I32), ("act_with", I32), ("lr", F32), ("beta1", F32), ("beta2", F32),
                 ("eps", F32), ("grid", I32), ("metrics_len", I32), ("stagger", I32),
-                ("student_dtype", I32), ("accum_steps", I32)]
+                ("student_dtype", I32), ("accum_steps", I32), ("f32_split", I32)]
 
 
 nat.register({
@@ -84,6 +84,7 @@ class DistillConfig:
     stagger: bool = True               # spread episode phases over the batch (reacher_distill.h)
     student_dtype: str = "f32"         # "f32" | "bf16" (BASELINE config 5: bf16 student MLP)
     accum_steps: int = 1               # env steps per optimiser step (1 = the reference)
+    f32_split: bool = False            # f32 hidden layers on bf16 MFMAs via exact 3-piece splits (reacher_distill.h)
 
 
 class DistillTrainer:
@@ -110,7 +111,7 @@ class DistillTrainer:
                       seed=cfg.seed % 2 ** 64, loss=LOSSES[cfg.loss], act_with=ACTORS[cfg.act_with], lr=cfg.lr,
                       beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps, grid=cfg.grid, metrics_len=cfg.metrics_len,
                       stagger=int(bool(cfg.stagger)), student_dtype=DTYPES[cfg.student_dtype],
-                      accum_steps=max(1, int(cfg.accum_steps)))
+                      accum_steps=max(1, int(cfg.accum_steps)), f32_split=int(bool(cfg.f32_split)))
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             nat.check(self._lib.rdd_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,

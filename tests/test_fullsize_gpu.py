@@ -6,6 +6,7 @@ DAgger with the bf16 student) through size-independent properties, on one MI355X
     contract -- within f32 summation order (relative L2 < 1e-5); the shards' env states are
     the full batch's, bitwise (each env's step is independent of the batch split);
   * determinism: the same full-size rollout twice is bitwise identical;
+  * (each with the exact f32 products and with f32_split, the split-bf16 hidden layers)
   * the whole c5 global batch (1,048,576 envs) on one GPU equals its eight 131,072-env
     shards summed (the 8-GPU step), the same way.
 """
@@ -28,10 +29,12 @@ def _rollout(tr):
     return tr.grad().clone(), tr.env_state()
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("wl", ["c4", "c5"])
-def test_full_size_shard_linearity_and_state(wl):
+def test_full_size_shard_linearity_and_state(wl, split):
     kw = dict(loss="mse", act_with="teacher") if wl == "c4" else \
         dict(loss="mse", act_with="student", student_dtype="bf16")
+    kw["f32_split"] = split
     N = 262144 if wl == "c4" else 2 * 131072
     g_full, s_full = _rollout(_tr(n_envs=N, **kw))
     parts = [_rollout(_tr(n_envs_global=N, rank=r, world_size=2, **kw)) for r in range(2)]
@@ -41,9 +44,10 @@ def test_full_size_shard_linearity_and_state(wl):
     assert torch.equal(torch.cat([parts[0][1], parts[1][1]], dim=1), s_full)
 
 
-def test_full_size_rollout_is_deterministic():
-    a = _rollout(_tr(n_envs=262144))
-    b = _rollout(_tr(n_envs=262144))
+@pytest.mark.parametrize("split", [False, True])
+def test_full_size_rollout_is_deterministic(split):
+    a = _rollout(_tr(n_envs=262144, f32_split=split))
+    b = _rollout(_tr(n_envs=262144, f32_split=split))
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
@@ -63,26 +67,29 @@ def test_c5_global_batch_equals_eight_shards():
     assert np.isfinite(g_full.cpu().numpy()).all()
 
 
-def test_c4_full_size_gradient_matches_oracle():
+@pytest.mark.parametrize("split", [False, True])
+def test_c4_full_size_gradient_matches_oracle(split):
     """c4 at its full per-GPU size (262,144 envs, teacher-driven, staggered, MSE): the rollout
     gradient vs the f64 numpy oracle (policy_np, pinned to the reference graph) within
     2e-4 x max|g|, and every env's transition vs the f64 C oracle (tests/test_distill_gpu.py
     _grad_check)."""
     from tests.test_distill_gpu import _grad_check, _trainer
-    tr = _trainer(262144, loss="mse")
+    tr = _trainer(262144, loss="mse", f32_split=split)
     assert tr.cfg.stagger
     _grad_check(tr, "mse", "teacher")
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("loss", ["mse", "kl"])
-def test_c5_shard_gradient_matches_bf16_oracle(loss):
+def test_c5_shard_gradient_matches_bf16_oracle(loss, split):
     """A c5 shard (rank 5 of 8: 131,072 of 1,048,576 envs, DAgger, bf16 student) vs the bf16
     oracle (policy_np.forward_bf16 / backward_bf16, MSE normalised by the global N), with the
     tolerances of tests/test_distill_gpu.py's bf16 tests."""
     from oracle import policy_np as pn
     from tests.test_distill_gpu import _np_params, _obs_from_state
     N, rank = 8 * 131072, 5
-    tr = _tr(n_envs_global=N, rank=rank, world_size=8, loss=loss, act_with="student", student_dtype="bf16")
+    tr = _tr(n_envs_global=N, rank=rank, world_size=8, loss=loss, act_with="student", student_dtype="bf16",
+             f32_split=split)
     assert tr.n_local == 131072 and tr.env_base == rank * 131072
     st0 = tr.env_state().cpu().numpy()
     sp = tr.student_params().cpu().numpy().astype(np.float64)
