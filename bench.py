@@ -50,6 +50,11 @@ WORKLOADS = {
 # FLOPs per env-step by MFMA precision: teacher forward f32; student fwd + bwd f32 or bf16
 FLOP_TEACHER = 2 * (11 * 64 + 64 * 64 + 64 * 2)
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+# f32_split: the K = 64 products (teacher + student layer 2, student dH1) run as six bf16
+# partial products each, so their f32-equivalent peak is the bf16 peak / 6; the rest stays
+# on the f32 MFMA (layer 1, dW2, dW1) or VALU (the 64x2 output layer)
+FLOP_SPLIT_PER_NET_L2 = 2 * 64 * 64
+PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
 
 
 def parse():
@@ -67,9 +72,11 @@ def parse():
                     help="also time K env-steps per optimiser step (SURVEY §8d: K = 50 = one episode); 0 = skip")
     ap.add_argument("--conv-steps", type=int, default=5000,
                     help="convergence leg: optimiser steps allowed to reach student action-MSE < 1e-3; 0 = skip")
-    ap.add_argument("--f32-mode", default="exact", choices=["exact", "split"],
-                    help="f32 hidden-layer products: exact f32 MFMA, or f32 emulated on bf16 MFMAs by exact "
-                         "3-piece operand splits (include/reacher_distill.h f32_split)")
+    ap.add_argument("--f32-mode", default="split", choices=["exact", "split"],
+                    help="f32 hidden-layer products: f32 emulated on bf16 MFMAs by exact 3-piece operand splits "
+                         "(include/reacher_distill.h f32_split; default), or every product on the f32 MFMA")
+    ap.add_argument("--no-exact-leg", action="store_true",
+                    help="skip the secondary timing of the exact-f32-MFMA kernel beside the split one")
     ap.add_argument("--conv-small-envs", type=int, default=256,
                     help="env count of the second convergence run (the env-step reading of the budget)")
     return ap.parse_args()
@@ -178,6 +185,52 @@ def copy_bandwidth(dev, gib=1.0, iters=40):
     e.record()
     torch.cuda.synchronize(dev)
     return 2 * 4 * n * iters / (s.elapsed_time(e) * 1e-3) / 1e9
+
+
+def mixed_peak(sdt, split):
+    """The MFMA-time-weighted peak of the kernel's FLOP mix (f32 MFMA, split-emulated f32,
+    bf16): the roofline the kernel's algorithmic FLOP/s is quoted against."""
+    if sdt == "bf16":   # bf16 student fwd + bwd; teacher f32 (its layer 2 split or not)
+        f_s = FLOP_PER_ENV_STEP - FLOP_TEACHER
+        f_split = FLOP_SPLIT_PER_NET_L2 if split else 0
+        f_f32 = FLOP_TEACHER - f_split
+        return FLOP_PER_ENV_STEP / (f_f32 / PEAK_F32_TFLOPS + f_split / PEAK_SPLIT_TFLOPS + f_s / PEAK_BF16_TFLOPS)
+    if split:           # teacher L2 + student L2 + student dH1
+        f_split = 3 * FLOP_SPLIT_PER_NET_L2
+        return FLOP_PER_ENV_STEP / ((FLOP_PER_ENV_STEP - f_split) / PEAK_F32_TFLOPS + f_split / PEAK_SPLIT_TFLOPS)
+    return PEAK_F32_TFLOPS
+
+
+def time_leg(wl, n, sdt, split, dev, lr, steps, warmup, npass=100):
+    """Secondary timing at world size 1: `steps` fused steps (no events), then the rollout
+    kernel's event-timed launch (the other f32 mode beside the headline's)."""
+    import torch
+
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
+                                      student_dtype=sdt, f32_split=split), device=dev)
+    for _ in range(warmup):
+        tr.step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(npass)]
+    for a, b in evs:
+        a.record()
+        tr.launch(tr.STAGE_ROLLOUT)
+        b.record()
+        tr.launch(tr.STAGE_REDUCE_APPLY)
+    torch.cuda.synchronize(dev)
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    tr.close()
+    achieved = FLOP_PER_ENV_STEP * n / (kern_ms * 1e-3) / 1e12
+    peak = mixed_peak(sdt, split)
+    return {"f32_mode": "split" if split else "exact", "value": n * steps / el, "ms_per_step": el * 1e3 / steps,
+            "launch_us": kern_ms * 1e3, "achieved_tflops": achieved, "peak_tflops": peak, "frac": achieved / peak,
+            "frac_of_f32_mfma_peak": achieved / PEAK_F32_TFLOPS}
 
 
 def cpu_baseline(workload, seconds, threads, n):
@@ -403,16 +456,15 @@ def main():
         value = n * world * args.steps / elapsed
         launch_s = kern_ms * 1e-3
         achieved = FLOP_PER_ENV_STEP * n / launch_s / 1e12
-        peak = PEAK_F32_TFLOPS
-        if sdt == "bf16":   # mixed: the MFMA-time-weighted peak of f32 teacher + bf16 student FLOPs
-            f_s = FLOP_PER_ENV_STEP - FLOP_TEACHER
-            peak = FLOP_PER_ENV_STEP / (FLOP_TEACHER / PEAK_F32_TFLOPS + f_s / PEAK_BF16_TFLOPS)
+        peak = mixed_peak(sdt, split)
         copy_gbs = copy_bandwidth(dev)
         # HBM bytes per rollout launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
         # MI355X_MICROARCH.md §HBM); counters cannot be read from inside this process, so the
         # committed profile of this workload is used and named in traffic_source
         traffic, traffic_src = None, None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}.json")
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}_{args.f32_mode}.json")
+        if not os.path.exists(pmc) and not split:
+            pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}.json")   # round-1 name
         if os.path.exists(pmc):
             with open(pmc) as fh:
                 pj = json.load(fh)
@@ -420,6 +472,9 @@ def main():
             traffic_src = {"file": os.path.relpath(pmc, ROOT), "measured": pj.get("measured", "round 1 (r01i/r01q)"),
                            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes "
                                      "(scripts/profile_workload.sh, scripts/pmc_traffic.py)"}
+        other = None
+        if world == 1 and not args.no_exact_leg:   # the other f32 mode, same workload, for comparison
+            other = time_leg(wl, n, sdt, not split, dev, args.lr, args.steps, args.warmup)
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
@@ -430,13 +485,19 @@ def main():
                        "envs_total": n * world, "student": f"MlpPolicy 2x64 tanh (5060 params, {sdt})",
                        "teacher": "MlpPolicy 2x64 tanh", "loss": wl["loss"], "act_with": wl["act_with"],
                        "optimizer": f"TF1 Adam lr {args.lr}, 1 step per env-step",
-                       "parallelism": f"dp{world}", "collective": collective, "f32_mode": args.f32_mode},
+                       "parallelism": f"dp{world}", "collective": collective, "f32_mode": args.f32_mode,
+                       "f32_arith": ("hidden-layer products (K = 64) f32-emulated on bf16 MFMA: exact 3-piece bf16 "
+                                     "operand split, six partial products, f32 accumulate; the rest exact f32"
+                                     if split else "every product on v_mfma_f32_16x16x4_f32 (exact f32)")},
             # the north star's student action-MSE: after the convergence leg (< 1e-3 within its
             # budget); the timed run's own value (220 steps from init) is kept beside it
             "student_mse": conv["student_mse_final"] if conv is not None else mse,
             "student_mse_timed_run": mse,
             "roofline": {"kernel": "rollout_kernel", "bound": "mfma", "achieved": achieved,
                          "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                         "peak_basis": ("MFMA-time-weighted peak of the FLOP mix: f32 MFMA 157.3 TF; split-emulated "
+                                        "f32 (six bf16 products) 2500/6 TF; bf16 2500 TF"),
+                         "frac_of_f32_mfma_peak": achieved / PEAK_F32_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "flop_per_env_step": FLOP_PER_ENV_STEP, "launch_us": kern_ms * 1e3,
                          "launch_timing": f"HIP events around each of {npass} rollout launches, a pass after "
@@ -445,6 +506,8 @@ def main():
                          "hbm_peak_gbs": PEAK_HBM_GBS, "hbm_copy_gbs_measured": copy_gbs},
             "replicas_identical": replicas,
         }
+        if other is not None:
+            out["other_f32_mode"] = other
         if accum is not None:
             out["accum"] = accum
         if conv is not None:

@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include <stdlib.h>
+#include <string.h>
 
 #include <new>
 
@@ -406,7 +407,8 @@ constexpr int NB_B3 = NB_W3 + HID * ACD;
 constexpr int NB_LS = NB_B3 + ACD;
 constexpr int NB_MU = NB_LS + ACD;
 constexpr int NB_RS = NB_MU + 12;
-static_assert(NB_RS + 12 <= NET_S && NB_B1 % 4 == 0 && NB_W3 % 4 == 0, "bf16 student image");
+constexpr int NETB_S = (NB_RS + 12 + 3) & ~3;   // bf16 student image (floats)
+static_assert(NETB_S <= NET_S && NB_B1 % 4 == 0 && NB_W3 % 4 == 0, "bf16 student image");
 
 __device__ __forceinline__ int kperm(int s, int g, int jj) { return 32 * s + 4 * g + (jj & 3) + 16 * (jj >> 2); }
 
@@ -885,11 +887,13 @@ __device__ __forceinline__ float env_step_group(const RolloutArgs& a, uint32_t C
 
 // LDS floats of the teacher / student images of a rollout instance
 constexpr int img_t(bool SPL) { return SPL ? NETX : NET; }
-constexpr int img_s(bool BS, bool SPL) { return BS ? NET_S : (SPL ? NETX_S : NET_S); }
-static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NET_S + PAIRS * PSCR) * 4 <= 160 * 1024,
+constexpr int img_s(bool BS, bool SPL) { return BS ? NETB_S : (SPL ? NETX_S : NET_S); }
+static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NETB_S + PAIRS * PSCR) * 4 <= 160 * 1024,
               "LDS budget (split images)");
 
-template <bool BS, bool SPL>   // BS: bf16 student (RDD_DTYPE_BF16); SPL: split-bf16 f32 hidden layers
+// BS: bf16 student (RDD_DTYPE_BF16); SPL: split-bf16 f32 hidden layers; CP: the consumer wave
+// steps the envs (else the producer does, from the state it loaded for the observations)
+template <bool BS, bool SPL, bool CP>
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     constexpr int TN = img_t(SPL), SN = img_s(BS, SPL);
     __shared__ __attribute__((aligned(16))) float lds[TN + SN + PAIRS * PSCR];
@@ -948,8 +952,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             if (k >= 2 && !(ok = wait_ge(flags + 2, k - 1, err))) break;
             STAMP(8);
             const int64_t base = grp * gs;
-            const int64_t i = base + lane;
-            const bool lvalid = lane < gs && i < a.n;   // this lane has an env
+            const uint32_t i = (uint32_t)base + (uint32_t)lane;   // n <= 2^31 (rdd_create)
+            const bool lvalid = lane < gs && (int64_t)i < a.n;   // this lane has an env
             float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
             float* act = PS + P_ACT + (k & 1) * GROUP * 2;
             rd::State st{};   // this lane's env, kept in registers for the env.step after the tiles
@@ -957,10 +961,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 float ob[OBD];
                 if (a.obs_in) {   // observation-batch mode: rows given by the caller
 #pragma unroll
-                    for (int q = 0; q < OBD; ++q) ob[q] = lvalid ? a.obs_in[i * OBD + q] : 0.0f;
+                    for (int q = 0; q < OBD; ++q) ob[q] = lvalid ? a.obs_in[(size_t)i * OBD + q] : 0.0f;
                 } else {
                     if (k == 0) st = st0;
-                    else if (lvalid) load_state(a.state, a.n, (uint32_t)i, st);
+                    else if (lvalid) load_state(a.state, a.n, i, st);
                     rd::observe<false>(st, ob);
                 }
                 float* o = obs + lane * SOS;
@@ -1039,15 +1043,18 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             }
             if (!ok) break;
             // ---------------------------------------------------------- env.step (one env per lane)
-            // The producer computed this group's actions itself, so it steps the envs at once:
-            // the consumer's share is then only the gradient tiles, and the pipeline drains
-            // behind the last tile instead of behind the last tile plus a group's physics.
+            // !CP: the producer computed this group's actions itself, so it steps the envs at
+            // once from the state it holds (the consumer's share is then the gradient tiles
+            // only).  CP: the consumer steps them after its last tile of the group, which
+            // balances the roles when the producer's forward is the longer one (split / bf16).
             STAMP(4);
-            if (a.obs_in) {   // observation-batch mode: no env to step
-                if (lvalid) met_n += 1.0f;
-            } else {
-                wave_sync();   // act[] rows were written by the g = 0 lanes of each tile
-                if (lane < gs) met_r += env_step_group(a, C, i, lvalid, act[lane * 2], act[lane * 2 + 1], st, met_n);
+            if constexpr (!CP) {
+                if (a.obs_in) {   // observation-batch mode: no env to step
+                    if (lvalid) met_n += 1.0f;
+                } else {
+                    wave_sync();   // act[] rows were written by the g = 0 lanes of each tile
+                    if (lane < gs) met_r += env_step_group(a, C, i, lvalid, act[lane * 2], act[lane * 2 + 1], st, met_n);
+                }
             }
             STAMP(5);
         }
@@ -1082,7 +1089,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         if (lane == 0) {
             R[P_B3] = gb3a; R[P_B3 + 1] = gb3b; R[P_LS] = gls0; R[P_LS + 1] = gls1;
             R[P_TOT + 1] = met_l; R[P_TOT + 2] = met_m;
-            R[P_TOT] = met_r; R[P_TOT + 3] = met_n;
+            if constexpr (!CP) { R[P_TOT] = met_r; R[P_TOT + 3] = met_n; }
         }
     } else {
         // ============================================================ consumer wave
@@ -1098,6 +1105,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         }
         // student filter of input j for the dW1 A operand (lane-constant)
         const float smu = j < 12 ? LS[SMU + j] : 0.0f, srs = j < 12 ? LS[SRS + j] : 0.0f;
+        float met_r = 0.0f, met_n = 0.0f;   // CP: reward and env count of the envs this wave steps
         uint32_t tiles = 0;
         uint32_t k = 0;
         bool ok = true;
@@ -1105,6 +1113,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             const int64_t base = grp * gs;
             const float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
             const int ntile = (int)min((int64_t)(gs / TILE), (a.n - base + TILE - 1) / TILE);
+            const uint32_t i = (uint32_t)base + (uint32_t)lane;
+            const bool lvalid = lane < gs && (int64_t)i < a.n;
             for (int t = 0; t < ntile; ++t) {
                 STAMP(2);
                 if (!(ok = wait_ge(flags, tiles + 1, err))) break;
@@ -1245,11 +1255,24 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 STAMP(15);
             }
             if (!ok) break;
-            publish(flags + 2, k + 1);   // the obs buffer of group k may be reused
+            if constexpr (CP) {
+                STAMP(4);
+                if (a.obs_in) {
+                    if (lvalid) met_n += 1.0f;
+                } else if (lane < gs) {   // act[] rows: published with the group's tiles
+                    rd::State st{};
+                    if (lvalid) load_state(a.state, a.n, i, st);
+                    const float* act = PS + P_ACT + (k & 1) * GROUP * 2;
+                    met_r += env_step_group(a, C, i, lvalid, act[lane * 2], act[lane * 2 + 1], st, met_n);
+                }
+                STAMP(5);
+            }
+            publish(flags + 2, k + 1);   // the obs/act buffers of group k may be reused
         }
         // ------------------------------------------------------------ this wave's share
 #pragma unroll
         for (int x = 0; x < 4; ++x) gb2[x] = xsum32(xsum16(gb2[x]));   // over the k-groups g
+        if constexpr (CP) { met_r = wave_sum(met_r); met_n = wave_sum(met_n); }
         STAMP(6);
         __syncthreads();   // (one of the two barriers every wave meets) weights/scratch are free
         STAMP(9);
@@ -1269,6 +1292,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         if (g == 0) {
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb) R[RSHIFT + P_B2 + 16 * nb + j] = gb2[nb];
+        }
+        if (CP && lane == 0) {   // the producer's region entries past W2 hold the other metrics
+            R[RSHIFT + P_TOT] = met_r;
+            R[RSHIFT + P_TOT + 3] = met_n;
         }
     }
 
@@ -1513,7 +1540,21 @@ int student_kind(const rdd_trainer* t) {
 }
 int image_floats(int kind, bool student) {
     if (kind == IMG_SPLIT) return student ? NETX_S : NETX;
+    if (kind == IMG_BF16) return NETB_S;
     return student ? NET_S : NET;
+}
+
+// Which wave of a pair steps the envs: the consumer with the bf16 student,
+// whose consumer has little MFMA work (c5: 41.6 vs 42.8 us); the producer otherwise (the
+// consumer's dW2/dW1 accumulators plus the physics spill: c4 split 97.4 vs 93.9 us).
+// RDD_PHYS=producer|consumer overrides (measurement only, scripts/ab_phys.sh).
+bool consumer_physics(bool bs, bool spl) {
+    if (const char* e = getenv("RDD_PHYS")) {
+        if (!strcmp(e, "producer")) return false;
+        if (!strcmp(e, "consumer")) return true;
+    }
+    (void)spl;
+    return bs;
 }
 
 int grid_for(int64_t n, int gs, int cap) {
@@ -1548,10 +1589,13 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     }
     t->last_grid = grid;
     const bool bs = t->cfg.student_dtype == RDD_DTYPE_BF16, spl = t->cfg.f32_split != 0;
-    if (bs && spl) hipLaunchKernelGGL((rollout_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
-    else if (bs) hipLaunchKernelGGL((rollout_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
-    else if (spl) hipLaunchKernelGGL((rollout_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
-    else hipLaunchKernelGGL((rollout_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, t->stream, a);
+    const bool cp = consumer_physics(bs, spl);
+    void (*k)(RolloutArgs) = nullptr;
+    if (cp) k = bs ? (spl ? rollout_kernel<true, true, true> : rollout_kernel<true, false, true>)
+                   : (spl ? rollout_kernel<false, true, true> : rollout_kernel<false, false, true>);
+    else k = bs ? (spl ? rollout_kernel<true, true, false> : rollout_kernel<true, false, false>)
+                : (spl ? rollout_kernel<false, true, false> : rollout_kernel<false, false, false>);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
     return RD_OK;
 }

@@ -22,7 +22,11 @@ NSTAMP = 24
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
-    tr = DistillTrainer(DistillConfig(n_envs=n, seed=0), device="cuda:0")
+    # RD_SPLIT=1: f32_split; RD_WL=c5: DAgger with the bf16 student
+    c5 = os.environ.get("RD_WL") == "c5"
+    tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, f32_split=os.environ.get("RD_SPLIT") == "1",
+                                      act_with="student" if c5 else "teacher", student_dtype="bf16" if c5 else "f32"),
+                        device="cuda:0")
     lib = nat.load()
     lib.rdd_debug_stamps.restype = ctypes.c_int
     lib.rdd_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
