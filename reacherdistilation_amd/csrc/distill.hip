@@ -105,6 +105,37 @@ __device__ __forceinline__ int ridx(int p) { return p < P_B2 ? (p >> 6) * RROW +
 [[maybe_unused]] constexpr int NSTAMP = 24;                      // RD_STAMPS debug slots per wave (scripts/stamps.py)
 constexpr uint32_t SPIN_LIMIT = 1u << 22;       // ~0.1 s of s_sleep: a broken hand-off ends the launch
 
+// ctl words: [0] env steps C (the episode clocks), [1] optimiser steps S (metrics ring),
+// [2] beta1^S, [3] beta2^S (f32 bits); [4..7] the rollout's snapshot of [0..3], which this
+// kernel reads so that block 0 may rewrite [0..3] without racing the other blocks (no
+// atomics, no fences: stream order suffices); [8] hand-off timeout; [12] 1 if the last
+// rollout stepped the envs.
+struct ReduceArgs {
+    const float* ws;
+    int nblk;
+    float* grad;       // [P]
+    float* params;     // student params [P] (in the student net buffer)
+    float* m;
+    float* v;
+    uint32_t* ctl;
+    float* hist;       // [hist_len][4]
+    int hist_len;
+    int reduce, adam, accum;   // accum: grad (and the metrics slot) += this rollout's sums
+    int bump_env, bump_opt;    // advance the env clock (after a reduce) / the optimiser step
+    float lr, b1, b2, eps;
+    float* simg;       // student LDS image, refreshed with every updated parameter
+    int img_kind;      // IMG_F32 / IMG_SPLIT / IMG_BF16
+};
+
+#ifndef RDD_RED_COLS   // diagnostic builds may change the reduce blocking (A/B)
+#define RDD_RED_COLS 64
+#define RDD_RED_ROWS 16
+#endif
+constexpr int RED_COLS = RDD_RED_COLS;              // params per reduce block
+constexpr int RED_ROWS = RDD_RED_ROWS;              // partial rows summed in parallel
+constexpr int RED_BLOCK = RED_COLS * RED_ROWS;
+constexpr int RED_GRID = (P_PAD + RED_COLS - 1) / RED_COLS;
+
 struct RolloutArgs {
     int64_t n, env_base;
     uint64_t seed;
@@ -885,6 +916,67 @@ __device__ __forceinline__ float env_step_group(const RolloutArgs& a, uint32_t C
     return rew;
 }
 
+// The per-column arithmetic of the reduction: RED_ROWS row-threads per parameter, each
+// summing rows row, row + RED_ROWS, ... in four interleaved partial sums; the row-threads'
+// sums are then added in a fixed order (deterministic).
+__device__ __forceinline__ float col_rows(const float* ws, int nblk, int p, int row) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    const float* w = ws + p;
+    int b = row;
+#pragma unroll 4
+    for (; b + 3 * RED_ROWS < nblk; b += 4 * RED_ROWS) {
+        s0 += w[(int64_t)b * P_PAD];
+        s1 += w[(int64_t)(b + RED_ROWS) * P_PAD];
+        s2 += w[(int64_t)(b + 2 * RED_ROWS) * P_PAD];
+        s3 += w[(int64_t)(b + 3 * RED_ROWS) * P_PAD];
+    }
+    for (; b < nblk; b += RED_ROWS) s0 += w[(int64_t)b * P_PAD];
+    return (s0 + s1) + (s2 + s3);
+}
+
+// parameter p: total of its row-threads' sums (part[r * stride], r < RED_ROWS), the gradient /
+// metrics slot, then the TF1 ApplyAdam functor (training_ops.cc) and the image refresh
+__device__ __forceinline__ void col_finish(const ReduceArgs& a, int p, const float* part, int stride, float m_p,
+                                           float v_p, float w_p, uint32_t S, float b1p, float b2p) {
+    float g;
+    if (a.reduce) {
+        float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < RED_ROWS; ++r) q[r & 3] += part[r * stride];
+        g = (q[0] + q[1]) + (q[2] + q[3]);
+        if (p < P_TOT) {
+            if (a.accum) g += a.grad[p];
+            a.grad[p] = g;
+        } else {
+            float* h = a.hist + (int64_t)(S % (uint32_t)a.hist_len) * N_MET + (p - P_TOT);
+            *h = a.accum ? *h + g : g;
+        }
+    } else {
+        g = p < P_TOT ? a.grad[p] : 0.f;
+    }
+    if (a.adam && p < P_TOT) {
+        const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+        float m = m_p, v = v_p;
+        m += (g - m) * (1.0f - a.b1);
+        v += (g * g - v) * (1.0f - a.b2);
+        a.m[p] = m;
+        a.v[p] = v;
+        const float w = w_p - (m * alpha) / (sqrtf(v) + a.eps);
+        a.params[p] = w;
+        pack_param(a.simg, p, w, true, a.img_kind);
+    }
+}
+
+__device__ __forceinline__ void bump_ctl(const ReduceArgs& a, uint32_t C, uint32_t S, float b1p, float b2p,
+                                         uint32_t stepped) {
+    if (a.bump_env) a.ctl[0] = C + stepped;   // env steps: only after a launch that stepped the envs
+    if (a.bump_opt) {
+        a.ctl[1] = S + 1u;                     // optimiser steps
+        a.ctl[2] = __float_as_uint(b1p * a.b1);
+        a.ctl[3] = __float_as_uint(b2p * a.b2);
+    }
+}
+
 // LDS floats of the teacher / student images of a rollout instance
 constexpr int img_t(bool SPL) { return SPL ? NETX : NET; }
 constexpr int img_s(bool BS, bool SPL) { return BS ? NETB_S : (SPL ? NETX_S : NET_S); }
@@ -910,9 +1002,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     RTSTAMP(16);
     STAMP(0);
     const int gs = a.gs;   // envs per group: 64, or 32 / 16 to spread a small batch over more pairs
-    const int64_t ngroups = (a.n + gs - 1) / gs;
-    const int64_t gstride = (int64_t)gridDim.x * PAIRS;
-    const int64_t gfirst = (int64_t)blockIdx.x * PAIRS + pair;
+    // 32-bit group / env indices (n <= 2^31, rdd_create): fewer SGPRs live across the loops
+    const uint32_t n32 = (uint32_t)a.n;
+    const uint32_t ngroups = (n32 + (uint32_t)gs - 1) / (uint32_t)gs;
+    const uint32_t gstride = gridDim.x * PAIRS;
+    const uint32_t gfirst = blockIdx.x * PAIRS + pair;
     // a producer's first group of envs: its state loads are issued before the image copy so
     // that their HBM latency overlaps the prologue
     rd::State st0{};
@@ -947,13 +1041,13 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         uint32_t tiles = 0;
         uint32_t k = 0;
         bool ok = true;
-        for (int64_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
+        for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
             // the consumer is done with group k-2 (same obs/action buffers)
             if (k >= 2 && !(ok = wait_ge(flags + 2, k - 1, err))) break;
             STAMP(8);
-            const int64_t base = grp * gs;
-            const uint32_t i = (uint32_t)base + (uint32_t)lane;   // n <= 2^31 (rdd_create)
-            const bool lvalid = lane < gs && (int64_t)i < a.n;   // this lane has an env
+            const uint32_t base = grp * (uint32_t)gs;
+            const uint32_t i = base + (uint32_t)lane;   // n <= 2^31 (rdd_create)
+            const bool lvalid = lane < gs && i < n32;   // this lane has an env
             float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
             float* act = PS + P_ACT + (k & 1) * GROUP * 2;
             rd::State st{};   // this lane's env, kept in registers for the env.step after the tiles
@@ -974,7 +1068,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             }
             STAMP(11);
             wave_sync();
-            const int ntile = (int)min((int64_t)(gs / TILE), (a.n - base + TILE - 1) / TILE);
+            const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
             for (int t = 0; t < ntile; ++t) {
                 const bool tvalid = base + TILE * t + j < a.n;
                 const float* obt = obs + TILE * t * SOS;
@@ -1109,12 +1203,12 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         uint32_t tiles = 0;
         uint32_t k = 0;
         bool ok = true;
-        for (int64_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
-            const int64_t base = grp * gs;
+        for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
+            const uint32_t base = grp * (uint32_t)gs;
             const float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
-            const int ntile = (int)min((int64_t)(gs / TILE), (a.n - base + TILE - 1) / TILE);
-            const uint32_t i = (uint32_t)base + (uint32_t)lane;
-            const bool lvalid = lane < gs && (int64_t)i < a.n;
+            const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
+            const uint32_t i = base + (uint32_t)lane;
+            const bool lvalid = lane < gs && i < n32;
             for (int t = 0; t < ntile; ++t) {
                 STAMP(2);
                 if (!(ok = wait_ge(flags, tiles + 1, err))) break;
@@ -1315,37 +1409,6 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     RTSTAMP(17);
 }
 
-// ctl words: [0] env steps C (the episode clocks), [1] optimiser steps S (metrics ring),
-// [2] beta1^S, [3] beta2^S (f32 bits); [4..7] the rollout's snapshot of [0..3], which this
-// kernel reads so that block 0 may rewrite [0..3] without racing the other blocks (no
-// atomics, no fences: stream order suffices); [8] hand-off timeout; [12] 1 if the last
-// rollout stepped the envs.
-struct ReduceArgs {
-    const float* ws;
-    int nblk;
-    float* grad;       // [P]
-    float* params;     // student params [P] (in the student net buffer)
-    float* m;
-    float* v;
-    uint32_t* ctl;
-    float* hist;       // [hist_len][4]
-    int hist_len;
-    int reduce, adam, accum;   // accum: grad (and the metrics slot) += this rollout's sums
-    int bump_env, bump_opt;    // advance the env clock (after a reduce) / the optimiser step
-    float lr, b1, b2, eps;
-    float* simg;       // student LDS image, refreshed with every updated parameter
-    int img_kind;      // IMG_F32 / IMG_SPLIT / IMG_BF16
-};
-
-#ifndef RDD_RED_COLS   // diagnostic builds may change the reduce blocking (A/B)
-#define RDD_RED_COLS 64
-#define RDD_RED_ROWS 16
-#endif
-constexpr int RED_COLS = RDD_RED_COLS;              // params per reduce block
-constexpr int RED_ROWS = RDD_RED_ROWS;              // partial rows summed in parallel
-constexpr int RED_BLOCK = RED_COLS * RED_ROWS;
-constexpr int RED_GRID = (P_PAD + RED_COLS - 1) / RED_COLS;
-
 // Sum the rollout's per-workgroup partials (fixed order: deterministic), then TF1 Adam.
 __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
     __shared__ float part[RED_ROWS][RED_COLS];
@@ -1360,61 +1423,10 @@ __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
         v_p = a.v[p];
         w_p = a.params[p];
     }
-    if (a.reduce) {
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        if (p < P_PAD) {
-            const float* w = a.ws + p;
-            int b = row;
-#pragma unroll 4
-            for (; b + 3 * RED_ROWS < a.nblk; b += 4 * RED_ROWS) {
-                s0 += w[(int64_t)b * P_PAD];
-                s1 += w[(int64_t)(b + RED_ROWS) * P_PAD];
-                s2 += w[(int64_t)(b + 2 * RED_ROWS) * P_PAD];
-                s3 += w[(int64_t)(b + 3 * RED_ROWS) * P_PAD];
-            }
-            for (; b < a.nblk; b += RED_ROWS) s0 += w[(int64_t)b * P_PAD];
-        }
-        part[row][col] = (s0 + s1) + (s2 + s3);
-    }
+    if (a.reduce) part[row][col] = p < P_PAD ? col_rows(a.ws, a.nblk, p, row) : 0.f;
     __syncthreads();
-    if (row == 0 && p < P_PAD) {
-        float g;
-        if (a.reduce) {
-            float q[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int r = 0; r < RED_ROWS; ++r) q[r & 3] += part[r][col];
-            g = (q[0] + q[1]) + (q[2] + q[3]);
-            if (p < P_TOT) {
-                if (a.accum) g += a.grad[p];
-                a.grad[p] = g;
-            } else {
-                float* h = a.hist + (int64_t)(S % (uint32_t)a.hist_len) * N_MET + (p - P_TOT);
-                *h = a.accum ? *h + g : g;
-            }
-        } else {
-            g = p < P_TOT ? a.grad[p] : 0.f;
-        }
-        if (a.adam && p < P_TOT) {
-            // TF1 ApplyAdam functor (training_ops.cc)
-            const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-            float m = m_p, v = v_p;
-            m += (g - m) * (1.0f - a.b1);
-            v += (g * g - v) * (1.0f - a.b2);
-            a.m[p] = m;
-            a.v[p] = v;
-            const float w = w_p - (m * alpha) / (sqrtf(v) + a.eps);
-            a.params[p] = w;
-            pack_param(a.simg, p, w, true, a.img_kind);
-        }
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (a.bump_env) a.ctl[0] = C + a.ctl[12];   // env steps: only after a launch that stepped the envs
-        if (a.bump_opt) {
-            a.ctl[1] = S + 1u;                       // optimiser steps
-            a.ctl[2] = __float_as_uint(b1p * a.b1);
-            a.ctl[3] = __float_as_uint(b2p * a.b2);
-        }
-    }
+    if (row == 0 && p < P_PAD) col_finish(a, p, &part[0][col], RED_COLS, m_p, v_p, w_p, S, b1p, b2p);
+    if (blockIdx.x == 0 && threadIdx.x == 0) bump_ctl(a, C, S, b1p, b2p, a.ctl[12]);
 }
 
 __global__ __launch_bounds__(256) void reset_state_kernel(int64_t n, int64_t env_base, uint64_t seed, float* state) {
@@ -1562,6 +1574,31 @@ int grid_for(int64_t n, int gs, int cap) {
     return (int)(want < cap ? want : cap);
 }
 
+ReduceArgs reduce_args(const rdd_trainer* t, int reduce, int adam, int accum) {
+    ReduceArgs a;
+    a.ws = t->ws;
+    a.nblk = t->last_grid;
+    a.grad = t->grad;
+    a.params = t->snet;
+    a.m = t->m;
+    a.v = t->v;
+    a.ctl = t->ctl;
+    a.hist = t->hist;
+    a.hist_len = t->cfg.metrics_len;
+    a.reduce = reduce;
+    a.adam = adam;
+    a.accum = accum;
+    a.bump_env = reduce;
+    a.bump_opt = adam;
+    a.lr = t->cfg.lr;
+    a.b1 = t->cfg.beta1;
+    a.b2 = t->cfg.beta2;
+    a.eps = t->cfg.eps;
+    a.simg = t->simg;
+    a.img_kind = student_kind(t);
+    return a;
+}
+
 int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs = 0, int64_t n_obs_global = 0) {
     RolloutArgs a;
     a.n = obs_in ? n_obs : t->cfg.n_envs;
@@ -1603,27 +1640,7 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
 // reduce: partials -> grad (accum: +=) and advance the env clock; adam: TF1 Adam and
 // advance the optimiser step
 int launch_reduce(rdd_trainer* t, int reduce, int adam, int accum = 0) {
-    ReduceArgs a;
-    a.ws = t->ws;
-    a.nblk = t->last_grid;
-    a.grad = t->grad;
-    a.params = t->snet;
-    a.m = t->m;
-    a.v = t->v;
-    a.ctl = t->ctl;
-    a.hist = t->hist;
-    a.hist_len = t->cfg.metrics_len;
-    a.reduce = reduce;
-    a.adam = adam;
-    a.accum = accum;
-    a.bump_env = reduce;
-    a.bump_opt = adam;
-    a.lr = t->cfg.lr;
-    a.b1 = t->cfg.beta1;
-    a.b2 = t->cfg.beta2;
-    a.eps = t->cfg.eps;
-    a.simg = t->simg;
-    a.img_kind = student_kind(t);
+    const ReduceArgs a = reduce_args(t, reduce, adam, accum);
     hipLaunchKernelGGL(reduce_adam_kernel, dim3(RED_GRID), dim3(RED_BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "reduce_adam_kernel launch");
     return RD_OK;
