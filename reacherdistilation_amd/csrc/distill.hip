@@ -641,8 +641,11 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
     ms1 = xsum32(xsum16(ps1)) + LS[NX_B3 + 1];
 }
 
-// One net's forward with a split image (the teacher beside the bf16 student).
-__device__ __forceinline__ void mlp_forward_split(const float* L, const float* ob, int j, int g, float& m0, float& m1) {
+// One net's forward with a split image (the teacher beside the bf16 student; HO: also
+// return the hidden activations).
+template <bool HO>
+__device__ __forceinline__ void mlp_forward_split_t(const float* L, const float* ob, int j, int g, f32x4 (&H1)[4],
+                                                    f32x4 (&H2)[4], float& m0, float& m1) {
     f32x4 acc[4];
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -654,7 +657,6 @@ __device__ __forceinline__ void mlp_forward_split(const float* L, const float* o
 #pragma unroll
         for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], z, acc[fb]);
     }
-    f32x4 H1[4];
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
@@ -680,6 +682,7 @@ __device__ __forceinline__ void mlp_forward_split(const float* L, const float* o
         f32x4 h2;
 #pragma unroll
         for (int r = 0; r < 4; ++r) h2[r] = tanh_pre(acc[fb][r]);
+        if constexpr (HO) H2[fb] = h2;
         p0 = fmaf(h2[0], wa[0], p0); p1 = fmaf(h2[0], wa[1], p1);
         p0 = fmaf(h2[1], wa[2], p0); p1 = fmaf(h2[1], wa[3], p1);
         p0 = fmaf(h2[2], wb[0], p0); p1 = fmaf(h2[2], wb[1], p1);
@@ -688,6 +691,11 @@ __device__ __forceinline__ void mlp_forward_split(const float* L, const float* o
     m0 = xsum32(xsum16(p0)) + L[NX_B3];
     m1 = xsum32(xsum16(p1)) + L[NX_B3 + 1];
 }
+__device__ __forceinline__ void mlp_forward_split(const float* L, const float* ob, int j, int g, float& m0, float& m1) {
+    f32x4 h1[4], h2[4];
+    mlp_forward_split_t<false>(L, ob, j, g, h1, h2, m0, m1);
+}
+
 
 // ---------------------------------------------------------------- prepacked LDS images
 // The rollout's LDS images (teacher NET floats, student NET_S floats) are kept ready in
@@ -1200,155 +1208,155 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         // student filter of input j for the dW1 A operand (lane-constant)
         const float smu = j < 12 ? LS[SMU + j] : 0.0f, srs = j < 12 ? LS[SRS + j] : 0.0f;
         float met_r = 0.0f, met_n = 0.0f;   // CP: reward and env count of the envs this wave steps
-        uint32_t tiles = 0;
-        uint32_t k = 0;
+        uint32_t tiles = 0;   // tiles taken from the slot (the pair's global tile count)
         bool ok = true;
-        for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
-            const uint32_t base = grp * (uint32_t)gs;
-            const float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
-            const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
-            const uint32_t i = base + (uint32_t)lane;
-            const bool lvalid = lane < gs && i < n32;
-            for (int t = 0; t < ntile; ++t) {
-                STAMP(2);
-                if (!(ok = wait_ge(flags, tiles + 1, err))) break;
-                STAMP(3);
-                // read the whole slot, then free it for the producer's next tile
-                const float* h1t = PS + P_H1T;
-                const float* dzt = PS + P_DZT;
-                f32x4 H1[4], dZ[4], acc[4];
-                if constexpr (BS) {
-                    // dW2 operands over the tile's envs 4g..4g+3 (K = 16 envs), rounded to bf16
-                    s16x4 xa[4], yb[4];
+        // backward of tile t of the group whose observations are at obs: its slot is taken
+        // (tiles + 1 published), read, freed, and its gradients accumulated
+        auto bwd_tile = [&](const float* obs, int t) -> bool {
+            STAMP(2);
+            if (!wait_ge(flags, tiles + 1, err)) return false;
+            STAMP(3);
+            // read the whole slot, then free it for the producer's next tile
+            const float* h1t = PS + P_H1T;
+            const float* dzt = PS + P_DZT;
+            f32x4 H1[4], dZ[4], acc[4];
+            if constexpr (BS) {
+                // dW2 operands over the tile's envs 4g..4g+3 (K = 16 envs), rounded to bf16
+                s16x4 xa[4], yb[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    float xv[4], yv[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        xv[jj] = h1t[(4 * g + jj) * SAS + 16 * b + j];   // H1[16b + j][env 4g+jj]
+                        yv[jj] = dzt[(4 * g + jj) * SAS + 16 * b + j];   // dZ2[16b + j][env 4g+jj]
+                    }
+                    gb2[b] += (yv[0] + yv[1]) + (yv[2] + yv[3]);         // db2 partial (f32)
+                    xa[b] = pack4(xv[0], xv[1], xv[2], xv[3]);
+                    yb[b] = pack4(yv[0], yv[1], yv[2], yv[3]);
+                }
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
+                    dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
+                }
+                publish(flags + 1, ++tiles);
+                STAMP(13);
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma_k16(xa[mb], yb[nb], gW2[mb][nb]);
+                // dH1 = W2 . dZ2: two K = 32 steps, dZ2 in accumulator layout = the B operand
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const bf16x8 db = pack8(dZ[2 * s], dZ[2 * s + 1]);
+#pragma unroll
+                    for (int mb = 0; mb < 4; ++mb)
+                        acc[mb] = mfma_k32(ldbf8(LS + NB_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8), db, acc[mb]);
+                }
+            } else {
+                float x[4][4], y[4][4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
-                        float xv[4], yv[4];
-#pragma unroll
-                        for (int jj = 0; jj < 4; ++jj) {
-                            xv[jj] = h1t[(4 * g + jj) * SAS + 16 * b + j];   // H1[16b + j][env 4g+jj]
-                            yv[jj] = dzt[(4 * g + jj) * SAS + 16 * b + j];   // dZ2[16b + j][env 4g+jj]
-                        }
-                        gb2[b] += (yv[0] + yv[1]) + (yv[2] + yv[3]);         // db2 partial (f32)
-                        xa[b] = pack4(xv[0], xv[1], xv[2], xv[3]);
-                        yb[b] = pack4(yv[0], yv[1], yv[2], yv[3]);
+                        x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
+                        y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
                     }
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
-                        dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
-                    }
-                    publish(flags + 1, ++tiles);
-                    STAMP(13);
+                for (int b = 0; b < 4; ++b) {
+                    H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
+                    dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
+                }
+                publish(flags + 1, ++tiles);
+                STAMP(13);
+                // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) gb2[b] += y[s][b];
 #pragma unroll
                     for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-                        for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma_k16(xa[mb], yb[nb], gW2[mb][nb]);
-                    // dH1 = W2 . dZ2: two K = 32 steps, dZ2 in accumulator layout = the B operand
+                        for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[s][mb], y[s][nb], gW2[mb][nb]);
+                }
+                // dH1 = W2 . dZ2 (A = W2^T image)
 #pragma unroll
-                    for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (SPL) {   // two K = 32 steps on split pieces (dZ2 in accumulator layout = B)
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        const bf16x8 db = pack8(dZ[2 * s], dZ[2 * s + 1]);
+                        __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
+                        bf16x8 dp[3];
+                        split8(dZ[2 * s], dZ[2 * s + 1], dp);
 #pragma unroll
-                        for (int mb = 0; mb < 4; ++mb)
-                            acc[mb] = mfma_k32(ldbf8(LS + NB_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8), db, acc[mb]);
+                        for (int mb = 0; mb < 4; ++mb) {
+                            bf16x8 w[3];
+                            ld_pieces(LS, NX_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8, w);
+                            acc[mb] = mfma_split(w, dp, acc[mb]);
+                        }
                     }
                 } else {
-                    float x[4][4], y[4][4];
+                f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
 #pragma unroll
-                    for (int s = 0; s < 4; ++s)
+                for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-                        for (int b = 0; b < 4; ++b) {
-                            x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
-                            y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
+                    for (int r = 0; r < 4; ++r) {
+                        const f32x4 w = wn;
+                        if (fb * 4 + r < 15) {
+                            const int kn = (r == 3) ? 16 * (fb + 1) + 4 * g : 16 * fb + 4 * g + r + 1;
+                            wn = ld4(LS + N_W2T + kn * HID + 4 * j);
                         }
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
-                        dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
-                    }
-                    publish(flags + 1, ++tiles);
-                    STAMP(13);
-                    // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-#pragma unroll
-                        for (int b = 0; b < 4; ++b) gb2[b] += y[s][b];
-#pragma unroll
-                        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                            for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[s][mb], y[s][nb], gW2[mb][nb]);
-                    }
-                    // dH1 = W2 . dZ2 (A = W2^T image)
-#pragma unroll
-                    for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    if constexpr (SPL) {   // two K = 32 steps on split pieces (dZ2 in accumulator layout = B)
-#pragma unroll
-                        for (int s = 0; s < 2; ++s) {
-                            __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
-                            bf16x8 dp[3];
-                            split8(dZ[2 * s], dZ[2 * s + 1], dp);
-#pragma unroll
-                            for (int mb = 0; mb < 4; ++mb) {
-                                bf16x8 w[3];
-                                ld_pieces(LS, NX_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8, w);
-                                acc[mb] = mfma_split(w, dp, acc[mb]);
-                            }
-                        }
-                    } else {
-                    f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
-#pragma unroll
-                    for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const f32x4 w = wn;
-                            if (fb * 4 + r < 15) {
-                                const int kn = (r == 3) ? 16 * (fb + 1) + 4 * g : 16 * fb + 4 * g + r + 1;
-                                wn = ld4(LS + N_W2T + kn * HID + 4 * j);
-                            }
-#pragma unroll
-                            for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
-                        }
+                        for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
                     }
                 }
-                STAMP(14);
-                float* sa = PS + P_SA;
-#pragma unroll
-                for (int mb = 0; mb < 4; ++mb) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[mb][r] *= fmaf(-H1[mb][r], H1[mb][r], 1.0f);
-                    st4(sa + j * SAS + 16 * mb + 4 * g, acc[mb]);
-                }
-                wave_sync();
-                // dW1 (+ db1 as input row 11) += z^T dZ1; A = student-filtered inputs of env 4s+g
-                const float* obt = obs + TILE * t * SOS;
-                if constexpr (BS) {   // K = the tile's 16 envs (4g + jj), operands rounded to bf16
-                    float zz[4];
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const float xv = obt[(4 * g + jj) * SOS + (j < 12 ? j : 0)];
-                        zz[jj] = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
-                    }
-                    const s16x4 za = pack4(zz[0], zz[1], zz[2], zz[3]);
-#pragma unroll
-                    for (int nb = 0; nb < 4; ++nb) {
-                        const float* c = sa + 16 * nb + j;
-                        gW1[nb] = mfma_k16(za, pack4(c[(4 * g) * SAS], c[(4 * g + 1) * SAS], c[(4 * g + 2) * SAS],
-                                                     c[(4 * g + 3) * SAS]), gW1[nb]);
-                    }
-                } else {
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const float xv = obt[(4 * s + g) * SOS + (j < 12 ? j : 0)];
-                        const float z = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
-#pragma unroll
-                        for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, sa[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
-                    }
-                }
-                wave_sync();   // sa is rewritten by the next tile
-                STAMP(15);
             }
-            if (!ok) break;
+            STAMP(14);
+            float* sa = PS + P_SA;
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[mb][r] *= fmaf(-H1[mb][r], H1[mb][r], 1.0f);
+                st4(sa + j * SAS + 16 * mb + 4 * g, acc[mb]);
+            }
+            wave_sync();
+            // dW1 (+ db1 as input row 11) += z^T dZ1; A = student-filtered inputs of env 4s+g
+            const float* obt = obs + TILE * t * SOS;
+            if constexpr (BS) {   // K = the tile's 16 envs (4g + jj), operands rounded to bf16
+                float zz[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const float xv = obt[(4 * g + jj) * SOS + (j < 12 ? j : 0)];
+                    zz[jj] = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
+                }
+                const s16x4 za = pack4(zz[0], zz[1], zz[2], zz[3]);
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb) {
+                    const float* c = sa + 16 * nb + j;
+                    gW1[nb] = mfma_k16(za, pack4(c[(4 * g) * SAS], c[(4 * g + 1) * SAS], c[(4 * g + 2) * SAS],
+                                                 c[(4 * g + 3) * SAS]), gW1[nb]);
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const float xv = obt[(4 * s + g) * SOS + (j < 12 ? j : 0)];
+                    const float z = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, sa[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
+                }
+            }
+            wave_sync();   // sa is rewritten by the next tile
+            STAMP(15);
+            return true;
+        };
+        // after the last tile of group k (envs base ...): CP steps the envs; the group's
+        // obs/act buffers are then free
+        auto end_group = [&](uint32_t k, uint32_t base) {
+            const uint32_t i = base + (uint32_t)lane;
+            const bool lvalid = lane < gs && i < n32;
             if constexpr (CP) {
                 STAMP(4);
                 if (a.obs_in) {
@@ -1362,6 +1370,15 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 STAMP(5);
             }
             publish(flags + 2, k + 1);   // the obs/act buffers of group k may be reused
+        };
+        uint32_t k = 0;
+        for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
+            const uint32_t base = grp * (uint32_t)gs;
+            const float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
+            const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
+            for (int t = 0; ok && t < ntile; ++t) ok = bwd_tile(obs, t);
+            if (!ok) break;
+            end_group(k, base);
         }
         // ------------------------------------------------------------ this wave's share
 #pragma unroll
@@ -1556,17 +1573,17 @@ int image_floats(int kind, bool student) {
     return student ? NET_S : NET;
 }
 
-// Which wave of a pair steps the envs: the consumer with the bf16 student,
-// whose consumer has little MFMA work (c5: 41.6 vs 42.8 us); the producer otherwise (the
-// consumer's dW2/dW1 accumulators plus the physics spill: c4 split 97.4 vs 93.9 us).
-// RDD_PHYS=producer|consumer overrides (measurement only, scripts/ab_phys.sh).
-bool consumer_physics(bool bs, bool spl) {
+// Which wave of a pair steps the envs.  The producer's forward is the longer
+// role, so the consumer takes the physics when it can overlap the producer's next group:
+// with the bf16 student (c5: 39.7 vs 43.4 us) and from two groups per pair up (c4 split:
+// 92.1 vs 93.6 us); with one group per pair it would run after everything else (c3: 33.6
+// vs 33.2 us).  RDD_PHYS=producer|consumer overrides (measurement only, scripts/ab_phys.sh).
+bool consumer_physics(bool bs, int64_t groups_per_pair) {
     if (const char* e = getenv("RDD_PHYS")) {
         if (!strcmp(e, "producer")) return false;
         if (!strcmp(e, "consumer")) return true;
     }
-    (void)spl;
-    return bs;
+    return bs || groups_per_pair >= 2;
 }
 
 int grid_for(int64_t n, int gs, int cap) {
@@ -1626,7 +1643,8 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     }
     t->last_grid = grid;
     const bool bs = t->cfg.student_dtype == RDD_DTYPE_BF16, spl = t->cfg.f32_split != 0;
-    const bool cp = consumer_physics(bs, spl);
+    const int64_t groups = (a.n + a.gs - 1) / a.gs;
+    const bool cp = consumer_physics(bs, groups / ((int64_t)grid * PAIRS));
     void (*k)(RolloutArgs) = nullptr;
     if (cp) k = bs ? (spl ? rollout_kernel<true, true, true> : rollout_kernel<true, false, true>)
                    : (spl ? rollout_kernel<false, true, true> : rollout_kernel<false, false, true>);
