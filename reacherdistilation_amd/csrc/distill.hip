@@ -87,7 +87,8 @@ constexpr int P_ACT = P_SO + 2 * GROUP * SOS;   // [2][64][2] actions, by group 
 constexpr int P_H1T = P_ACT + 2 * GROUP * 2;    // slot: H1^T [16][SAS]
 constexpr int P_DZT = P_H1T + TILE * SAS;       // slot: dZ2^T [16][SAS]
 constexpr int P_SA = P_DZT + TILE * SAS;        // consumer-private: dZ1^T [16][SAS]
-constexpr int P_FLAGS = P_SA + TILE * SAS;      // u32 [0] tiles published [1] tiles consumed [2] groups done
+constexpr int P_SACT = P_SA + TILE * SAS;       // slot: the tile's actions [16][2] (CP: for the consumer's env step)
+constexpr int P_FLAGS = P_SACT + TILE * 2;      // u32 [0] tiles published [1] tiles consumed [2] groups done
 constexpr int PSCR = P_FLAGS + 4;
 constexpr int LDS_FLOATS = NET + NET_S + PAIRS * PSCR;
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
@@ -177,8 +178,12 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// x + x from the partner row (lane ^ 16) / half (lane ^ 32): v_permlane16/32_swap (VALU,
-// no LDS round trip).  Every lane gets the bitwise-identical sum.
+// x + x from the partner row (lane ^ 16) / half (lane ^ 32).  Every lane gets the
+// bitwise-identical sum (f32 addition commutes).  RD_XSUM_PERMLANE: v_permlane16/32_swap
+// (VALU, no LDS crossbar) -- measured non-deterministic in the split kernel with the
+// consumer-side env step (a value read right after the swap sometimes differs), so the
+// product uses __shfl_xor.
+#ifdef RD_XSUM_PERMLANE
 __device__ __forceinline__ float xsum16(float x) {
     const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(p[0]) + __uint_as_float(p[1]);
@@ -187,6 +192,10 @@ __device__ __forceinline__ float xsum32(float x) {
     const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(p[0]) + __uint_as_float(p[1]);
 }
+#else
+__device__ __forceinline__ float xsum16(float x) { return x + __shfl_xor(x, 16); }
+__device__ __forceinline__ float xsum32(float x) { return x + __shfl_xor(x, 32); }
+#endif
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -1112,8 +1121,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     met_l += lossv;
                     met_m += d0 * d0 + d1 * d1;
                     gb3a += dm0; gb3b += dm1; gls0 += dl0; gls1 += dl1;
-                    act[(TILE * t + j) * 2] = a.act_student ? ms0 : mt0;
-                    act[(TILE * t + j) * 2 + 1] = a.act_student ? ms1 : mt1;
+                    if (!CP) {   // the producer steps the envs itself, after the group's tiles
+                        act[(TILE * t + j) * 2] = a.act_student ? ms0 : mt0;
+                        act[(TILE * t + j) * 2 + 1] = a.act_student ? ms1 : mt1;
+                    }
                 }
                 // dW3 partials (env j of this lane) and dZ2 = (W3 . dmean) * (1 - H2^2)
                 f32x4 dZ[4];
@@ -1140,6 +1151,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 for (int fb = 0; fb < 4; ++fb) {
                     st4(h1t + j * SAS + 16 * fb + 4 * g, H1[fb]);
                     st4(dzt + j * SAS + 16 * fb + 4 * g, dZ[fb]);
+                }
+                if (CP && g == 0) {   // the consumer steps these envs: their actions travel with the slot
+                    PS[P_SACT + 2 * j] = a.act_student ? ms0 : mt0;
+                    PS[P_SACT + 2 * j + 1] = a.act_student ? ms1 : mt1;
                 }
                 publish(flags, ++tiles);
             }
@@ -1212,6 +1227,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         bool ok = true;
         // backward of tile t of the group whose observations are at obs: its slot is taken
         // (tiles + 1 published), read, freed, and its gradients accumulated
+        float act0 = 0.0f, act1 = 0.0f;   // CP: the action of this lane's env (taken from its tile's slot)
         auto bwd_tile = [&](const float* obs, int t) -> bool {
             STAMP(2);
             if (!wait_ge(flags, tiles + 1, err)) return false;
@@ -1239,6 +1255,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 for (int b = 0; b < 4; ++b) {
                     H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
                     dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
+                }
+                if (CP && (lane >> 4) == t) {
+                    act0 = PS[P_SACT + 2 * (lane & 15)];
+                    act1 = PS[P_SACT + 2 * (lane & 15) + 1];
                 }
                 publish(flags + 1, ++tiles);
                 STAMP(13);
@@ -1269,6 +1289,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 for (int b = 0; b < 4; ++b) {
                     H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
                     dZ[b] = ld4(dzt + j * SAS + 16 * b + 4 * g);
+                }
+                if (CP && (lane >> 4) == t) {
+                    act0 = PS[P_SACT + 2 * (lane & 15)];
+                    act1 = PS[P_SACT + 2 * (lane & 15) + 1];
                 }
                 publish(flags + 1, ++tiles);
                 STAMP(13);
@@ -1364,8 +1388,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 } else if (lane < gs) {   // act[] rows: published with the group's tiles
                     rd::State st{};
                     if (lvalid) load_state(a.state, a.n, i, st);
-                    const float* act = PS + P_ACT + (k & 1) * GROUP * 2;
-                    met_r += env_step_group(a, C, i, lvalid, act[lane * 2], act[lane * 2 + 1], st, met_n);
+                    met_r += env_step_group(a, C, i, lvalid, act0, act1, st, met_n);
                 }
                 STAMP(5);
             }
@@ -1573,17 +1596,20 @@ int image_floats(int kind, bool student) {
     return student ? NET_S : NET;
 }
 
-// Which wave of a pair steps the envs.  The producer's forward is the longer
-// role, so the consumer takes the physics when it can overlap the producer's next group:
-// with the bf16 student (c5: 39.7 vs 43.4 us) and from two groups per pair up (c4 split:
-// 92.1 vs 93.6 us); with one group per pair it would run after everything else (c3: 33.6
-// vs 33.2 us).  RDD_PHYS=producer|consumer overrides (measurement only, scripts/ab_phys.sh).
+// Which wave of a pair steps the envs.  The consumer with the bf16 student,
+// whose consumer role is light (c5: 39.7 vs 43.4 us); the producer otherwise.  With the f32
+// student the consumer variant measured faster from two groups per pair up (c4 split 92.1
+// vs 93.6 us) but its env step is NOT reproducible run to run with f32_split (a few hundred
+// envs per launch stepped with wrong actions; scripts/det_check.py), so it is not used; with
+// one group per pair it is slower anyway (c3 33.6 vs 33.2 us).  RDD_PHYS=producer|consumer
+// overrides (measurement only, scripts/ab_phys.sh).
 bool consumer_physics(bool bs, int64_t groups_per_pair) {
     if (const char* e = getenv("RDD_PHYS")) {
         if (!strcmp(e, "producer")) return false;
         if (!strcmp(e, "consumer")) return true;
     }
-    return bs || groups_per_pair >= 2;
+    (void)groups_per_pair;
+    return bs;
 }
 
 int grid_for(int64_t n, int gs, int cap) {
