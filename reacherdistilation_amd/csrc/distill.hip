@@ -178,12 +178,8 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// x + x from the partner row (lane ^ 16) / half (lane ^ 32).  Every lane gets the
-// bitwise-identical sum (f32 addition commutes).  RD_XSUM_PERMLANE: v_permlane16/32_swap
-// (VALU, no LDS crossbar) -- measured non-deterministic in the split kernel with the
-// consumer-side env step (a value read right after the swap sometimes differs), so the
-// product uses __shfl_xor.
-#ifdef RD_XSUM_PERMLANE
+// x + x from the partner row (lane ^ 16) / half (lane ^ 32): v_permlane16/32_swap (VALU,
+// no LDS round trip).  Every lane gets the bitwise-identical sum.
 __device__ __forceinline__ float xsum16(float x) {
     const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(p[0]) + __uint_as_float(p[1]);
@@ -192,10 +188,6 @@ __device__ __forceinline__ float xsum32(float x) {
     const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(p[0]) + __uint_as_float(p[1]);
 }
-#else
-__device__ __forceinline__ float xsum16(float x) { return x + __shfl_xor(x, 16); }
-__device__ __forceinline__ float xsum32(float x) { return x + __shfl_xor(x, 32); }
-#endif
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
