@@ -812,8 +812,9 @@ __global__ __launch_bounds__(256) void pack_net_kernel(const float* net, float* 
 // Both rollout images (contiguous in LDS: teacher then student) with every 16-B load of a
 // thread issued before its first LDS store, so a workgroup keeps ~3.7k loads in flight
 // instead of one round trip per loop iteration.
-template <int V4A, int V4B, int NT>
-__device__ __forceinline__ void copy_images(float* L, const float* ta, const float* sb) {
+// `between` runs while the loads are in flight (the producers' first observations).
+template <int V4A, int V4B, int NT, class F>
+__device__ __forceinline__ void copy_images(float* L, const float* ta, const float* sb, F&& between) {
     constexpr int TOT = V4A + V4B, PER = (TOT + NT - 1) / NT;
     f32x4 r[PER];
 #pragma unroll
@@ -822,6 +823,7 @@ __device__ __forceinline__ void copy_images(float* L, const float* ta, const flo
         if (x < V4A) r[u] = reinterpret_cast<const f32x4*>(ta)[x];
         else if (x < TOT) r[u] = reinterpret_cast<const f32x4*>(sb)[x - V4A];
     }
+    between();
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const int x = threadIdx.x + u * NT;
@@ -1004,7 +1006,6 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     const int j = lane & 15, g = lane >> 4;
     const int pair = wave & (PAIRS - 1);
     const bool producer = wave < PAIRS;
-    float* PS = lds + TN + SN + pair * PSCR;
     uint32_t* flags = reinterpret_cast<uint32_t*>(lds + TN + SN + pair * PSCR + P_FLAGS);
     uint32_t* err = a.ctl + 8;
 
@@ -1022,7 +1023,28 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     if (producer && !a.obs_in && gfirst < ngroups && lane < gs && gfirst * gs + lane < a.n)
         load_state(a.state, a.n, (uint32_t)(gfirst * gs + lane), st0);
     static_assert(NET % 4 == 0 && NET_S % 4 == 0, "16-B images");
-    copy_images<TN / 4, SN / 4, BLOCK>(LT, a.timg, a.simg);   // LS = LT + TN
+    // ... and its observations are formed (into obs buffer 0) while the image loads are in flight
+    float* PS = lds + TN + SN + pair * PSCR;
+    const bool first_obs = producer && gfirst < ngroups;
+    auto group_obs = [&](uint32_t k, uint32_t i, bool lvalid, rd::State& st) {
+        float ob[OBD];
+        if (a.obs_in) {   // observation-batch mode: rows given by the caller
+#pragma unroll
+            for (int q = 0; q < OBD; ++q) ob[q] = lvalid ? a.obs_in[(size_t)i * OBD + q] : 0.0f;
+        } else {
+            rd::observe<false>(st, ob);
+        }
+        float* o = PS + P_SO + (k & 1) * GROUP * SOS + lane * SOS;
+        st4(o, f32x4{ob[0], ob[1], ob[2], ob[3]});
+        st4(o + 4, f32x4{ob[4], ob[5], ob[6], ob[7]});
+        st4(o + 8, f32x4{ob[8], ob[9], ob[10], 1.0f});
+    };
+    copy_images<TN / 4, SN / 4, BLOCK>(LT, a.timg, a.simg, [&] {   // LS = LT + TN
+        if (first_obs) {
+            const uint32_t i = gfirst * (uint32_t)gs + (uint32_t)lane;
+            group_obs(0, i, lane < gs && i < n32, st0);
+        }
+    });
     using SO = Off<BS ? IMG_BF16 : (SPL ? IMG_SPLIT : IMG_F32)>;
     constexpr int SW3 = SO::W3, SMU = SO::MU, SRS = SO::RS;
     if (threadIdx.x < PAIRS * 4)
@@ -1060,20 +1082,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
             float* act = PS + P_ACT + (k & 1) * GROUP * 2;
             rd::State st{};   // this lane's env, kept in registers for the env.step after the tiles
-            {
-                float ob[OBD];
-                if (a.obs_in) {   // observation-batch mode: rows given by the caller
-#pragma unroll
-                    for (int q = 0; q < OBD; ++q) ob[q] = lvalid ? a.obs_in[(size_t)i * OBD + q] : 0.0f;
-                } else {
-                    if (k == 0) st = st0;
-                    else if (lvalid) load_state(a.state, a.n, i, st);
-                    rd::observe<false>(st, ob);
-                }
-                float* o = obs + lane * SOS;
-                st4(o, f32x4{ob[0], ob[1], ob[2], ob[3]});
-                st4(o + 4, f32x4{ob[4], ob[5], ob[6], ob[7]});
-                st4(o + 8, f32x4{ob[8], ob[9], ob[10], 1.0f});
+            if (k == 0) {
+                st = st0;   // observations formed in the prologue
+            } else {
+                if (!a.obs_in && lvalid) load_state(a.state, a.n, i, st);
+                group_obs(k, i, lvalid, st);
             }
             STAMP(11);
             wave_sync();
