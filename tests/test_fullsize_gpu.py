@@ -45,10 +45,15 @@ def test_full_size_shard_linearity_and_state(wl, split):
 
 
 @pytest.mark.parametrize("split", [False, True])
-def test_full_size_rollout_is_deterministic(split):
-    a = _rollout(_tr(n_envs=262144, f32_split=split))
-    b = _rollout(_tr(n_envs=262144, f32_split=split))
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+@pytest.mark.parametrize("wl", ["c4", "c5"])
+def test_full_size_rollout_is_deterministic(wl, split):
+    """Three fresh trainers, one rollout each: gradients and env states bitwise equal (c5 runs
+    the consumer-side env step, c4 the producer-side one)."""
+    kw = dict(n_envs=262144) if wl == "c4" else dict(n_envs=131072, act_with="student", student_dtype="bf16")
+    a = _rollout(_tr(f32_split=split, **kw))
+    for _ in range(2):
+        b = _rollout(_tr(f32_split=split, **kw))
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
 def test_c5_global_batch_equals_eight_shards():
