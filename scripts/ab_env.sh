@@ -1,15 +1,10 @@
 #!/bin/bash
-# A/B timing of environment-variable settings (e.g. RDD_GROUP_ENVS=16) on one GPU: one bench.py
-# line per setting and workload; every run has its own time limit and a failure ends the script.
-# usage: bash scripts/ab_env.sh TAG "workloads" "K=V" ...   ("-" = no setting)
-TAG=$1; WLS=$2; shift 2
+# A/B over an environment variable: ab_env.sh TAG VAR "v1 v2 .." "wl1 wl2 .." REPS [extra bench args]
+# (alternating runs; 1000 timed steps after 300 warm-up; an empty value leaves VAR unset)
+TAG=$1; VAR=$2; VALS=$3; WLS=$4; REPS=$5; shift 5; EXTRA="$@"
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-for wl in $WLS; do
-  for v in "$@"; do
-    tag=$(echo "$v" | tr '=' '_')
-    if [ "$v" = - ]; then envs=(); else envs=("$v"); fi
-    env "${envs[@]}" timeout -k 10 180 python3 bench.py --workload $wl --steps 300 --warmup 30 --accum 0 --no-cpu-baseline \
-      > $OUT/${wl}_$tag.json 2> $OUT/${wl}_$tag.err || { echo "FAIL $wl $v"; tail -5 $OUT/${wl}_$tag.err; exit 1; }
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], sys.argv[3], '%.4g'%d['value'], 'launch_us %.2f'%r['launch_us'], 'step_ms %.4f'%d['ms_per_step'], 'frac %.3f'%r['frac'])" $OUT/${wl}_$tag.json $wl "$v"
-  done
-done
+for rep in $(seq 1 $REPS); do for wl in $WLS; do for v in $VALS; do
+  f=$OUT/${wl}_${v}_$rep.json
+  env $VAR=$v timeout -k 10 120 python bench.py --workload $wl --steps 1000 --warmup 300 --no-cpu-baseline --no-exact-leg --accum 0 --conv-steps 0 $EXTRA > $f 2>$OUT/err.txt || exit 1
+  python3 -c "import json;d=json.load(open('$f'));print('$wl $VAR=$v rep $rep', '%.4g'%d['value'], 'step_us %.2f'%(1e3*d['ms_per_step']), 'launch_us %.2f'%d['roofline']['launch_us'])"
+done; done; done
