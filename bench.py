@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -62,6 +63,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed steps for this long before the W warm-up steps, so that the GPU's "
+                         "clocks have left their idle state (reported as 'settle' in the line)")
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--envs-per-gpu", type=int, default=0)
     ap.add_argument("--lr", type=float, default=1e-4)
@@ -201,7 +205,32 @@ def mixed_peak(sdt, split):
     return PEAK_F32_TFLOPS
 
 
-def time_leg(wl, n, sdt, split, dev, lr, steps, warmup, npass=100):
+def settle(step, dev, ms, world=1):
+    """Untimed steps for about `ms` of wall time: on a GPU that idled (trainer set-up, the
+    convergence leg's teardown) the first ~100 ms of steps run at ramping clocks -- c4 measured
+    93.6 us per step after 2,000 warm-up steps, 98.9 after 20 and 105.4 in a 20-step region
+    after 5.  The count is fixed after a 10-step probe and agreed over the ranks (MAX), since
+    every sharded step is a collective."""
+    import torch
+    if ms <= 0:
+        return {"steps": 0, "ms": 0.0}
+    t0 = time.perf_counter()
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize(dev)
+    probe = max(time.perf_counter() - t0, 1e-6)
+    k = torch.tensor([max(10, int(math.ceil(10 * ms * 1e-3 / probe)))], dtype=torch.int64, device=dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+    k = int(k.item())
+    for _ in range(k - 10):
+        step()
+    torch.cuda.synchronize(dev)
+    return {"steps": k, "ms": (time.perf_counter() - t0) * 1e3}
+
+
+def time_leg(wl, n, sdt, split, dev, lr, steps, warmup, npass=100, settle_ms=0.0):
     """Secondary timing at world size 1: `steps` fused steps (no events), then the rollout
     kernel's event-timed launch (the other f32 mode beside the headline's)."""
     import torch
@@ -209,6 +238,7 @@ def time_leg(wl, n, sdt, split, dev, lr, steps, warmup, npass=100):
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
     tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
                                       student_dtype=sdt, f32_split=split), device=dev)
+    settle(tr.step, dev, settle_ms)
     for _ in range(warmup):
         tr.step()
     torch.cuda.synchronize(dev)
@@ -385,6 +415,7 @@ def main():
             tr.allreduce_grad()
             tr.launch(tr.STAGE_APPLY)
 
+    settled = settle(one_step, dev, args.settle_ms, world)
     for _ in range(args.warmup):
         one_step()
     # the timed region: exactly `steps` steps, nothing else on the stream (no timing events)
@@ -474,10 +505,10 @@ def main():
                                      "(scripts/profile_workload.sh, scripts/pmc_traffic.py)"}
         other = None
         if world == 1 and not args.no_exact_leg:   # the other f32 mode, same workload, for comparison
-            other = time_leg(wl, n, sdt, not split, dev, args.lr, args.steps, args.warmup)
+            other = time_leg(wl, n, sdt, not split, dev, args.lr, args.steps, args.warmup, settle_ms=args.settle_ms)
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "settle": settled, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32" if sdt == "f32" else "bf16 student (f32 accumulate) + f32 teacher",
             "data": "synthetic: Philox(seed 0) Reacher-v2 resets, seeded synthetic teacher (normc, fixture logstd) "
                     "and student (2x64 MlpPolicy)",
