@@ -19,6 +19,8 @@
 // Activations of all steps stay resident in HBM (sized at create for max_windows).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include <new>
 
@@ -69,8 +71,9 @@ __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x))
 // X[r] = [dropout(ob[r]) (11) | prev[r] . Wp + bp (32) | 0]; r = t B + b
 __global__ __launch_bounds__(256) void inputs_kernel(const float* ob, const float* prev, const float* params,
                                                      float* X, int64_t R, int64_t B, float keep_prob, uint64_t seed,
-                                                     int64_t row_base, const uint32_t* ctl) {
+                                                     int64_t row_base, const uint32_t* ctl, uint32_t* bar) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx == 0) { bar[0] = 0u; bar[1] = 0u; }   // the persistent kernels' grid-barrier counters
     if (idx >= R * XLD) return;
     const int64_t r = idx / XLD;
     const int col = (int)(idx % XLD);
@@ -197,6 +200,326 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
     }
 }
 
+// ---------------------------------------------------------------- persistent recurrence
+// Small batches (B <= PR_ROWS windows, e.g. the reference's 20) are launch-latency bound:
+// ~10 us per recurrent step whatever the work.  lstm_fwd_persist_kernel runs ALL T steps of
+// the forward recurrence in one launch and lstm_bptt_persist_kernel all T steps of BPTT.
+// Workgroup w owns units 16w..16w+15 (13 workgroups): its slice of Wr stays in LDS for the
+// whole launch (the forward's 64 gate columns, BPTT's 16 rows of Wr^T), its cell states c
+// (forward) and dc (BPTT) stay in registers, and between steps the workgroups exchange h
+// (forward) or dz (BPTT) through global memory across a grid barrier: an agent-scope arrival
+// counter with release/acquire fences (the workgroups sit on different XCDs, whose L2s are
+// not coherent), a bounded spin that raises a flag instead of hanging (all 13 workgroups are
+// co-resident: one per CU of 256).  The forward's MFMA sequence and cell arithmetic are
+// lstm_rec_fwd_kernel's, so G, c and h are bitwise those of the per-step launches.
+constexpr int PR_ROWS = 32, PR_UNITS = 16, PR_K = 208, PR_GRID = (U + PR_UNITS - 1) / PR_UNITS;
+constexpr int PR_WS = 80;    // forward Wr slice row stride: [k][16 gate + unit], conflict-free B reads
+constexpr int PR_HS = 48;    // A operand row stride: [k][row], conflict-free A reads
+constexpr int PR_ZS = 68;    // gate pre-activation exchange [row][64 + pad]
+constexpr uint32_t PR_SPIN_LIMIT = 1u << 22;
+
+// Hand-off between the workgroups of a persistent launch (cdna_hip_programming.md §6 Guideline
+// 16, the write-through form): the exchanged payload (h, dz) is stored with sc1 buffer stores
+// and drained (s_waitcnt vmcnt(0)) before the workgroup's arrival on an agent-scope counter,
+// and EVERY load of it is an sc1 buffer load -- no L2 writeback or L1 invalidate fences (a
+// release/acquire pair per step measured ~3.5 us).  All other data these kernels read was
+// written before the launch.
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pr_rsrc(const float* base, int64_t floats) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)(floats * 4), 0x00020000);
+}
+__device__ __forceinline__ rdg::f32x4 pr_load4(__amdgpu_buffer_rsrc_t r, int64_t idx) {   // sc1
+    return __builtin_bit_cast(rdg::f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
+}
+__device__ __forceinline__ void pr_store(__amdgpu_buffer_rsrc_t r, int64_t idx, float x) {   // sc1
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)(idx * 4), 0, 16);
+}
+
+// grid barrier #k of a launch (target = k * gridDim.x arrivals on *bar); false on timeout
+__device__ __forceinline__ bool pr_grid_sync(uint32_t* bar, uint32_t target, uint32_t* err) {
+    __shared__ int ok_s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 payload stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int ok = 1;
+        for (uint32_t spins = 0; __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+            if (++spins > PR_SPIN_LIMIT) {
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        ok_s = ok;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
+    return ok_s != 0;
+}
+
+// rows [32][NB*U] of a [B][ld] matrix -> S[b*PR_K + k][row] (row stride PR_HS); every 16-B load
+// of the thread is issued before its first LDS store.  ld4(row, col) loads 4 floats.
+template <int NB, class L>
+__device__ __forceinline__ void stage_rows(int B, float (*S)[PR_HS], L&& ld4) {
+    constexpr int F4 = U / 4, PER = (NB * PR_ROWS * F4 + 255) / 256;
+    rdg::f32x4 v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int f = threadIdx.x + 256 * j, b = f / (PR_ROWS * F4), r = f - b * (PR_ROWS * F4);
+        const int row = r / F4, k4 = r - row * F4;
+        v[j] = (b < NB && row < B) ? ld4(row, b * U + 4 * k4) : rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int f = threadIdx.x + 256 * j, b = f / (PR_ROWS * F4), r = f - b * (PR_ROWS * F4);
+        const int row = r / F4, k4 = r - row * F4;
+        if (b < NB) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S[b * PR_K + 4 * k4 + e][row] = v[j][e];
+        }
+    }
+}
+
+// bar: [0] forward arrivals [1] BPTT arrivals (zeroed by the preceding inputs / loss kernels)
+// [2] timeout flag.  state0: null (zero state) or [c | h] of [B][U] each; Cs/H rows of step 0
+// are written from it for the backward.
+__global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ Z,
+                                                               const float* __restrict__ state0, float* __restrict__ G,
+                                                               float* __restrict__ Cs, float* __restrict__ H, int B,
+                                                               int T, uint32_t* bar, int dbg) {
+    __shared__ __attribute__((aligned(16))) float Ws[PR_K][PR_WS];
+    __shared__ __attribute__((aligned(16))) float Hs[PR_K][PR_HS];
+    __shared__ __attribute__((aligned(16))) float Zl[PR_ROWS][PR_ZS];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
+    const int u0 = blockIdx.x * PR_UNITS;
+    const int rb = wave & 1, ch = wave >> 1;   // rows 16 rb.., gate blocks 2 ch, 2 ch + 1
+    const __amdgpu_buffer_rsrc_t rH = pr_rsrc(H, (int64_t)(T + 1) * B * U);
+    {   // Wr slice: rows k of 4 gate blocks x 16 units (four 16-B pieces each), loads batched
+        constexpr int PER = (PR_K * 16 + 255) / 256;
+        rdg::f32x4 v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int f = tid + 256 * j, k = f >> 4, y = (f >> 2) & 3, c4 = f & 3, u = u0 + 4 * c4;
+            v[j] = (k < U && u < U) ? *reinterpret_cast<const rdg::f32x4*>(Wr + (int64_t)k * G4 + y * U + u)
+                                    : rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int f = tid + 256 * j, k = f >> 4, y = (f >> 2) & 3, c4 = f & 3;
+            if (k < PR_K) *reinterpret_cast<rdg::f32x4*>(&Ws[k][16 * y + 4 * c4]) = v[j];
+        }
+    }
+    for (int x = tid; x < (PR_K - U) * PR_HS; x += 256) Hs[U + x / PR_HS][x % PR_HS] = 0.0f;   // k >= U: never written
+    // this thread's (row, unit) points of the cell: p = tid, tid + 256 over B x 16
+    float cst[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int pt = tid + 256 * q, row = pt >> 4, u = u0 + (pt & 15);
+        cst[q] = 0.0f;
+        if (row < B && u < U) {
+            const int64_t idx = (int64_t)row * U + u;
+            const float c0 = state0 ? state0[idx] : 0.0f, h0 = state0 ? state0[(int64_t)B * U + idx] : 0.0f;
+            cst[q] = c0;
+            Cs[idx] = c0;   // rows of step 0, read by the backward
+            H[idx] = h0;
+        }
+    }
+    // the input half of a step's gate pre-activations (written by the Zx GEMM before this
+    // launch): loaded one step ahead, before the grid barrier, so that only h crosses it
+    float zx[2][4];
+    auto load_zx = [&](int s) {
+        const float* Zs = Z + (int64_t)s * B * G4;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int pt = tid + 256 * q, row = pt >> 4, u = u0 + (pt & 15);
+            const bool ok = row < B && u < U;
+#pragma unroll
+            for (int y = 0; y < 4; ++y) zx[q][y] = ok ? Zs[(int64_t)row * G4 + y * U + u] : 0.0f;
+        }
+    };
+    load_zx(0);
+    for (int s = 0; s < T; ++s) {
+        // A operand: h_s [B][U] -> Hs[k][row] (step 0: the initial state, read directly)
+        const float* hs = s == 0 ? (state0 ? state0 + (int64_t)B * U : nullptr) : H + (int64_t)s * B * U;
+        if (!(dbg & 1)) {
+            if (s > 0) {   // h_s: written in this launch (sc1)
+                const int64_t base = (int64_t)s * B * U;
+                stage_rows<1>(B, Hs, [&](int row, int c) { return pr_load4(rH, base + (int64_t)row * U + c); });
+            } else if (hs) {
+                stage_rows<1>(B, Hs, [&](int row, int c) {
+                    return *reinterpret_cast<const rdg::f32x4*>(hs + (int64_t)row * U + c);
+                });
+            } else {
+                for (int x = tid; x < PR_ROWS * U; x += 256) Hs[x % U][x / U] = 0.0f;
+            }
+        }
+        __syncthreads();
+        // one accumulation chain per gate block and k order as lstm_rec_fwd_kernel (bitwise);
+        // the two blocks' chains interleave
+        rdg::f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        if (!(dbg & 2)) {
+            for (int kt = 0; kt < PR_K / 16; ++kt) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int kk = 16 * kt + 4 * q + gq;
+                    const float a = Hs[kk][16 * rb + i];
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Ws[kk][16 * (2 * ch) + i], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Ws[kk][16 * (2 * ch + 1) + i], acc1, 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // C layout: lane (i, gq) holds rows 4 gq + r, column i
+            Zl[16 * rb + 4 * gq + r][16 * (2 * ch) + i] = acc0[r];
+            Zl[16 * rb + 4 * gq + r][16 * (2 * ch + 1) + i] = acc1[r];
+        }
+        __syncthreads();
+        // TF1 LSTMCell (lstm_rec_fwd_kernel's arithmetic)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int pt = tid + 256 * q, row = pt >> 4, ul = pt & 15, u = u0 + ul;
+            if (row >= B || u >= U) continue;
+            const float* zr = Zl[row];
+            const float gi = sigm((zr[ul] + 0.0f) + zx[q][0]), gj = tanhf((zr[16 + ul] + 0.0f) + zx[q][1]);
+            const float gf = sigm((zr[32 + ul] + 0.0f) + zx[q][2] + 1.0f), go = sigm((zr[48 + ul] + 0.0f) + zx[q][3]);
+            const float c = fmaf(gf, cst[q], gi * gj);
+            cst[q] = c;
+            const int64_t row_g = (int64_t)s * B + row;
+            float* g = G + row_g * G4;
+            g[u] = gi; g[U + u] = gj; g[2 * U + u] = gf; g[3 * U + u] = go;
+            Cs[(row_g + B) * U + u] = c;
+            pr_store(rH, (row_g + B) * U + u, go * tanhf(c));
+        }
+        if (s + 1 < T) {
+            load_zx(s + 1);
+            if (!(dbg & 4) && !pr_grid_sync(bar, (uint32_t)(s + 1) * gridDim.x, bar + 2)) return;
+        }
+    }
+}
+
+// BPTT of all T steps, split-K over the workgroups: per step s (T-1 .. 0) workgroup w
+//  (1) sums dh_next for its 16 units from the 13 partials of step s+1 (fixed order, sc1 loads),
+//  (2) runs the cell backward at its (row, unit) points -> dz_s of its 64 gate columns (to dZ
+//      for the weight gradients, and to LDS),
+//  (3) multiplies those 64 columns by its 64 rows of Wr^T: a partial dh_{s-1} for ALL units,
+//      stored sc1 to its slot of a per-step-parity partial buffer, then the grid barrier.
+// So a step exchanges 13 x 2 KB per workgroup (the units' partials), not all of dz (64 KB).
+constexpr int PB_N = 208;    // units, padded: 13 column blocks of 16
+constexpr int PB_PART = PB_N * PR_ROWS;   // floats of one workgroup's partial [unit][row]
+__global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ dHh,
+                                                                const float* __restrict__ G, const float* __restrict__ Cs,
+                                                                float* __restrict__ dZ, float* __restrict__ part, int B,
+                                                                int T, uint32_t* bar, int dbg) {
+    __shared__ __attribute__((aligned(16))) float Wb[64][PB_N];        // [local gate col y*16+c][unit]
+    __shared__ __attribute__((aligned(16))) float As[64][PR_HS];       // dz_s of the local columns: [col][row]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
+    const int u0 = blockIdx.x * PR_UNITS;
+    const int rb = wave & 1, cb0 = (wave >> 1) * 7, ncb = (wave >> 1) ? 6 : 7;   // rows 16 rb.., column blocks
+    const __amdgpu_buffer_rsrc_t rP = pr_rsrc(part, (int64_t)2 * PR_GRID * PB_PART);
+    {   // Wb[y*16 + c][n] = Wr[n][y*U + u0 + c]: rows n of Wr, 16 consecutive gate columns each
+        constexpr int PER = (PB_N * 16 + 255) / 256;
+        rdg::f32x4 v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int f = tid + 256 * j, n = f >> 4, y = (f >> 2) & 3, c4 = f & 3, u = u0 + 4 * c4;
+            v[j] = (n < U && u < U) ? *reinterpret_cast<const rdg::f32x4*>(Wr + (int64_t)n * G4 + y * U + u)
+                                    : rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int f = tid + 256 * j, n = f >> 4, y = (f >> 2) & 3, c4 = f & 3;
+            if (n < PB_N) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Wb[16 * y + 4 * c4 + e][n] = v[j][e];
+            }
+        }
+    }
+    for (int x = tid; x < 64 * PR_HS; x += 256) As[x / PR_HS][x % PR_HS] = 0.0f;   // rows >= B stay 0
+    // this thread's points: unit c = tid & 15, rows 4 r4 .. 4 r4 + 3 (threads < 128)
+    const int c = tid & 15, r4 = tid >> 4, u = u0 + c;
+    const bool act = tid < 128 && u < U;
+    float dcs[4] = {0.f, 0.f, 0.f, 0.f};
+    float cg[4][4], cct[4], ccp[4], cdh[4];
+    auto load_cell = [&](int s) {   // gates, c_t, c_{t-1}, dh from the head: written before the launch
+        const int64_t rs = (int64_t)s * B;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * r4 + r;
+            const bool ok = act && row < B;
+            const int64_t idx = (rs + row) * U + u;
+            const float* g = G + (rs + row) * G4;
+#pragma unroll
+            for (int y = 0; y < 4; ++y) cg[r][y] = ok ? g[y * U + u] : 0.0f;
+            cct[r] = ok ? Cs[idx + (int64_t)B * U] : 0.0f;
+            ccp[r] = ok ? Cs[idx] : 0.0f;
+            cdh[r] = ok ? dHh[idx] : 0.0f;
+        }
+    };
+    load_cell(T - 1);
+    uint32_t nsync = 0;
+    for (int s = T - 1; s >= 0; --s) {
+        float dhn[4] = {0.f, 0.f, 0.f, 0.f};
+        if (s < T - 1 && act && !(dbg & 1)) {   // (1) dh_next: the 13 partials of step s+1, fixed order
+            const int64_t pb = (int64_t)((s + 1) & 1) * PR_GRID * PB_PART + (int64_t)u * PR_ROWS + 4 * r4;
+            rdg::f32x4 v[PR_GRID];
+#pragma unroll
+            for (int w = 0; w < PR_GRID; ++w) v[w] = pr_load4(rP, pb + (int64_t)w * PB_PART);
+            rdg::f32x4 acc = v[0];
+#pragma unroll
+            for (int w = 1; w < PR_GRID; ++w) acc += v[w];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dhn[r] = acc[r];
+        }
+        // (2) TF1 LSTMCell backward (cell_bwd_kernel's arithmetic)
+        const int64_t rs = (int64_t)s * B;
+        if (act) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * r4 + r;
+                if (row >= B) continue;
+                const float gi = cg[r][0], gj = cg[r][1], gf = cg[r][2], go = cg[r][3];
+                const float dh = s < T - 1 ? cdh[r] + dhn[r] : cdh[r];
+                const float tc = tanhf(cct[r]);
+                const float dcv = fmaf(dh * go, fmaf(-tc, tc, 1.0f), dcs[r]);
+                const float z0 = dcv * gj * gi * (1.0f - gi), z1 = dcv * gi * fmaf(-gj, gj, 1.0f);
+                const float z2 = dcv * ccp[r] * gf * (1.0f - gf), z3 = dh * tc * go * (1.0f - go);
+                float* dz = dZ + (rs + row) * G4;
+                dz[u] = z0; dz[U + u] = z1; dz[2 * U + u] = z2; dz[3 * U + u] = z3;
+                As[c][row] = z0; As[16 + c][row] = z1; As[32 + c][row] = z2; As[48 + c][row] = z3;
+                dcs[r] = dcv * gf;
+            }
+        }
+        if (s == 0) break;
+        load_cell(s - 1);
+        __syncthreads();
+        // (3) partial dh_{s-1}[row][n] over the local columns, for every unit n
+        rdg::f32x4 acc[7];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) acc[q] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!(dbg & 2)) {
+#pragma unroll
+            for (int kq = 0; kq < 16; ++kq) {
+                const int kk = 4 * kq + gq;
+                const float a = As[kk][16 * rb + i];
+#pragma unroll
+                for (int q = 0; q < 7; ++q)
+                    if (q < ncb) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Wb[kk][16 * (cb0 + q) + i], acc[q], 0, 0, 0);
+            }
+        }
+        const int64_t po = (int64_t)(s & 1) * PR_GRID * PB_PART + (int64_t)blockIdx.x * PB_PART;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {   // lane (i, gq): rows 16 rb + 4 gq .. +3 of unit 16 (cb0 + q) + i
+            if (q < ncb)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[q]), rP,
+                                                       (int)((po + (int64_t)(16 * (cb0 + q) + i) * PR_ROWS + 16 * rb + 4 * gq) * 4),
+                                                       0, 16);
+        }
+        __syncthreads();   // As is rewritten by the next step's cell
+        if (!(dbg & 4) && !pr_grid_sync(bar + 1, ++nsync * gridDim.x, bar + 2)) return;
+    }
+}
+
 // BPTT through one cell (dh = dh_head + dh_next; dc carried in place).  The fused backward
 // runs this only for the last step; the others ride in the dh GEMM's epilogue
 // (rdg::EPI_LSTM_BWD, the same arithmetic)
@@ -222,7 +545,8 @@ __global__ __launch_bounds__(256) void cell_bwd_kernel(const float* dh_head, con
 
 // loss (reference loss.py:3-13 / action-MSE) and dY; per-block partials (fixed-order tree)
 __global__ __launch_bounds__(LOSS_BLOCK) void loss_kernel(const float* Y, const float* tgt, float* dY, int64_t R,
-                                                          int loss, float inv_n, float* part) {
+                                                          int loss, float inv_n, float* part, uint32_t* ctl, float* hist,
+                                                          int hist_len) {
     __shared__ float sl[LOSS_BLOCK], ss[LOSS_BLOCK];
     const int64_t r = (int64_t)blockIdx.x * LOSS_BLOCK + threadIdx.x;
     float lv = 0.f, sq = 0.f;
@@ -262,6 +586,17 @@ __global__ __launch_bounds__(LOSS_BLOCK) void loss_kernel(const float* Y, const 
     if (threadIdx.x == 0) {
         part[2 * blockIdx.x] = sl[0];
         part[2 * blockIdx.x + 1] = ss[0];
+    }
+    if (gridDim.x == 1 && hist) {   // one block: metrics_kernel's work here (one launch fewer)
+        if (threadIdx.x == 0) {
+            float* h = hist + (int64_t)(ctl[0] % (uint32_t)hist_len) * N_MET;
+            h[0] = sl[0];
+            h[1] = ss[0];
+            h[2] = (float)R;
+            h[3] = 0.f;
+        }
+        __syncthreads();   // ctl[0] is read before the snapshot below rewrites nothing it needs
+        if (threadIdx.x < 4) ctl[4 + threadIdx.x] = ctl[threadIdx.x];
     }
 }
 
@@ -382,6 +717,8 @@ struct rdl_trainer {
     float *split = nullptr, *colws = nullptr, *lpart = nullptr, *hist = nullptr;
     int64_t colws_floats = 0;
     uint32_t* ctl = nullptr;
+    uint32_t* bar = nullptr;   // persistent kernels: [0] forward / [1] BPTT barrier arrivals, [2] timeout flag
+    float* bpart = nullptr;    // persistent BPTT: per-step-parity partial dh of every workgroup
     int64_t last_B = 0;   // windows of the last forward pass (rdl_final_state)
 };
 
@@ -438,6 +775,20 @@ hipError_t colsum(rdl_trainer* t, const float* src, int64_t M, int N, int64_t ld
 
 #define RDL_CK(call, what) RD_HIP((call), what)
 
+// the persistent recurrence kernels for batches of at most PR_ROWS windows; RDL_PERSIST=0
+// keeps the per-step launches (measurement)
+int pr_dbg() {   // RDL_PR_DBG: bit 0 skip the exchange loads, 1 the MFMAs, 2 the barrier (timing only)
+    const char* e = getenv("RDL_PR_DBG");
+    return e ? atoi(e) : 0;
+}
+
+bool persistent(int64_t B) {
+    if (const char* e = getenv("RDL_PERSIST")) {
+        if (!strcmp(e, "0")) return false;
+    }
+    return B <= PR_ROWS;
+}
+
 // forward over all T steps of B windows.  out_pdflat: where the head's output goes (the
 // internal Y when training).
 int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float* state0, int64_t B, float* out_pdflat,
@@ -448,8 +799,14 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     t->last_B = B;
     hipLaunchKernelGGL(inputs_kernel, dim3((unsigned)((R * XLD + 255) / 256)), dim3(256), 0, t->stream, ob, prev, P,
                        t->X, R, B, train ? t->cfg.keep_prob : 1.0f, t->cfg.seed, t->cfg.row_base,
-                       (const uint32_t*)t->ctl);
+                       (const uint32_t*)t->ctl, t->bar);
     RDL_CK(hipGetLastError(), "rdl inputs_kernel");
+    if (persistent(B)) {   // Zx, then all T recurrent steps in one launch (it writes the step-0 state rows)
+        RDL_CK(mm(t, (int)R, G4, XI, t->X, XLD, 0, P + OFF_WL, G4, 0, t->Z, G4, P + OFF_BL), "rdl gemm Zx");
+        hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
+                           (const float*)t->Z, state0, t->G, t->Cs, t->H, (int)B, T, t->bar, pr_dbg());
+        RDL_CK(hipGetLastError(), "rdl lstm_fwd_persist_kernel");
+    } else {
     if (state0) {
         RDL_CK(hipMemcpyAsync(t->Cs, state0, sizeof(float) * B * U, hipMemcpyDeviceToDevice, t->stream), "rdl state");
         RDL_CK(hipMemcpyAsync(t->H, state0 + B * U, sizeof(float) * B * U, hipMemcpyDeviceToDevice, t->stream),
@@ -478,6 +835,7 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
         RDL_CK(hipGetLastError(), "rdl lstm_rec_fwd_kernel");
 #endif
     }
+    }
     // head over all T x B rows (student_nn.py:42-46)
     const float* Hc = t->H + B * U;
     RDL_CK(mm(t, (int)R, H1, U, Hc, U, 0, P + OFF_W1, H1, 0, t->A1, L1, P + OFF_B1, rdg::EPI_TANH), "rdl head1");
@@ -495,12 +853,16 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     const float* P = t->params;
     float* g = t->grad;
     const int lblk = (int)((R + LOSS_BLOCK - 1) / LOSS_BLOCK);
+    const bool fold = lblk == 1;   // a single loss block writes the metrics itself
     hipLaunchKernelGGL(loss_kernel, dim3(lblk), dim3(LOSS_BLOCK), 0, t->stream, (const float*)t->Y, tgt, t->dY, R,
-                       t->cfg.loss, 1.0f / ((float)T * (float)B_global), t->lpart);
+                       t->cfg.loss, 1.0f / ((float)T * (float)B_global), t->lpart, t->ctl, fold ? t->hist : nullptr,
+                       t->cfg.metrics_len);
     RDL_CK(hipGetLastError(), "rdl loss_kernel");
-    hipLaunchKernelGGL(metrics_kernel, dim3(1), dim3(256), 0, t->stream, (const float*)t->lpart, lblk, (float)R,
-                       t->ctl, t->hist, t->cfg.metrics_len);
-    RDL_CK(hipGetLastError(), "rdl metrics_kernel");
+    if (!fold) {
+        hipLaunchKernelGGL(metrics_kernel, dim3(1), dim3(256), 0, t->stream, (const float*)t->lpart, lblk, (float)R,
+                           t->ctl, t->hist, t->cfg.metrics_len);
+        RDL_CK(hipGetLastError(), "rdl metrics_kernel");
+    }
     // head backward (weight gradients over all rows; data gradients with the tanh derivative fused)
     // per layer, [dW; db] (weight gradient, ones column) beside the data gradient with tanh'
     RDL_CK(mm2(t, ga(H4 + 1, 4, Ri, t->A4, L4, 1, t->dY, 4, 0, g + OFF_W5, 4),
@@ -522,6 +884,12 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     RDL_CK(colsum(t, t->D64b, R, H1, H1, g + OFF_B1), "rdl db1");
     // BPTT (the gate buffer Z is reused for dz: the forward keeps activations in G)
     float* dZl = t->Z;
+    if (persistent(B)) {
+        hipLaunchKernelGGL(lstm_bptt_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
+                           (const float*)t->dHh, (const float*)t->G, (const float*)t->Cs, dZl, t->bpart, (int)B, T,
+                           t->bar, pr_dbg());
+        RDL_CK(hipGetLastError(), "rdl lstm_bptt_persist_kernel");
+    } else {
     RDL_CK(hipMemsetAsync(t->dc, 0, sizeof(float) * B * U, t->stream), "rdl bptt");
     const unsigned cb = (unsigned)((B * U + 255) / 256);
 #ifdef RD_LSTM_UNFUSED   // diagnostic build: dh GEMM and cell backward as two launches per step
@@ -559,6 +927,7 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
         RDL_CK(rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus), "rdl gemm dh + cell");
     }
 #endif
+    }
     // LSTM weights: dWl = [x | h_prev]^T dz over all rows; dbl; then dp -> dWp, dbp
     RDL_CK(mm2(t, ga(XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4),
                ga(U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4)),
@@ -638,6 +1007,9 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     alloc(&t->lpart, 2 * ((R + LOSS_BLOCK - 1) / LOSS_BLOCK));
     alloc(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
     if (e == hipSuccess) e = hipMalloc((void**)&t->ctl, sizeof(uint32_t) * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&t->bar, sizeof(uint32_t) * 4);
+    alloc(&t->bpart, (int64_t)2 * PR_GRID * PB_PART);
+    if (e == hipSuccess) e = hipMemsetAsync(t->bar, 0, sizeof(uint32_t) * 4, t->stream);
     t->grad = t->own_grad;
     if (e != hipSuccess) {
         rdl_destroy(t);
@@ -667,10 +1039,11 @@ int rdl_destroy(rdl_trainer* t) {
     rd::DeviceGuard dg(t->device);
     float* bufs[] = {t->params, t->m, t->v, t->own_grad, t->X, t->H, t->Cs, t->Z, t->G, t->A1, t->A2, t->A3, t->A4,
                      t->Y, t->dY, t->D32, t->D64a, t->D128, t->D64b, t->dHh, t->dP, t->dhn, t->dc, t->split,
-                     t->colws, t->lpart, t->hist};
+                     t->colws, t->lpart, t->hist, t->bpart};
     for (float* p : bufs)
         if (p) (void)hipFree(p);
     if (t->ctl) (void)hipFree(t->ctl);
+    if (t->bar) (void)hipFree(t->bar);
     delete t;
     return RD_OK;
 }

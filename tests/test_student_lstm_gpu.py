@@ -281,3 +281,29 @@ def test_driver_restores_and_saves_the_student(tmp_path):
     saved = st.params().clone()
     st2, _, _ = lstm_train.train(train=False, restore=True, student_path=path, log=msgs.append)
     assert torch.equal(st2.params(), saved)
+
+
+@pytest.mark.parametrize("T,B,with_state", [(10, 20, False), (10, 32, True), (1, 7, True), (3, 1, False)])
+def test_persistent_recurrence_matches_per_step_launches(monkeypatch, T, B, with_state):
+    """B <= 32: the whole forward recurrence and the whole BPTT each run as one persistent
+    launch (lstm_fwd_persist_kernel / lstm_bptt_persist_kernel).  Forward: bitwise the per-step
+    kernels (same MFMA sequence and cell arithmetic); gradient: the dh sums over the 800 gate
+    columns run in another order, so within 1e-5 of max|g| (and both within the oracle bound)."""
+    ob, prev, t = _batch(T, B, 11 + B)
+    st = np.random.RandomState(4).uniform(-.5, .5, (2, B, 200)).astype(np.float32) if with_state else None
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RDL_PERSIST", mode)
+        tr = _trainer(T, B, "kl")
+        y, fin = tr.forward(_t(ob), _t(prev), None if st is None else _t(st))
+        g = tr.rollout(_t(ob), _t(prev), _t(t), None if st is None else _t(st)).cpu().numpy()
+        out[mode] = (y.cpu().numpy(), fin[0].cpu().numpy(), fin[1].cpu().numpy(), g, tr.params().cpu().numpy())
+        tr.close()
+    for a, b in zip(out["1"][:3], out["0"][:3]):
+        assert np.array_equal(a, b)
+    g1, g0 = out["1"][3], out["0"][3]
+    assert np.abs(g1 - g0).max() <= 1e-5 * np.abs(g0).max()
+    p = out["1"][4]
+    fw = ln.forward(p, ob, prev, st)
+    _, d, _ = ln.loss_and_dout(fw["pdflat"], t, "kl", T * B)
+    _grad_check(g1, ln.backward(p, fw, d))
