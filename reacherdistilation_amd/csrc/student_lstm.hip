@@ -409,10 +409,13 @@ constexpr int PB_N = 208;    // units, padded: 13 column blocks of 16
 constexpr int PB_PART = PB_N * PR_ROWS;   // floats of one workgroup's partial [unit][row]
 __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ dHh,
                                                                 const float* __restrict__ G, const float* __restrict__ Cs,
-                                                                float* __restrict__ dZ, float* __restrict__ part, int B,
-                                                                int T, uint32_t* bar, int dbg) {
+                                                                float* __restrict__ dZ, float* __restrict__ part,
+                                                                float* __restrict__ dbl, const float* __restrict__ prev,
+                                                                float* __restrict__ Q, int B, int T, uint32_t* bar,
+                                                                int dbg) {
     __shared__ __attribute__((aligned(16))) float Wb[64][PB_N];        // [local gate col y*16+c][unit]
     __shared__ __attribute__((aligned(16))) float As[64][PR_HS];       // dz_s of the local columns: [col][row]
+    static_assert(PR_HS >= 40, "As also holds the 5 x 8 row-group sums at the end");
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int u0 = blockIdx.x * PR_UNITS;
     const int rb = wave & 1, cb0 = (wave >> 1) * 7, ncb = (wave >> 1) ? 6 : 7;   // rows 16 rb.., column blocks
@@ -440,7 +443,9 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
     const int c = tid & 15, r4 = tid >> 4, u = u0 + c;
     const bool act = tid < 128 && u < U;
     float dcs[4] = {0.f, 0.f, 0.f, 0.f};
-    float cg[4][4], cct[4], ccp[4], cdh[4];
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};   // dbl: this thread's rows, all steps, per gate
+    float qsum[4][4] = {};                    // Q = prev^T dz: [prev component][gate]
+    float cg[4][4], cct[4], ccp[4], cdh[4], cpv[4][4];
     auto load_cell = [&](int s) {   // gates, c_t, c_{t-1}, dh from the head: written before the launch
         const int64_t rs = (int64_t)s * B;
 #pragma unroll
@@ -454,6 +459,8 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
             cct[r] = ok ? Cs[idx + (int64_t)B * U] : 0.0f;
             ccp[r] = ok ? Cs[idx] : 0.0f;
             cdh[r] = ok ? dHh[idx] : 0.0f;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) cpv[r][a] = ok ? prev[(rs + row) * 4 + a] : 0.0f;
         }
     };
     load_cell(T - 1);
@@ -487,6 +494,14 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
                 float* dz = dZ + (rs + row) * G4;
                 dz[u] = z0; dz[U + u] = z1; dz[2 * U + u] = z2; dz[3 * U + u] = z3;
                 As[c][row] = z0; As[16 + c][row] = z1; As[32 + c][row] = z2; As[48 + c][row] = z3;
+                bsum[0] += z0; bsum[1] += z1; bsum[2] += z2; bsum[3] += z3;
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    qsum[a][0] = fmaf(cpv[r][a], z0, qsum[a][0]);
+                    qsum[a][1] = fmaf(cpv[r][a], z1, qsum[a][1]);
+                    qsum[a][2] = fmaf(cpv[r][a], z2, qsum[a][2]);
+                    qsum[a][3] = fmaf(cpv[r][a], z3, qsum[a][3]);
+                }
                 dcs[r] = dcv * gf;
             }
         }
@@ -518,6 +533,249 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
         __syncthreads();   // As is rewritten by the next step's cell
         if (!(dbg & 4) && !pr_grid_sync(bar + 1, ++nsync * gridDim.x, bar + 2)) return;
     }
+    // dbl (the gate bias gradient) and Q = prev^T dz of the local columns: the 8 row groups'
+    // sums, in order (As[col][8 j + r4] holds sum j of row group r4)
+    __syncthreads();
+    if (tid < 128) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            As[16 * y + c][r4] = bsum[y];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) As[16 * y + c][8 * (a + 1) + r4] = qsum[a][y];
+        }
+    }
+    __syncthreads();
+    for (int o = tid; o < 64 * 5; o += 256) {
+        const int col = o & 63, j = o >> 6, y = col >> 4, uu = u0 + (col & 15);
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v += As[col][8 * j + k];
+        if (uu < U) {
+            if (j == 0) dbl[y * U + uu] = v;
+            else Q[(j - 1) * G4 + y * U + uu] = v;
+        }
+    }
+}
+
+// dWp = Q . Wl[11:43]^T and dbp = Wl[11:43] . dbl: the input-side dense32 layer's gradients
+// (student_nn.py:26) from the BPTT kernel's gate sums, without materialising dP = dZ . Wl^T
+// (the same sums in another order: sum over the rows first, then over the 800 gate columns)
+__global__ __launch_bounds__(256) void dense32_grad_kernel(const float* __restrict__ P, const float* __restrict__ Q,
+                                                           float* __restrict__ g) {
+    // block o: 0..127 dWp[a][c] (a = o / 32), 128..159 dbp[c]; a fixed-order tree over 256 threads
+    __shared__ float red[256];
+    const int o = blockIdx.x, c = o & 31;
+    const float* w = P + OFF_WL + (int64_t)(11 + c) * G4;
+    const float* q = o < 128 ? Q + (o >> 5) * G4 : g + OFF_BL;
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < (G4 + 255) / 256; ++j) {
+        const int k = threadIdx.x + 256 * j;
+        if (k < G4) v = fmaf(w[k], q[k], v);
+    }
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) g[(o < 128 ? OFF_WP : OFF_BP - 128) + o] = red[0];
+}
+
+// ---------------------------------------------------------------- fused head (small batches)
+// The head 200-64-128-64-32-4 (student_nn.py:42-46) over a few hundred rows is five launches of
+// ~10 us each, none of them busy.  head_fwd_kernel runs all five layers for 16 rows per
+// workgroup: activations stay in LDS between layers, weights stream from L2 as the B
+// operands, and every layer's output is also stored (A1..A4 for the backward, Y).  Same MFMA
+// k order and epilogue (acc + b, tanhf) as the unsplit rd_gemm launches it replaces.
+constexpr int HF_ROWS = 16, HF_MAX_ROWS = 2048;
+template <int K, int N, bool TANH, int LI, int LO>
+__device__ __forceinline__ void head_layer(const float (*in)[LI], float (*out)[LO], const float* __restrict__ W,
+                                           const float* __restrict__ b, float* __restrict__ gout, int ldg,
+                                           int64_t row0, int64_t R) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
+    constexpr int NB = (N + 15) / 16;
+#pragma unroll
+    for (int it = 0; it < (NB + 3) / 4; ++it) {   // unrolled: every weight load of the layer in flight at once
+        const int cb = wave + 4 * it;
+        if (cb >= NB) break;
+        const int col = 16 * cb + i;
+        const bool cv = col < N;
+        rdg::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kq = 0; kq < K / 4; ++kq) {
+            const int k = 4 * kq + gq;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(in[i][k], cv ? W[k * N + col] : 0.0f, acc, 0, 0, 0);
+        }
+        const float bv = cv ? b[col] : 0.0f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * gq + r;
+            float v = acc[r] + bv;
+            if (TANH) v = tanhf(v);
+            if (cv) {
+                out[row][col] = v;
+                if (row0 + row < R) gout[(row0 + row) * ldg + col] = v;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// rows row0.. of a [R][ld] matrix, columns 0..COLS-1 -> dst[16][LDD] (zero past R): every
+// load of the thread issued before its first LDS store (one round trip, not one per element)
+template <int COLS, int LDD>
+__device__ __forceinline__ void head_stage(const float* __restrict__ src, int ld, int64_t row0, int64_t R,
+                                           float (*dst)[LDD]) {
+    constexpr int PER = (HF_ROWS * COLS + 255) / 256;
+    float v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int x = threadIdx.x + 256 * j, row = x / COLS, c = x - row * COLS;
+        v[j] = (x < HF_ROWS * COLS && row0 + row < R) ? src[(row0 + row) * ld + c] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int x = threadIdx.x + 256 * j, row = x / COLS, c = x - row * COLS;
+        if (x < HF_ROWS * COLS) dst[row][c] = v[j];
+    }
+}
+
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P,
+                                                       float* A1, float* A2, float* A3, float* A4, float* Y, int64_t R) {
+    __shared__ __attribute__((aligned(16))) float X0[HF_ROWS][U + 4];
+    __shared__ __attribute__((aligned(16))) float X1[HF_ROWS][L1];
+    __shared__ __attribute__((aligned(16))) float X2[HF_ROWS][L2];
+    __shared__ __attribute__((aligned(16))) float X3[HF_ROWS][L3];
+    __shared__ __attribute__((aligned(16))) float X4[HF_ROWS][L4];
+    __shared__ __attribute__((aligned(16))) float X5[HF_ROWS][8];
+    const int64_t row0 = (int64_t)blockIdx.x * HF_ROWS;
+    head_stage<U, U + 4>(Hc, U, row0, R, X0);
+    __syncthreads();
+    head_layer<U, H1, true>(X0, X1, P + OFF_W1, P + OFF_B1, A1, L1, row0, R);
+    head_layer<H1, H2, true>(X1, X2, P + OFF_W2, P + OFF_B2, A2, L2, row0, R);
+    head_layer<H2, H3, true>(X2, X3, P + OFF_W3, P + OFF_B3, A3, L3, row0, R);
+    head_layer<H3, H4, true>(X3, X4, P + OFF_W4, P + OFF_B4, A4, L4, row0, R);
+    head_layer<H4, 4, false>(X4, X5, P + OFF_W5, P + OFF_B5, Y, 4, row0, R);
+}
+
+// Head backward for the same small batches: per 16-row workgroup the data gradients down the
+// head (tanh' of the stored activations fused, as the EPI_DTANH GEMMs), dh_head for BPTT,
+// and the five [dW; db] weight-gradient partials over its rows (the stored activations carry
+// the ones column; Hc gets one in LDS) as one partial row of the flat [W1 b1 ... W5 b5] range;
+// head_wgrad_reduce_kernel sums the rows in a fixed order.  Two launches instead of six.
+constexpr int HB_PART = P_LSTM - OFF_W1;   // 31,652 floats: [W1;b1][W2;b2][W3;b3][W4;b4][W5;b5]
+// dIn[16][NI] = (dOut[16][KO] . W^T) (* (1 - act^2) when DT); W is [NI][KO] (layer input x output)
+template <int KO, int NI, bool DT, int LD, int LI, int LA>
+__device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)[LI], const float (*act)[LA],
+                                           const float* __restrict__ W, float* gout, int ldg, int64_t row0, int64_t R) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
+    constexpr int NB = (NI + 15) / 16;
+#pragma unroll
+    for (int it = 0; it < (NB + 3) / 4; ++it) {   // unrolled: every weight load of the layer in flight at once
+        const int cb = wave + 4 * it;
+        if (cb >= NB) break;
+        const int col = 16 * cb + i;
+        const bool cv = col < NI;
+        rdg::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kq = 0; kq < KO / 4; ++kq) {
+            const int k = 4 * kq + gq;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dout[i][k], cv ? W[col * KO + k] : 0.0f, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * gq + r;
+            float v = acc[r];
+            if (DT) {
+                const float a = act[row][col < NI ? col : 0];
+                v *= fmaf(-a, a, 1.0f);
+            }
+            if (cv) {
+                if (din) din[row][col] = v;
+                if (gout && row0 + row < R) gout[(row0 + row) * ldg + col] = v;
+            }
+        }
+    }
+}
+// part[m][n] = sum over the 16 rows of act[row][m] d[row][n], m < M (the last input row is the
+// ones column: the bias gradient), n < N
+template <int M, int N, int LA, int LD>
+__device__ __forceinline__ void head_wgrad(const float (*act)[LA], const float (*d)[LD], float* __restrict__ part) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
+    constexpr int MB = (M + 15) / 16, NB = (N + 15) / 16;
+    for (int t = wave; t < MB * NB; t += 4) {
+        const int m0 = 16 * (t / NB), n0 = 16 * (t % NB);
+        const int mc = m0 + i < M ? m0 + i : M - 1, nc = n0 + i < N ? n0 + i : N - 1;
+        rdg::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = 4 * s + gq;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(act[k][mc], d[k][nc], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * gq + r, n = n0 + i;
+            if (m < M && n < N) part[m * N + n] = acc[r];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P,
+                                                       const float* __restrict__ A1, const float* __restrict__ A2,
+                                                       const float* __restrict__ A3, const float* __restrict__ A4,
+                                                       const float* __restrict__ dY, float* __restrict__ dHh,
+                                                       float* __restrict__ part, int64_t R) {
+    __shared__ __attribute__((aligned(16))) float X0[HF_ROWS][U + 4];   // Hc, ones column U
+    __shared__ __attribute__((aligned(16))) float X1[HF_ROWS][L1];
+    __shared__ __attribute__((aligned(16))) float X2[HF_ROWS][L2];
+    __shared__ __attribute__((aligned(16))) float X3[HF_ROWS][L3];
+    __shared__ __attribute__((aligned(16))) float X4[HF_ROWS][L4];
+    __shared__ __attribute__((aligned(16))) float D5[HF_ROWS][8];
+    __shared__ __attribute__((aligned(16))) float D4[HF_ROWS][L4];
+    __shared__ __attribute__((aligned(16))) float D3[HF_ROWS][L3];
+    __shared__ __attribute__((aligned(16))) float D2[HF_ROWS][L2];
+    __shared__ __attribute__((aligned(16))) float D1[HF_ROWS][L1];
+    const int64_t row0 = (int64_t)blockIdx.x * HF_ROWS;
+    // rows past R are zero (activations and gradients): they add nothing to the partials
+    head_stage<U, U + 4>(Hc, U, row0, R, X0);
+    head_stage<H1 + 1, L1>(A1, L1, row0, R, X1);   // with the ones column
+    head_stage<H2 + 1, L2>(A2, L2, row0, R, X2);
+    head_stage<H3 + 1, L3>(A3, L3, row0, R, X3);
+    head_stage<H4 + 1, L4>(A4, L4, row0, R, X4);
+    head_stage<4, 8>(dY, 4, row0, R, D5);
+    if (threadIdx.x < HF_ROWS) X0[threadIdx.x][U] = row0 + threadIdx.x < R ? 1.0f : 0.0f;
+    __syncthreads();
+    head_dgrad<4, H4, true>(D5, D4, X4, P + OFF_W5, nullptr, 0, row0, R);
+    __syncthreads();
+    head_dgrad<H4, H3, true>(D4, D3, X3, P + OFF_W4, nullptr, 0, row0, R);
+    __syncthreads();
+    head_dgrad<H3, H2, true>(D3, D2, X2, P + OFF_W3, nullptr, 0, row0, R);
+    __syncthreads();
+    head_dgrad<H2, H1, true>(D2, D1, X1, P + OFF_W2, nullptr, 0, row0, R);
+    __syncthreads();
+    head_dgrad<H1, U, false>(D1, (float(*)[U + 4]) nullptr, X0, P + OFF_W1, dHh, U, row0, R);   // dh_head
+    float* pw = part + (int64_t)blockIdx.x * HB_PART;
+    head_wgrad<U + 1, H1>(X0, D1, pw);                                   // [dW1; db1]
+    head_wgrad<H1 + 1, H2>(X1, D2, pw + (OFF_W2 - OFF_W1));              // [dW2; db2]
+    head_wgrad<H2 + 1, H3>(X2, D3, pw + (OFF_W3 - OFF_W1));
+    head_wgrad<H3 + 1, H4>(X3, D4, pw + (OFF_W4 - OFF_W1));
+    head_wgrad<H4 + 1, 4>(X4, D5, pw + (OFF_W5 - OFF_W1));
+}
+
+// grad[OFF_W1 + p] = sum over the workgroups' partial rows, in row order
+__global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part, int nwg,
+                                                                float* __restrict__ g) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= HB_PART) return;
+    float a = 0.f, b = 0.f;
+    int w = 0;
+    for (; w + 1 < nwg; w += 2) {
+        a += part[(int64_t)w * HB_PART + p];
+        b += part[(int64_t)(w + 1) * HB_PART + p];
+    }
+    if (w < nwg) a += part[(int64_t)w * HB_PART + p];
+    g[OFF_W1 + p] = a + b;
 }
 
 // BPTT through one cell (dh = dh_head + dh_next; dc carried in place).  The fused backward
@@ -719,6 +977,7 @@ struct rdl_trainer {
     uint32_t* ctl = nullptr;
     uint32_t* bar = nullptr;   // persistent kernels: [0] forward / [1] BPTT barrier arrivals, [2] timeout flag
     float* bpart = nullptr;    // persistent BPTT: per-step-parity partial dh of every workgroup
+    float* qbuf = nullptr;     // persistent BPTT: Q = prev^T dz [4][800]
     int64_t last_B = 0;   // windows of the last forward pass (rdl_final_state)
 };
 
@@ -782,6 +1041,14 @@ int pr_dbg() {   // RDL_PR_DBG: bit 0 skip the exchange loads, 1 the MFMAs, 2 th
     return e ? atoi(e) : 0;
 }
 
+// the one-launch head forward for at most HF_MAX_ROWS rows; RDL_FUSED_HEAD=0 keeps the five GEMMs
+bool fused_head(int64_t R) {
+    if (const char* e = getenv("RDL_FUSED_HEAD")) {
+        if (!strcmp(e, "0")) return false;
+    }
+    return R <= HF_MAX_ROWS;
+}
+
 bool persistent(int64_t B) {
     if (const char* e = getenv("RDL_PERSIST")) {
         if (!strcmp(e, "0")) return false;
@@ -838,6 +1105,12 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     }
     // head over all T x B rows (student_nn.py:42-46)
     const float* Hc = t->H + B * U;
+    if (fused_head(R)) {
+        hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)((R + HF_ROWS - 1) / HF_ROWS)), dim3(256), 0, t->stream, Hc, P,
+                           t->A1, t->A2, t->A3, t->A4, out_pdflat, R);
+        RDL_CK(hipGetLastError(), "rdl head_fwd_kernel");
+        return RD_OK;
+    }
     RDL_CK(mm(t, (int)R, H1, U, Hc, U, 0, P + OFF_W1, H1, 0, t->A1, L1, P + OFF_B1, rdg::EPI_TANH), "rdl head1");
     RDL_CK(mm(t, (int)R, H2, H1, t->A1, L1, 0, P + OFF_W2, H2, 0, t->A2, L2, P + OFF_B2, rdg::EPI_TANH), "rdl head2");
     RDL_CK(mm(t, (int)R, H3, H2, t->A2, L2, 0, P + OFF_W3, H3, 0, t->A3, L3, P + OFF_B3, rdg::EPI_TANH), "rdl head3");
@@ -863,6 +1136,17 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
                            t->ctl, t->hist, t->cfg.metrics_len);
         RDL_CK(hipGetLastError(), "rdl metrics_kernel");
     }
+    const float* Hc = t->H + B * U;
+    if (fused_head(R)) {   // the head backward as two launches (head_bwd_kernel + fixed-order reduce)
+        const unsigned nwg = (unsigned)((R + HF_ROWS - 1) / HF_ROWS);
+        hipLaunchKernelGGL(head_bwd_kernel, dim3(nwg), dim3(256), 0, t->stream, Hc, P, (const float*)t->A1,
+                           (const float*)t->A2, (const float*)t->A3, (const float*)t->A4, (const float*)t->dY, t->dHh,
+                           t->split, R);
+        RDL_CK(hipGetLastError(), "rdl head_bwd_kernel");
+        hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((HB_PART + 255) / 256), dim3(256), 0, t->stream,
+                           (const float*)t->split, (int)nwg, g);
+        RDL_CK(hipGetLastError(), "rdl head_wgrad_reduce_kernel");
+    } else {
     // head backward (weight gradients over all rows; data gradients with the tanh derivative fused)
     // per layer, [dW; db] (weight gradient, ones column) beside the data gradient with tanh'
     RDL_CK(mm2(t, ga(H4 + 1, 4, Ri, t->A4, L4, 1, t->dY, 4, 0, g + OFF_W5, 4),
@@ -877,17 +1161,17 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     RDL_CK(mm2(t, ga(H1 + 1, H2, Ri, t->A1, L1, 1, t->D128, H2, 0, g + OFF_W2, H2),
                ga(Ri, H1, H2, t->D128, H2, 0, P + OFF_W2, H2, 1, t->D64b, H1, rdg::EPI_DTANH, t->A1, L1)),
            "rdl dW2 db2 | dZ1");
-    const float* Hc = t->H + B * U;
     RDL_CK(mm2(t, ga(U, H1, Ri, Hc, U, 1, t->D64b, H1, 0, g + OFF_W1, H1),
                ga(Ri, U, H1, t->D64b, H1, 0, P + OFF_W1, H1, 1, t->dHh, U)),
            "rdl dW1 | dHhead");
     RDL_CK(colsum(t, t->D64b, R, H1, H1, g + OFF_B1), "rdl db1");
+    }
     // BPTT (the gate buffer Z is reused for dz: the forward keeps activations in G)
     float* dZl = t->Z;
     if (persistent(B)) {
         hipLaunchKernelGGL(lstm_bptt_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
-                           (const float*)t->dHh, (const float*)t->G, (const float*)t->Cs, dZl, t->bpart, (int)B, T,
-                           t->bar, pr_dbg());
+                           (const float*)t->dHh, (const float*)t->G, (const float*)t->Cs, dZl, t->bpart, g + OFF_BL,
+                           prev, t->qbuf, (int)B, T, t->bar, pr_dbg());
         RDL_CK(hipGetLastError(), "rdl lstm_bptt_persist_kernel");
     } else {
     RDL_CK(hipMemsetAsync(t->dc, 0, sizeof(float) * B * U, t->stream), "rdl bptt");
@@ -932,10 +1216,15 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     RDL_CK(mm2(t, ga(XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4),
                ga(U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4)),
            "rdl dWl x | h");
-    RDL_CK(colsum(t, dZl, R, G4, G4, g + OFF_BL), "rdl dbl");
-    RDL_CK(mm(t, Ri, 32, G4, dZl, G4, 0, P + OFF_WL + 11 * G4, G4, 1, t->dP, 32), "rdl dP");
-    RDL_CK(mm(t, 4, 32, Ri, prev, 4, 1, t->dP, 32, 0, g + OFF_WP, 32), "rdl dWp");
-    RDL_CK(colsum(t, t->dP, R, 32, 32, g + OFF_BP), "rdl dbp");
+    if (!persistent(B)) RDL_CK(colsum(t, dZl, R, G4, G4, g + OFF_BL), "rdl dbl");   // else summed in BPTT
+    if (persistent(B)) {   // from the BPTT kernel's dbl and Q = prev^T dz: one launch
+        hipLaunchKernelGGL(dense32_grad_kernel, dim3(160), dim3(256), 0, t->stream, P, (const float*)t->qbuf, g);
+        RDL_CK(hipGetLastError(), "rdl dense32_grad_kernel");
+    } else {
+        RDL_CK(mm(t, Ri, 32, G4, dZl, G4, 0, P + OFF_WL + 11 * G4, G4, 1, t->dP, 32), "rdl dP");
+        RDL_CK(mm(t, 4, 32, Ri, prev, 4, 1, t->dP, 32, 0, g + OFF_WP, 32), "rdl dWp");
+        RDL_CK(colsum(t, t->dP, R, 32, 32, g + OFF_BP), "rdl dbp");
+    }
     return RD_OK;
 }
 
@@ -1009,6 +1298,7 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     if (e == hipSuccess) e = hipMalloc((void**)&t->ctl, sizeof(uint32_t) * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&t->bar, sizeof(uint32_t) * 4);
     alloc(&t->bpart, (int64_t)2 * PR_GRID * PB_PART);
+    alloc(&t->qbuf, 4 * G4);
     if (e == hipSuccess) e = hipMemsetAsync(t->bar, 0, sizeof(uint32_t) * 4, t->stream);
     t->grad = t->own_grad;
     if (e != hipSuccess) {
@@ -1039,7 +1329,7 @@ int rdl_destroy(rdl_trainer* t) {
     rd::DeviceGuard dg(t->device);
     float* bufs[] = {t->params, t->m, t->v, t->own_grad, t->X, t->H, t->Cs, t->Z, t->G, t->A1, t->A2, t->A3, t->A4,
                      t->Y, t->dY, t->D32, t->D64a, t->D128, t->D64b, t->dHh, t->dP, t->dhn, t->dc, t->split,
-                     t->colws, t->lpart, t->hist, t->bpart};
+                     t->colws, t->lpart, t->hist, t->bpart, t->qbuf};
     for (float* p : bufs)
         if (p) (void)hipFree(p);
     if (t->ctl) (void)hipFree(t->ctl);

@@ -307,3 +307,27 @@ def test_persistent_recurrence_matches_per_step_launches(monkeypatch, T, B, with
     fw = ln.forward(p, ob, prev, st)
     _, d, _ = ln.loss_and_dout(fw["pdflat"], t, "kl", T * B)
     _grad_check(g1, ln.backward(p, fw, d))
+
+
+@pytest.mark.parametrize("T,B", [(10, 20), (3, 130), (1, 5)])
+def test_fused_head_matches_the_layer_gemms(monkeypatch, T, B):
+    """At most 2,048 rows: the head's forward is one launch (head_fwd_kernel) and its backward
+    two (head_bwd_kernel + a fixed-order reduce).  Same MFMA k order and epilogues as the
+    per-layer GEMMs for the activations and the data gradients, so the outputs, dh_head and
+    everything BPTT derives from it (the LSTM's gradients) are bitwise those of
+    RDL_FUSED_HEAD=0; the head's weight gradients sum the rows in per-16-row partials, so they
+    agree to 1e-5 of their largest entry."""
+    ob, prev, t = _batch(T, B, 21 + B)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RDL_FUSED_HEAD", mode)
+        tr = _trainer(T, B, "mse")
+        y, _ = tr.forward(_t(ob), _t(prev))
+        g = tr.rollout(_t(ob), _t(prev), _t(t)).cpu().numpy()
+        out[mode] = (y.cpu().numpy(), g)
+        tr.close()
+    assert np.array_equal(out["1"][0], out["0"][0])
+    w1 = ln.LAYOUT["W1"][0]   # the head's [W1 b1 ... W5 b5] range starts here
+    assert np.array_equal(out["1"][1][:w1], out["0"][1][:w1])
+    h1, h0 = out["1"][1][w1:], out["0"][1][w1:]
+    assert np.abs(h1 - h0).max() <= 1e-5 * np.abs(h0).max()
