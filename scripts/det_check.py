@@ -22,7 +22,9 @@ def roll(**kw):
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 CASES = {"c4s": dict(n_envs=262144, f32_split=True), "c4e": dict(n_envs=262144, f32_split=False),
          "c5": dict(n_envs=131072, act_with="student", student_dtype="bf16", f32_split=True),
-         "c5e": dict(n_envs=131072, act_with="student", student_dtype="bf16", f32_split=False)}
+         "c5e": dict(n_envs=131072, act_with="student", student_dtype="bf16", f32_split=False),
+         "c2s": dict(n_envs=4096, f32_split=True), "c2e": dict(n_envs=4096, f32_split=False),
+         "c3s": dict(n_envs=65536, loss="kl", f32_split=True)}
 for name in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["c4s", "c4e"]):
     kw = CASES[name]
     ref = roll(**kw)
@@ -36,4 +38,4 @@ for name in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["c4s", "c4e"]):
                   "unstepped in bad run:", same_as_start, "grad entries differing", (ref[0] != b[0]).nonzero().flatten()[:8].tolist(),
                   "state rows differing", (ref[1][:, bad] != b[1][:, bad]).any(1).nonzero().flatten().tolist())
         else:
-            print(os.environ.get("RDD_PHYS"), kw, "rep", r, "identical")
+            print(os.environ.get("RDD_PHYS"), os.environ.get("RDD_EP"), kw, "rep", r, "identical")
