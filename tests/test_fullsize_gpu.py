@@ -44,12 +44,16 @@ def test_full_size_shard_linearity_and_state(wl, split):
     assert torch.equal(torch.cat([parts[0][1], parts[1][1]], dim=1), s_full)
 
 
+WL_KW = {"c2": dict(n_envs=4096), "c3": dict(n_envs=65536, loss="kl"), "c4": dict(n_envs=262144),
+         "c5": dict(n_envs=131072, act_with="student", student_dtype="bf16")}
+
+
 @pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("wl", ["c4", "c5"])
+@pytest.mark.parametrize("wl", ["c2", "c3", "c4", "c5"])
 def test_full_size_rollout_is_deterministic(wl, split):
-    """Three fresh trainers, one rollout each: gradients and env states bitwise equal (c5 runs
-    the consumer-side env step, c4 the producer-side one)."""
-    kw = dict(n_envs=262144) if wl == "c4" else dict(n_envs=131072, act_with="student", student_dtype="bf16")
+    """Three fresh trainers, one rollout each: gradients and env states bitwise equal (every
+    config steps the envs on the producer wave)."""
+    kw = WL_KW[wl]
     a = _rollout(_tr(f32_split=split, **kw))
     for _ in range(2):
         b = _rollout(_tr(f32_split=split, **kw))
