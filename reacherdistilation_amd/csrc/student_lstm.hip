@@ -1451,9 +1451,13 @@ int rdl_bind_grad_buffer(rdl_trainer* t, float* grad) {
 int rdl_get_counter(rdl_trainer* t, int64_t* opt_steps) {
     if (!t || !opt_steps) return rd::set_error(RD_EINVAL, "rdl_get_counter: null argument");
     rd::DeviceGuard dg(t->device);
-    uint32_t c[8];
+    uint32_t c[8], b[4];
     RD_HIP(hipMemcpyAsync(c, t->ctl, sizeof(c), hipMemcpyDeviceToHost, t->stream), "rdl_get_counter");
+    RD_HIP(hipMemcpyAsync(b, t->bar, sizeof(b), hipMemcpyDeviceToHost, t->stream), "rdl_get_counter");
     RD_HIP(hipStreamSynchronize(t->stream), "rdl_get_counter");
+    if (b[2])   // a persistent launch gave up at a grid barrier (workgroups not co-resident)
+        return rd::set_error(RD_EINVAL, "rdl: a persistent recurrence launch timed out at its grid barrier; "
+                                        "the steps since are invalid (RDL_PERSIST=0 avoids the persistent kernels)");
     *opt_steps = c[0];
     return RD_OK;
 }
