@@ -88,6 +88,8 @@ int rdl_step(rdl_trainer* t, const float* ob, const float* prev_pdflat, const fl
              const float* state0, int64_t windows);
 float* rdl_grad_buffer(rdl_trainer* t);
 int rdl_bind_grad_buffer(rdl_trainer* t, float* grad);
+/* optimiser steps taken; RD_EINVAL if a persistent recurrence launch (<= 32 windows) gave up
+ * at its grid barrier since the trainer was created (its steps are invalid) */
 int rdl_get_counter(rdl_trainer* t, int64_t* opt_steps);
 /* [count][4] = loss, sum |mu_s - mu_t|^2, rows (T x B), 0 */
 int rdl_read_metrics(rdl_trainer* t, int64_t count, double* out);
