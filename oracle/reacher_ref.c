@@ -23,6 +23,9 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <string.h>
 
 /* model constants as constant expressions */
@@ -204,12 +207,21 @@ void rdo_distill_step(int64_t n, int64_t n_global, int64_t env_base, uint64_t se
                       const float* sp, const float* smu, const float* ssd, int loss, int act_student,
                       int stagger, float* grad, double* metrics, int nthreads) {
     memset(grad, 0, sizeof(float) * P_TOT);
-    double rsum = 0, lsum = 0, msum = 0;
     const float tls0 = tp[P_LS], tls1 = tp[P_LS + 1];
     const float sls0 = sp[P_LS], sls1 = sp[P_LS + 1];
-#pragma omp parallel num_threads(nthreads) reduction(+ : rsum, lsum, msum)
+    if (nthreads < 1) nthreads = 1;
+    /* per-thread partials, summed in thread order afterwards: the result does not depend on
+       which thread finishes first (deterministic for a given nthreads) */
+    float* gpart = (float*)calloc((size_t)nthreads * P_TOT, sizeof(float));
+    double* mpart = (double*)calloc((size_t)nthreads * 3, sizeof(double));
+#pragma omp parallel num_threads(nthreads)
     {
-        float* g = (float*)calloc(P_TOT, sizeof(float));
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        float* g = gpart + (size_t)tid * P_TOT;
+        double rsum = 0, lsum = 0, msum = 0;
 #pragma omp for schedule(static)
         for (int64_t i = 0; i < n; ++i) {
             float s[8], ob[OBD];
@@ -249,10 +261,19 @@ void rdo_distill_step(int64_t n, int64_t n_global, int64_t env_base, uint64_t se
             }
             for (int k = 0; k < 8; ++k) state[k * n + i] = s[k];
         }
-#pragma omp critical
-        for (int k = 0; k < P_TOT; ++k) grad[k] += g[k];
-        free(g);
+        mpart[3 * tid] = rsum;
+        mpart[3 * tid + 1] = lsum;
+        mpart[3 * tid + 2] = msum;
     }
+    double rsum = 0, lsum = 0, msum = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        for (int k = 0; k < P_TOT; ++k) grad[k] += gpart[(size_t)t * P_TOT + k];
+        rsum += mpart[3 * t];
+        lsum += mpart[3 * t + 1];
+        msum += mpart[3 * t + 2];
+    }
+    free(gpart);
+    free(mpart);
     metrics[0] += rsum;
     metrics[1] += lsum;
     metrics[2] += msum;
