@@ -37,5 +37,9 @@ for name in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["c4s", "c4e"]):
             print(os.environ.get("RDD_PHYS"), kw, "rep", r, "bad envs", len(bad), "first", e, "last", bad[-1].item(),
                   "unstepped in bad run:", same_as_start, "grad entries differing", (ref[0] != b[0]).nonzero().flatten()[:8].tolist(),
                   "state rows differing", (ref[1][:, bad] != b[1][:, bad]).any(1).nonzero().flatten().tolist())
+        elif not torch.equal(ref[0], b[0]):
+            d = (ref[0] != b[0]).nonzero().flatten()
+            print(os.environ.get("RDD_PHYS"), kw, "rep", r, "states identical, grad entries differ:",
+                  d[:8].tolist(), "max", float((ref[0] - b[0]).abs().max()))
         else:
-            print(os.environ.get("RDD_PHYS"), os.environ.get("RDD_EP"), kw, "rep", r, "identical")
+            print(os.environ.get("RDD_PHYS"), kw, "rep", r, "identical")
