@@ -173,6 +173,31 @@ __device__ __forceinline__ float tanh_pre(float y) {
     return fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(y) + 1.0f), 1.0f);
 #endif
 }
+// tanh_pre on the four rows of an accumulator.  PK: the add and the fma as packed-f32 pairs
+// (v_pk_add_f32 / v_pk_fma_f32), bitwise the same results.  Measured per call site
+// (profiles/r02_pk_tanh.txt): PK pays in the split pair forward (c3/c4 ≈1 % per step) and
+// loses beside the bf16 student's MFMAs (c5 −1.5 %), so only that forward uses it.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <bool PK = false>
+__device__ __forceinline__ f32x4 tanh4(f32x4 y) {
+#ifndef RD_ABL_TANH
+    if constexpr (!PK) {
+        return f32x4{tanh_pre(y[0]), tanh_pre(y[1]), tanh_pre(y[2]), tanh_pre(y[3])};
+    } else {
+        f32x2 e0 = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+        f32x2 e1 = {__builtin_amdgcn_exp2f(y[2]), __builtin_amdgcn_exp2f(y[3])};
+        e0 = e0 + 1.0f;
+        e1 = e1 + 1.0f;
+        const f32x2 r0 = {__builtin_amdgcn_rcpf(e0[0]), __builtin_amdgcn_rcpf(e0[1])};
+        const f32x2 r1 = {__builtin_amdgcn_rcpf(e1[0]), __builtin_amdgcn_rcpf(e1[1])};
+        const f32x2 t0 = __builtin_elementwise_fma(r0, (f32x2){-2.0f, -2.0f}, (f32x2){1.0f, 1.0f});
+        const f32x2 t1 = __builtin_elementwise_fma(r1, (f32x2){-2.0f, -2.0f}, (f32x2){1.0f, 1.0f});
+        return f32x4{t0[0], t0[1], t1[0], t1[1]};
+    }
+#else
+    return f32x4{tanh_pre(y[0]), tanh_pre(y[1]), tanh_pre(y[2]), tanh_pre(y[3])};
+#endif
+}
 
 // The per-wave scratch is private to its wave: LDS instructions of one wave execute in
 // issue order, so staging needs only a compiler-level barrier, not s_barrier.
@@ -283,8 +308,7 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
     }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) H1[fb][r] = tanh_pre(acc[fb][r]);
+        H1[fb] = tanh4(acc[fb]);
     // layer 2: K = 64; k-step (kb, r) uses features 16 kb + 4 g + r = this lane's H1[kb][r]
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + N_B2 + 16 * fb + 4 * g);
@@ -307,8 +331,7 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
     for (int fb = 0; fb < 4; ++fb) {
         const f32x4 wa = ld4(L + N_W3 + (16 * fb + 4 * g) * 2);       // W3[f][0..1], f = 16fb+4g+0,1
         const f32x4 wb = ld4(L + N_W3 + (16 * fb + 4 * g) * 2 + 4);   // f = 16fb+4g+2,3
-#pragma unroll
-        for (int r = 0; r < 4; ++r) H2[fb][r] = tanh_pre(acc[fb][r]);
+        H2[fb] = tanh4(acc[fb]);
         p0 = fmaf(H2[fb][0], wa[0], p0); p1 = fmaf(H2[fb][0], wa[1], p1);
         p0 = fmaf(H2[fb][1], wa[2], p0); p1 = fmaf(H2[fb][1], wa[3], p1);
         p0 = fmaf(H2[fb][2], wb[0], p0); p1 = fmaf(H2[fb][2], wb[1], p1);
@@ -345,12 +368,10 @@ __device__ __forceinline__ void mlp_forward_pair(const float* LT, const float* L
     }
     f32x4 T1[4];
 #pragma unroll
-    for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            T1[fb][r] = tanh_pre(at[fb][r]);
-            H1[fb][r] = tanh_pre(as[fb][r]);
-        }
+    for (int fb = 0; fb < 4; ++fb) {
+        T1[fb] = tanh4(at[fb]);
+        H1[fb] = tanh4(as[fb]);
+    }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) {
         at[fb] = ld4(LT + N_B2 + 16 * fb + 4 * g);
@@ -380,11 +401,8 @@ __device__ __forceinline__ void mlp_forward_pair(const float* LT, const float* L
         const f32x4 ta = ld4(LT + N_W3 + (16 * fb + 4 * g) * 2), tb = ld4(LT + N_W3 + (16 * fb + 4 * g) * 2 + 4);
         const f32x4 sa = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2), sb = ld4(LS + N_W3 + (16 * fb + 4 * g) * 2 + 4);
         f32x4 t2;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            t2[r] = tanh_pre(at[fb][r]);
-            H2[fb][r] = tanh_pre(as[fb][r]);
-        }
+        t2 = tanh4(at[fb]);
+        H2[fb] = tanh4(as[fb]);
         pt0 = fmaf(t2[0], ta[0], pt0); pt1 = fmaf(t2[0], ta[1], pt1);
         pt0 = fmaf(t2[1], ta[2], pt0); pt1 = fmaf(t2[1], ta[3], pt1);
         pt0 = fmaf(t2[2], tb[0], pt0); pt1 = fmaf(t2[2], tb[1], pt1);
@@ -593,12 +611,10 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
     }
     f32x4 T1[4];
 #pragma unroll
-    for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            T1[fb][r] = tanh_pre(at[fb][r]);
-            H1[fb][r] = tanh_pre(as[fb][r]);
-        }
+    for (int fb = 0; fb < 4; ++fb) {
+        T1[fb] = tanh4<true>(at[fb]);
+        H1[fb] = tanh4<true>(as[fb]);
+    }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) {
         at[fb] = ld4(LT + NX_B2 + 16 * fb + 4 * g);
@@ -626,11 +642,8 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
         const f32x4 ta = ld4(LT + NX_W3 + (16 * fb + 4 * g) * 2), tb = ld4(LT + NX_W3 + (16 * fb + 4 * g) * 2 + 4);
         const f32x4 sa = ld4(LS + NX_W3 + (16 * fb + 4 * g) * 2), sb = ld4(LS + NX_W3 + (16 * fb + 4 * g) * 2 + 4);
         f32x4 t2;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            t2[r] = tanh_pre(at[fb][r]);
-            H2[fb][r] = tanh_pre(as[fb][r]);
-        }
+        t2 = tanh4<true>(at[fb]);
+        H2[fb] = tanh4<true>(as[fb]);
         pt0 = fmaf(t2[0], ta[0], pt0); pt1 = fmaf(t2[0], ta[1], pt1);
         pt0 = fmaf(t2[1], ta[2], pt0); pt1 = fmaf(t2[1], ta[3], pt1);
         pt0 = fmaf(t2[2], tb[0], pt0); pt1 = fmaf(t2[2], tb[1], pt1);
@@ -664,8 +677,7 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
     }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) H1[fb][r] = tanh_pre(acc[fb][r]);
+        H1[fb] = tanh4(acc[fb]);
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NX_B2 + 16 * fb + 4 * g);
 #pragma unroll
@@ -685,8 +697,7 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
         const f32x4 wa = ld4(L + NX_W3 + (16 * fb + 4 * g) * 2);
         const f32x4 wb = ld4(L + NX_W3 + (16 * fb + 4 * g) * 2 + 4);
         f32x4 h2;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h2[r] = tanh_pre(acc[fb][r]);
+        h2 = tanh4(acc[fb]);
         if constexpr (HO) H2[fb] = h2;
         p0 = fmaf(h2[0], wa[0], p0); p1 = fmaf(h2[0], wa[1], p1);
         p0 = fmaf(h2[1], wa[2], p0); p1 = fmaf(h2[1], wa[3], p1);
@@ -854,8 +865,7 @@ __device__ __forceinline__ void mlp_forward_bf16(const float* L, const float* ob
     for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma_k32(ldbf8(L + NB_W1, ((g * 4 + fb) * 16 + j) * 8), zb, acc[fb]);
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) H1[fb][r] = tanh_pre(kTanhScale * acc[fb][r]);
+        H1[fb] = tanh4(kTanhScale * acc[fb]);
     // layer 2: two K = 32 steps over the permuted feature order kperm
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NB_B2 + 16 * fb + 4 * g);
@@ -871,8 +881,7 @@ __device__ __forceinline__ void mlp_forward_bf16(const float* L, const float* ob
     for (int fb = 0; fb < 4; ++fb) {
         const f32x4 wa = ld4(L + NB_W3 + (16 * fb + 4 * g) * 2);
         const f32x4 wb = ld4(L + NB_W3 + (16 * fb + 4 * g) * 2 + 4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) H2[fb][r] = tanh_pre(kTanhScale * acc[fb][r]);
+        H2[fb] = tanh4(kTanhScale * acc[fb]);
         p0 = fmaf(H2[fb][0], wa[0], p0); p1 = fmaf(H2[fb][0], wa[1], p1);
         p0 = fmaf(H2[fb][1], wa[2], p0); p1 = fmaf(H2[fb][1], wa[3], p1);
         p0 = fmaf(H2[fb][2], wb[0], p0); p1 = fmaf(H2[fb][2], wb[1], p1);
