@@ -175,8 +175,8 @@ __device__ __forceinline__ float tanh_pre(float y) {
 }
 // tanh_pre on the four rows of an accumulator.  PK: the add and the fma as packed-f32 pairs
 // (v_pk_add_f32 / v_pk_fma_f32), bitwise the same results.  Measured per call site
-// (profiles/r02_pk_tanh.txt): PK pays in the split pair forward (c3/c4 ≈1 % per step) and
-// loses beside the bf16 student's MFMAs (c5 −1.5 %), so only that forward uses it.
+// (profiles/r02_pk_tanh.txt): PK pays in the split pair forward (c3/c4 ≈1 % per step), is
+// neutral in the bf16 student's and loses in the c5 teacher's (−1.5 %), so only the pair uses it.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool PK = false>
 __device__ __forceinline__ f32x4 tanh4(f32x4 y) {
@@ -526,13 +526,14 @@ __device__ __forceinline__ void split8(f32x4 lo, f32x4 hi, bf16x8 (&p)[3]) {
     const float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     uint32_t u0[8], u1[8], u2[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t u = __float_as_uint(x[i]);
-        const float r = x[i] - __uint_as_float(u & 0xffff0000u);
-        const uint32_t ur = __float_as_uint(r);
-        u0[i] = u;
-        u1[i] = ur;
-        u2[i] = __float_as_uint(r - __uint_as_float(ur & 0xffff0000u));
+    for (int i = 0; i < 8; i += 2) {   // the two exact subtractions per pair as v_pk_add_f32
+        const f32x2 xv = {x[i], x[i + 1]};
+        const uint32_t ua = __float_as_uint(x[i]), ub = __float_as_uint(x[i + 1]);
+        const f32x2 r = xv - f32x2{__uint_as_float(ua & 0xffff0000u), __uint_as_float(ub & 0xffff0000u)};
+        const uint32_t ra = __float_as_uint(r[0]), rb = __float_as_uint(r[1]);
+        const f32x2 l = r - f32x2{__uint_as_float(ra & 0xffff0000u), __uint_as_float(rb & 0xffff0000u)};
+        u0[i] = ua; u0[i + 1] = ub; u1[i] = ra; u1[i + 1] = rb;
+        u2[i] = __float_as_uint(l[0]); u2[i + 1] = __float_as_uint(l[1]);
     }
     u32x4 q0, q1, q2;
 #pragma unroll
