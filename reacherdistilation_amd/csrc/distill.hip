@@ -133,13 +133,24 @@ struct ReduceArgs {
 };
 
 #ifndef RDD_RED_COLS   // diagnostic builds may change the reduce blocking (A/B)
-#define RDD_RED_COLS 64
+#define RDD_RED_COLS 32
 #define RDD_RED_ROWS 16
 #endif
-constexpr int RED_COLS = RDD_RED_COLS;              // params per reduce block
+// The partials workspace is column-chunked: chunk c (params 32c .. 32c+31) holds the rows of
+// every workgroup of the launch contiguously, [chunk][row][RED_COLS], one 128-B line per row,
+// so one reduce block per chunk reads one contiguous run and the reduce spreads over 159
+// blocks (with [row][P_PAD] rows a block needed 64 columns for 256-B segments: 80 blocks
+// pulled c4's 5.2 MB of partials).  Bitwise the same sums (the row order per column depends
+// on RED_ROWS only).  16-column chunks (317 blocks) make the rollout's stores half lines and
+// cost it 5 us at c4 (profiles/r02_ws_chunked.txt).
+constexpr int RED_COLS = RDD_RED_COLS;              // params per reduce block = chunk width
 constexpr int RED_ROWS = RDD_RED_ROWS;              // partial rows summed in parallel
 constexpr int RED_BLOCK = RED_COLS * RED_ROWS;
 constexpr int RED_GRID = (P_PAD + RED_COLS - 1) / RED_COLS;
+constexpr int P_WS = RED_GRID * RED_COLS;           // workspace floats per partial row
+__device__ __forceinline__ int64_t ws_index(int p, int row, int rows) {
+    return ((int64_t)(p / RED_COLS) * rows + row) * RED_COLS + (p % RED_COLS);
+}
 
 struct RolloutArgs {
     int64_t n, env_base;
@@ -148,7 +159,7 @@ struct RolloutArgs {
     const float* tnet;                     // teacher: params[P], mu[11], sd[11] (contiguous)
     const float* snet;                     // student
     uint32_t* ctl;                         // [0] completed steps, [4..7] snapshot
-    float* ws;                             // [gridDim.x][P_PAD]
+    float* ws;                             // [RED_GRID][gridDim.x][RED_COLS] (ws_index)
     int loss, act_student, stagger;
     float inv_n_global;
     int gs;                                // envs per group (16, 32 or 64)
@@ -946,16 +957,16 @@ __device__ __forceinline__ float env_step_group(const RolloutArgs& a, uint32_t C
 // sums are then added in a fixed order (deterministic).
 __device__ __forceinline__ float col_rows(const float* ws, int nblk, int p, int row) {
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    const float* w = ws + p;
+    const float* w = ws + ws_index(p, 0, nblk);   // row b of column p at w[b * RED_COLS]
     int b = row;
 #pragma unroll 4
     for (; b + 3 * RED_ROWS < nblk; b += 4 * RED_ROWS) {
-        s0 += w[(int64_t)b * P_PAD];
-        s1 += w[(int64_t)(b + RED_ROWS) * P_PAD];
-        s2 += w[(int64_t)(b + 2 * RED_ROWS) * P_PAD];
-        s3 += w[(int64_t)(b + 3 * RED_ROWS) * P_PAD];
+        s0 += w[b * RED_COLS];
+        s1 += w[(b + RED_ROWS) * RED_COLS];
+        s2 += w[(b + 2 * RED_ROWS) * RED_COLS];
+        s3 += w[(b + 3 * RED_ROWS) * RED_COLS];
     }
-    for (; b < nblk; b += RED_ROWS) s0 += w[(int64_t)b * P_PAD];
+    for (; b < nblk; b += RED_ROWS) s0 += w[b * RED_COLS];
     return (s0 + s1) + (s2 + s3);
 }
 
@@ -1493,13 +1504,14 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     // Both roles passed exactly one s_barrier above (a wave-level count on gfx950, so the
     // two call sites pair up); this second one publishes the regions.
     __syncthreads();
-    f32x4* out = reinterpret_cast<f32x4*>(a.ws + (int64_t)blockIdx.x * P_PAD);
+    static_assert(RED_COLS % 4 == 0, "a 16-B store stays inside one workspace chunk");
 #pragma unroll
     for (int u = 0; u < (P_PAD / 4 + BLOCK - 1) / BLOCK; ++u) {
         const int p4 = threadIdx.x + u * BLOCK;
         if (p4 < P_PAD / 4) {
             const int q = ridx(4 * p4);   // 4 | 64: the four entries stay contiguous
-            out[p4] = (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q));
+            st4(a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x),
+                (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q)));
         }
     }
     STAMP(7);
@@ -1612,7 +1624,7 @@ struct rdd_trainer {
     float* v = nullptr;
     float* grad = nullptr;     // [P] (own or bound)
     float* own_grad = nullptr;
-    float* ws = nullptr;       // [grid][P_PAD]
+    float* ws = nullptr;       // partials of up to ws_rows workgroups (ws_index layout)
     float* hist = nullptr;     // [hist_len][4]
     uint32_t* ctl = nullptr;   // [16]: step words, snapshot, [8] hand-off timeout flag
     unsigned long long* dbg = nullptr;   // RD_STAMPS builds only
@@ -1796,7 +1808,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     alloc((void**)&t->v, sizeof(float) * P_TOT);
     alloc((void**)&t->own_grad, sizeof(float) * P_TOT);
     t->grad = t->own_grad;
-    alloc((void**)&t->ws, sizeof(float) * (size_t)t->ws_rows * P_PAD);
+    alloc((void**)&t->ws, sizeof(float) * (size_t)t->ws_rows * P_WS);
     alloc((void**)&t->hist, sizeof(float) * (size_t)t->cfg.metrics_len * N_MET);
     alloc((void**)&t->ctl, sizeof(uint32_t) * 16);
 #ifdef RD_STAMPS
