@@ -44,7 +44,7 @@ WORKLOADS = {
                desc="BASELINE config 3: 65,536 envs/GPU, Gaussian KL(s||t) distillation, fp32"),
     "c4": dict(envs=262144, loss="mse", act_with="teacher",
                desc="BASELINE config 4: 262,144 envs per GPU, RCCL student-grad all-reduce, MSE, fp32"),
-    "c5": dict(envs=131072, loss="mse", act_with="student", student_dtype="bf16",
+    "c5": dict(envs=131072, envs_global=1048576, loss="mse", act_with="student", student_dtype="bf16",
                desc="BASELINE config 5 shard: DAgger (student acts, teacher relabels), 1,048,576 envs over 8 GPUs "
                     "= 131,072 envs/GPU, bf16 student MLP (f32 master + Adam), f32 teacher, MSE"),
 }
@@ -81,6 +81,8 @@ def parse():
                          "(include/reacher_distill.h f32_split; default), or every product on the f32 MFMA")
     ap.add_argument("--no-exact-leg", action="store_true",
                     help="skip the secondary timing of the exact-f32-MFMA kernel beside the split one")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="at N > 1 skip the strong-scaling leg (the workload's fixed global batch over the ranks)")
     ap.add_argument("--conv-small-envs", type=int, default=256,
                     help="env count of the second convergence run (the env-step reading of the budget)")
     return ap.parse_args()
@@ -261,6 +263,43 @@ def time_leg(wl, n, sdt, split, dev, lr, steps, warmup, npass=100, settle_ms=0.0
     return {"f32_mode": "split" if split else "exact", "value": n * steps / el, "ms_per_step": el * 1e3 / steps,
             "launch_us": kern_ms * 1e3, "achieved_tflops": achieved, "peak_tflops": peak, "frac": achieved / peak,
             "frac_of_f32_mfma_peak": achieved / PEAK_F32_TFLOPS}
+
+
+def strong_leg(wl, total, sdt, split, dev, lr, steps, warmup, rank, world, comm, settle_ms=0.0):
+    """BASELINE config 4's own wording, "262 144 envs sharded across 8 x MI355X": the
+    workload's fixed global batch split over the ranks (`n_envs_global`, contiguous shards,
+    Philox key = global env id), timed like the headline (barrier + synchronize around
+    exactly `steps` fused steps, MAX over ranks).  Reported beside the weak-scaling value."""
+    import torch
+    import torch.distributed as dist
+
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    tr = DistillTrainer(DistillConfig(n_envs_global=total, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
+                                      student_dtype=sdt, f32_split=split),
+                        device=dev, rank=rank, world_size=world, comm=comm)
+    settle(tr.step, dev, settle_ms, world)
+    for _ in range(warmup):
+        tr.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    same = tr.replicas_identical() if world > 1 else True
+    out = {"envs_total": total, "envs_per_gpu": tr.n_local, "steps": steps, "value": total * steps / el,
+           "ms_per_step": el * 1e3 / steps, "replicas_identical": same, "scaling": "strong"}
+    tr.close()
+    return out
 
 
 def cpu_baseline(workload, seconds, threads, n):
@@ -475,6 +514,14 @@ def main():
                  "replicas_identical": tk.replicas_identical() if world > 1 else True}
         tk.close()
 
+    # the strong-scaling reading of the workload (its fixed global batch over the ranks); at
+    # one GPU it is the headline run itself (c4: 262,144 envs on one GPU)
+    strong = None
+    total = wl.get("envs_global", wl["envs"])
+    if world > 1 and not args.no_strong and not args.envs_per_gpu:
+        strong = strong_leg(wl, total, sdt, split, dev, args.lr, max(args.steps, 100), args.warmup, rank, world, comm,
+                            settle_ms=min(args.settle_ms, 100.0))
+
     # student action-MSE vs teacher over the last steps (all ranks)
     met = tr.metrics(min(10, tr.counter()))
     mt = torch.tensor(met.sum(0), dtype=torch.float64, device=dev)
@@ -539,6 +586,8 @@ def main():
         }
         if other is not None:
             out["other_f32_mode"] = other
+        if strong is not None:
+            out["strong_scaling"] = strong
         if accum is not None:
             out["accum"] = accum
         if conv is not None:
