@@ -265,6 +265,25 @@ def time_leg(wl, n, sdt, split, dev, lr, steps, warmup, npass=100, settle_ms=0.0
             "frac_of_f32_mfma_peak": achieved / PEAK_F32_TFLOPS}
 
 
+def exchange_latency(comm, dev, n=5060, iters=200, warmup=20):
+    """Mean time of one in-place all-reduce of the student gradient's size (5,060 floats) on
+    the bound communicator, back to back on the current stream (HIP events, all ranks)."""
+    import torch
+    import torch.distributed as dist
+    x = torch.ones(n, dtype=torch.float32, device=dev)
+    for _ in range(warmup):
+        comm.allreduce_(x)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        comm.allreduce_(x)
+    b.record()
+    torch.cuda.synchronize(dev)
+    return {"floats": n, "us": a.elapsed_time(b) * 1e3 / iters, "iters": iters}
+
+
 def strong_leg(wl, total, sdt, split, dev, lr, steps, warmup, rank, world, comm, settle_ms=0.0):
     """BASELINE config 4's own wording, "262 144 envs sharded across 8 x MI355X": the
     workload's fixed global batch split over the ranks (`n_envs_global`, contiguous shards,
@@ -401,9 +420,29 @@ def main():
     # stream (include/reacher_comm.h); RD_COMM=torch keeps torch.distributed's collective.
     # A communicator that fails its one-shot self-check is dropped for torch's (reported).
     comm, collective = None, "none"
-    if world > 1:
+    exchange = None
+    want = os.environ.get("RD_COMM", "xgmi")
+    if world > 1 and want == "xgmi":
+        # the default: the one-shot xGMI push (include/reacher_comm.h rd_xcomm_*); falls back
+        # to the native RCCL communicator, then torch's collective, and says which one ran
+        from reacherdistilation_amd.dist import XgmiComm
+        try:
+            comm = XgmiComm(dev)
+            ok = comm.self_check()
+        except Exception as e:   # noqa: BLE001  (reported in the line, never silent)
+            print(f"xGMI exchange unavailable ({e}); trying RCCL", file=sys.stderr)
+            comm, ok = None, False
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 1:
+            collective = "xgmi push (native, one kernel, trainer stream)"
+            exchange = exchange_latency(comm, dev)
+        else:
+            comm = None
+            want = "rccl"
+    if world > 1 and comm is None:
         collective = "torch.distributed"
-        if dist.get_backend() == "nccl" and os.environ.get("RD_COMM", "rccl") == "rccl":
+        if dist.get_backend() == "nccl" and want == "rccl":
             from reacherdistilation_amd.dist import RcclComm
             try:
                 comm = RcclComm(dev)
@@ -415,6 +454,7 @@ def main():
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if int(flag.item()) == 1:
                 collective = "rccl (native, trainer stream)"
+                exchange = exchange_latency(comm, dev)
             else:
                 comm = None
                 collective = "torch.distributed (native RCCL self-check failed)"
@@ -588,6 +628,8 @@ def main():
             out["other_f32_mode"] = other
         if strong is not None:
             out["strong_scaling"] = strong
+        if exchange is not None:
+            out["exchange"] = exchange
         if accum is not None:
             out["accum"] = accum
         if conv is not None:
@@ -606,6 +648,8 @@ def main():
     if world > 1:
         tr.close()
         if comm is not None:
+            torch.cuda.synchronize(dev)
+            dist.barrier()   # (xGMI) no peer still writes into this rank's exchange buffer
             comm.close()
         dist.destroy_process_group()
 

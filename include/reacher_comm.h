@@ -53,6 +53,23 @@ int rd_comm_allreduce_f32(rd_comm* c, float* buf, int64_t n, void* hip_stream);
 int rd_comm_nranks(const rd_comm* c);
 int rd_comm_destroy(rd_comm* c);
 
+/* The same exchange without RCCL: a one-shot push over xGMI (rd_xgmi.hip).  Each rank
+ * allocates an exchange buffer of uncached device memory (2 x RD_XG ranks x `cap` floats +
+ * flags) and exports it: rd_xcomm_create() writes this rank's RD_XCOMM_HANDLE_BYTES IPC handle
+ * to `handle`; the ranks all-gather the handles (e.g. over the torch.distributed group) and
+ * every rank calls rd_xcomm_connect() with the nranks handles in rank order, which maps every
+ * peer's buffer.  rd_comm_allreduce_f32() on such a communicator is ONE kernel per exchange:
+ * each rank writes its n <= cap floats into its slot of every rank's buffer (one block per
+ * destination, all xGMI links at once), raises a flag there, waits for every flag in its own
+ * buffer and sums the slots in rank order -- so every rank gets bitwise the same sum.  At most
+ * 8 ranks (one node).  rd_comm_check() returns nonzero if an exchange ever waited past its
+ * limit (~4 s) for a peer.  The reference's exchange it replaces: MpiAdam's Allreduce(SUM)
+ * (backup/student_rollout.py:658-659,709). */
+#define RD_XCOMM_HANDLE_BYTES 64
+int rd_xcomm_create(rd_comm** out, int nranks, int rank, int device, int64_t cap, uint8_t* handle);
+int rd_xcomm_connect(rd_comm* c, const uint8_t* handles);
+int rd_comm_check(rd_comm* c);
+
 #ifdef __cplusplus
 }
 #endif

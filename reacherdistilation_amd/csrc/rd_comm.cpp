@@ -17,6 +17,7 @@
 
 #include "../../include/reacher.h"
 #include "../../include/reacher_comm.h"
+#include "rd_comm_impl.h"
 #include "rd_common.h"
 
 namespace {
@@ -62,12 +63,6 @@ int nccl_fail(ncclResult_t e, const char* what) {
 }
 
 }  // namespace
-
-struct rd_comm {
-    ncclComm_t comm = nullptr;
-    int nranks = 0, rank = 0, device = 0;
-    double timeout_s = 60.0;
-};
 
 namespace {
 
@@ -149,6 +144,7 @@ int rd_comm_allreduce_f32(rd_comm* c, float* buf, int64_t n, void* hip_stream) {
     if (!c || !buf || n <= 0) return rd::set_error(RD_EINVAL, "rd_comm_allreduce_f32: bad argument");
     rd::DeviceGuard g(c->device);
     RD_HIP(g.err, "rd_comm_allreduce_f32: hipSetDevice");
+    if (c->xgmi) return xgmi_allreduce(c, buf, n, (hipStream_t)hip_stream);
     ncclResult_t e = rccl().all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, (hipStream_t)hip_stream);
     if (e == ncclInProgress) return wait_ready(c, "ncclAllReduce");   // first use: connection setup
     if (e != ncclSuccess) return nccl_fail(e, "ncclAllReduce");
@@ -160,6 +156,7 @@ int rd_comm_nranks(const rd_comm* c) { return c ? c->nranks : 0; }
 int rd_comm_destroy(rd_comm* c) {
     if (!c) return RD_OK;
     rd::DeviceGuard g(c->device);
+    if (c->xgmi) xgmi_release(c);
     if (c->comm) {
         if (wait_ready(c, "rd_comm_destroy") == RD_OK) (void)rccl().destroy(c->comm);
         else (void)rccl().abort(c->comm);

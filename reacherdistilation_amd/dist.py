@@ -152,6 +152,72 @@ class RcclComm:
             pass
 
 
+class XgmiComm(RcclComm):
+    """The exchange as one xGMI push kernel (include/reacher_comm.h rd_xcomm_*): every rank
+    exports an uncached exchange buffer, the group all-gathers the IPC handles, every rank maps
+    the others'; an all-reduce then writes this rank's gradient into its slot of every rank's
+    buffer, raises a flag there, waits for all flags and sums the slots in rank order (bitwise
+    the same on every rank).  Created collectively like RcclComm: a failure on any rank (no
+    IPC, a buffer that cannot be mapped) raises on every rank.  `cap` = floats per exchange."""
+
+    def __init__(self, device, group=None, cap: int = 8192):
+        import ctypes
+
+        import torch
+        import torch.distributed as dist
+
+        from . import _native as nat
+        self._lib = nat.load()
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        on_dev = dist.get_backend(group) == "nccl"
+        # 1. every rank: its exchange buffer and IPC handle (+ a success byte)
+        h = ctypes.c_void_p()
+        hb = (ctypes.c_uint8 * 64)()
+        rc = self._lib.rd_xcomm_create(ctypes.byref(h), self.world, self.rank, device.index, int(cap), hb)
+        why = "" if rc == 0 else self._lib.rd_last_error().decode(errors="replace")
+        self.handle = h if rc == 0 else None
+        mine = torch.tensor(list(bytes(hb)) + [1 if rc == 0 else 0], dtype=torch.uint8)
+        if on_dev:
+            mine = mine.to(device)
+        allh = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(allh, mine, group=group)
+        allh = [t.cpu() for t in allh]
+        bad = [r for r, t in enumerate(allh) if int(t[-1]) != 1]
+        if bad:
+            self.close()
+            raise nat.NativeError(f"xGMI exchange: rank(s) {bad} could not export a buffer"
+                                  f"{' (this rank: ' + why + ')' if why else ''}")
+        # 2. every rank maps every other rank's buffer; the group agrees on the outcome
+        flat = (ctypes.c_uint8 * (64 * self.world))(*[b for t in allh for b in t[:64].tolist()])
+        rc = self._lib.rd_xcomm_connect(self.handle, flat)
+        why = "" if rc == 0 else self._lib.rd_last_error().decode(errors="replace")
+        ok = torch.zeros(self.world, dtype=torch.int32)
+        ok[self.rank] = 1 if rc == 0 else 0
+        if on_dev:
+            ok = ok.to(device)
+        dist.all_reduce(ok, group=group)
+        bad = [r for r, v in enumerate(ok.cpu().tolist()) if v != 1]
+        if bad:
+            self.close()
+            raise nat.NativeError(f"xGMI exchange: rank(s) {bad} could not map the peers' buffers"
+                                  f"{' (this rank: ' + why + ')' if why else ''}")
+
+    def check(self):
+        """Raise if an exchange of this rank ever waited past its limit for a peer."""
+        from . import _native as nat
+        nat.check(self._lib.rd_comm_check(self.handle), "rd_comm_check")
+
+    def self_check(self) -> bool:
+        ok = super().self_check()
+        self.check()
+        return ok
+
+
 def checksum(t) -> int:
     """Exact position-weighted checksum of a float32 tensor's bits (int64 arithmetic)."""
     import torch
