@@ -201,3 +201,64 @@ def test_rank0_id_failure_reaches_every_rank():
                        start_method="spawn")
     assert out[0][0] == out[1][0] == "NativeError"
     assert "failed on rank 0" in out[1][1] and "injected failure" in out[0][1]
+
+
+def _xcomm_rank(rank, world, port, out, inject=None):
+    import datetime
+
+    import torch.distributed as dist
+
+    from reacherdistilation_amd import _native as nat
+    from reacherdistilation_amd.dist import XgmiComm
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=30))
+    if inject == "rank1_map":   # every rank exports a buffer; rank 1 cannot map its peer's
+        lib = nat.load()
+        lib.rd_xcomm_create = lambda h, nranks, r, dev, cap, hb: 0
+        lib.rd_xcomm_connect = (lambda c, hs: 1) if rank == 1 else (lambda c, hs: 0)
+        lib.rd_last_error = lambda: b"injected map failure"
+        lib.rd_comm_destroy = lambda c: 0
+    try:
+        XgmiComm(torch.device("cuda", 0))
+        out[rank] = ("created", "")
+    except Exception as e:  # noqa: BLE001
+        out[rank] = (type(e).__name__, str(e))
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="the no-device failure path is exercised on CPU hosts")
+def test_xgmi_comm_failure_reaches_every_rank():
+    """include/reacher_comm.h rd_xcomm_*: two gloo ranks build dist.XgmiComm on a host
+    without a HIP device: neither can export a buffer, the all-gather of the handles carries
+    that, and both raise NativeError naming the ranks -- no rank left waiting."""
+    out = mp.get_context("spawn").Manager().dict()
+    mp.start_processes(_xcomm_rank, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    assert out[0][0] == out[1][0] == "NativeError"
+    assert "[0, 1] could not export" in out[0][1] and "[0, 1] could not export" in out[1][1]
+
+
+def test_xgmi_map_failure_reaches_every_rank():
+    """Rank 1 cannot map rank 0's exchange buffer (injected): the group agrees on the
+    outcome, both ranks raise, and rank 0's message names rank 1."""
+    out = mp.get_context("spawn").Manager().dict()
+    mp.start_processes(_xcomm_rank, args=(2, _free_port(), out, "rank1_map"), nprocs=2, join=True,
+                       start_method="spawn")
+    assert out[0][0] == out[1][0] == "NativeError"
+    assert "[1] could not map" in out[0][1] and "injected map failure" in out[1][1]
+
+
+def test_xgmi_comm_host_contract():
+    """rd_xcomm_* argument errors and a buffer on a missing device fail with a message."""
+    import ctypes
+
+    from reacherdistilation_amd import _native as nat
+    lib = nat.load()
+    h, hb = ctypes.c_void_p(), (ctypes.c_uint8 * 64)()
+    assert lib.rd_xcomm_create(ctypes.byref(h), 9, 0, 0, 5060, hb) != 0     # more than 8 ranks
+    assert b"bad argument" in lib.rd_last_error()
+    assert lib.rd_xcomm_create(ctypes.byref(h), 2, 2, 0, 5060, hb) != 0     # rank out of range
+    assert lib.rd_xcomm_create(ctypes.byref(h), 2, 0, 0, 0, hb) != 0        # no capacity
+    assert lib.rd_xcomm_connect(None, hb) != 0 and lib.rd_comm_check(None) != 0
+    if not torch.cuda.is_available():
+        assert lib.rd_xcomm_create(ctypes.byref(h), 1, 0, 0, 5060, hb) != 0  # no HIP device here
+        assert lib.rd_last_error()
