@@ -41,6 +41,8 @@ class DeviceDataset:
         self.B, self.T, self.epochs = int(batch_size), int(steps_unrolled), int(epochs)
         self._gen = torch.Generator().manual_seed(int(seed))   # host RNG: indices only
         self._mem_slots = []   # ring slots flushed since the last full page (reference data_in_memory)
+        self._zeros = torch.zeros(PDFLAT_SHAPE, dtype=torch.float32, device=self.device)
+        self._with = torch.tensor([[0.0], [1.0]], dtype=torch.float32, device=self.device)   # stepped with t / s
 
     # -- reference interface -------------------------------------------------------------
     def num_episodes(self) -> int:
@@ -49,16 +51,19 @@ class DeviceDataset:
     def write(self, ob, reward=0.0, t_pdflat=None, s_pdflat=None, stepped_with: str = "t"):
         if self.curr_len >= EPISODE_STEPS:
             raise RuntimeError(f"episode already holds {EPISODE_STEPS} steps; flush() first")
-        r = self.curr[self.curr_len]
-        r[F_OB:F_REW] = torch.as_tensor(ob, dtype=torch.float32).reshape(-1)[:OBSPACE_SHAPE].to(self.device)
-        r[F_REW] = reward.reshape(()) if torch.is_tensor(reward) else float(reward)   # device reward: no sync
-        z = torch.zeros(PDFLAT_SHAPE)
-        r[F_T:F_S] = torch.as_tensor(t_pdflat if t_pdflat is not None else z, dtype=torch.float32).reshape(-1).to(
-            self.device)
-        r[F_S:F_WITH] = torch.as_tensor(s_pdflat if s_pdflat is not None else z, dtype=torch.float32).reshape(-1).to(
-            self.device)
-        r[F_WITH] = 1.0 if stepped_with == "s" else 0.0
+        # one concatenation straight into the record (one launch per step; device inputs, as
+        # the drivers pass them, are used in place: no host round trip, no sync)
+        torch.cat((self._field(ob, OBSPACE_SHAPE), self._field(reward, 1), self._field(t_pdflat, PDFLAT_SHAPE),
+                   self._field(s_pdflat, PDFLAT_SHAPE), self._with[1 if stepped_with == "s" else 0]),
+                  out=self.curr[self.curr_len])
         self.curr_len += 1
+
+    def _field(self, x, n):
+        if x is None:
+            return self._zeros[:n]
+        if not (torch.is_tensor(x) and x.device == self.device and x.dtype == torch.float32):
+            x = torch.as_tensor(x, dtype=torch.float32).to(self.device)
+        return x.reshape(-1)[:n]
 
     def flush(self):
         """Close the current episode.  Only complete episodes (EPISODE_STEPS records) enter
@@ -101,15 +106,22 @@ class DeviceDataset:
         n = self.stored()
         if n == 0:
             return
+        steps = torch.arange(self.T)
         for _ in range(self.epochs):
             eps = torch.randint(0, n, (self.B,), generator=self._gen)
             start = int(torch.randint(0, EPISODE_STEPS - self.T + 1, (1,), generator=self._gen))
-            rec = self.ring[eps.to(self.device)]                      # [B, 50, REC]
-            prev = self._prev(rec)[:, start:start + self.T]           # [B, T, 5]
-            win = rec[:, start:start + self.T].transpose(0, 1)        # [T, B, REC]
-            prev = prev.transpose(0, 1)
-            yield (win[..., F_OB:F_REW].contiguous(), win[..., F_T:F_S].contiguous(),
-                   prev[..., :PDFLAT_SHAPE].contiguous(), prev[..., PDFLAT_SHAPE:].contiguous())
+            # ONE gather of the window's records and of their predecessors (the prev fields):
+            # flat record rows [2, T, B] of the ring, built on the host, one copy to the device
+            row = (eps * EPISODE_STEPS)[None, :] + (start + steps)[:, None]          # [T, B]
+            idx = torch.stack((row, (row - 1).clamp_min(0))).to(self.device)
+            g = self.ring.view(-1, REC)[idx]                                       # [2, T, B, REC]
+            prev_t, prev_r = g[1, ..., F_T:F_S], g[1, ..., F_REW:F_REW + 1]
+            if start == 0:   # the first record of an episode has no predecessor: zeros
+                prev_t, prev_r = prev_t.clone(), prev_r.clone()
+                prev_t[0] = 0.0
+                prev_r[0] = 0.0
+            yield (g[0, ..., F_OB:F_REW].contiguous(), g[0, ..., F_T:F_S].contiguous(),
+                   prev_t.contiguous(), prev_r.contiguous())
 
     def bptt_batches(self):
         """The truncated-BPTT variant's windows (reference backup/dataset_bbpt.py:179-193):
