@@ -526,6 +526,8 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
 
     replicas = tr.replicas_identical() if world > 1 else True   # SURVEY §8e checksum
+    if comm is not None and hasattr(comm, "check"):
+        comm.check()   # (xGMI) raise if any exchange of the run waited past its limit for a peer
 
     accum = None
     if args.accum > 1:   # secondary line: one optimiser step (+ all-reduce) per K env-steps

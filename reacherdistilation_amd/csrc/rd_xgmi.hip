@@ -74,7 +74,8 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
     if (threadIdx.x == a.nranks) {
         const uint32_t want = a.epoch * (uint32_t)a.nranks;
         for (uint32_t spins = 0;; ++spins) {
-            if (__hip_atomic_load(a.err + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+            if ((int32_t)(__hip_atomic_load(a.err + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0)
+                break;   // wrap-safe: the count passes 2^32 after ~5e8 exchanges
             if (spins > XG_SPIN_LIMIT) {
                 __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
