@@ -32,6 +32,8 @@ namespace {
 constexpr int XG_BLOCK = 256;
 constexpr int XG_FLAGS_BYTES = 256;                 // flags[2][RD_XG_MAX] (uint32), padded
 constexpr uint32_t XG_SPIN_LIMIT = 1u << 22;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int XG_UNROLL = 8;                        // float4 per thread issued at once: n <= 8,192
 
 struct XgArgs {
     char* buf[RD_XG_MAX];     // every rank's exchange buffer (mapped here)
@@ -54,13 +56,26 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
     const uint32_t par = a.epoch & 1u;
     const int dst = blockIdx.x;                       // one block per destination rank
     // 1. push: this rank's gradient -> slot[rank] of rank dst's buffer
-    {
+    {   // every load is issued before the first store (clamped indices, no branch around a
+        // load): a load -> store loop waited one memory latency per iteration.  Needs n >= 4
+        // for the clamped lanes' t4[0] (smaller n: the scalar tail below alone)
         float* to = slot_of(a.buf[dst], a.cap, par, a.rank);
-        const int64_t n4 = a.n / 4;
-        const float4* s4 = reinterpret_cast<const float4*>(a.grad);
-        float4* t4 = reinterpret_cast<float4*>(to);
-        for (int64_t i = threadIdx.x; i < n4; i += XG_BLOCK) t4[i] = s4[i];
-        for (int64_t i = 4 * n4 + threadIdx.x; i < a.n; i += XG_BLOCK) to[i] = a.grad[i];
+        const int n4 = (int)(a.n / 4);
+        const f32x4* s4 = reinterpret_cast<const f32x4*>(a.grad);
+        f32x4* t4 = reinterpret_cast<f32x4*>(to);
+        f32x4 v[XG_UNROLL];   // a native vector type: HIP's float4 (a union) kept the array in scratch
+#pragma unroll
+        for (int u = 0; u < XG_UNROLL; ++u) {
+            const int i = threadIdx.x + u * XG_BLOCK;
+            v[u] = s4[i < n4 ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < XG_UNROLL; ++u) {   // no branch around a store either: on gfx9 the
+            const int i = threadIdx.x + u * XG_BLOCK;   // store counter is vmcnt, and a store in a
+            t4[i < n4 ? i : 0] = v[u];   // branch waited for every earlier one (one xGMI round
+        }                                // trip each); past n4 a lane rewrites t4[0] = s4[0]
+        for (int i = threadIdx.x + XG_UNROLL * XG_BLOCK; i < n4; i += XG_BLOCK) t4[i] = s4[i];   // n > 8,192
+        for (int64_t i = 4 * (int64_t)n4 + threadIdx.x; i < a.n; i += XG_BLOCK) to[i] = a.grad[i];
     }
     __threadfence_system();   // every thread's stores have landed (acknowledged) ...
     __syncthreads();
@@ -101,8 +116,12 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
     const int64_t lo = per * blockIdx.x, hi = lo + per < a.n ? lo + per : a.n;
     char* me = const_cast<char*>(a.mine);
     for (int64_t i = lo + threadIdx.x; i < hi; i += XG_BLOCK) {
-        float s = slot_of(me, a.cap, par, 0)[i];
-        for (int r = 1; r < a.nranks; ++r) s += slot_of(me, a.cap, par, r)[i];
+        float v[RD_XG_MAX];   // all ranks' values in flight at once (uncached: HBM latency each)
+#pragma unroll
+        for (int r = 0; r < RD_XG_MAX; ++r) v[r] = slot_of(me, a.cap, par, r < a.nranks ? r : 0)[i];
+        float s = v[0];
+#pragma unroll
+        for (int r = 1; r < RD_XG_MAX; ++r) s = r < a.nranks ? s + v[r] : s;   // rank order
         a.grad[i] = s;
     }
 }
