@@ -92,6 +92,20 @@ def test_rollout_gradient_matches_oracle(n, loss):
     assert m.shape == (0, 4)
 
 
+@pytest.mark.parametrize("grid,n", [(7, 3000), (300, 300 * 4 * 64), (257, 20000)])
+def test_gradient_over_explicit_grids(grid, n):
+    """rdd_config.grid sets the workgroups (= partial rows of the column-chunked workspace the
+    reduce sums): few rows, more rows than the 256 a reduce thread sums in its unrolled
+    four-way loop (the remainder path), and a count that is no multiple of 64 -- the same
+    gradient as the oracle; the grid changes only the summation order."""
+    tr = _trainer(n, loss="kl", grid=grid)
+    g, g64, _, _ = _grad_check(tr, "kl", "teacher")
+    ref = _trainer(n, loss="kl")
+    ref.rollout()
+    gr = ref.grad().cpu().numpy()
+    assert np.abs(g - gr).max() <= 1e-5 * np.abs(gr).max()
+
+
 def test_dagger_rollout_and_adam_step():
     n = 4096
     tr = _trainer(n, loss="mse", act="student")
