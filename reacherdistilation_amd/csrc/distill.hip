@@ -1303,6 +1303,9 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     dbg_t = t;
 #endif
                 }
+#ifdef RD_CP_WAIT   // diagnostic: every outstanding slot read has returned before the slot is freed
+                __builtin_amdgcn_s_waitcnt(0);
+#endif
                 publish(flags + 1, ++tiles);
                 STAMP(13);
 #pragma unroll
@@ -1342,6 +1345,9 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     dbg_t = t;
 #endif
                 }
+#ifdef RD_CP_WAIT   // diagnostic: every outstanding slot read has returned before the slot is freed
+                __builtin_amdgcn_s_waitcnt(0);
+#endif
                 publish(flags + 1, ++tiles);
                 STAMP(13);
                 // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
