@@ -58,6 +58,12 @@ FLOP_SPLIT_PER_NET_L2 = 2 * 64 * 64
 PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
 
 
+def default_f32_mode():
+    """The headline runs the library's default f32 mode (DistillConfig.f32_split)."""
+    from reacherdistilation_amd.distill import DistillConfig
+    return "split" if DistillConfig().f32_split else "exact"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,7 +82,7 @@ def parse():
                     help="also time K env-steps per optimiser step (SURVEY §8d: K = 50 = one episode); 0 = skip")
     ap.add_argument("--conv-steps", type=int, default=5000,
                     help="convergence leg: optimiser steps allowed to reach student action-MSE < 1e-3; 0 = skip")
-    ap.add_argument("--f32-mode", default="split", choices=["exact", "split"],
+    ap.add_argument("--f32-mode", default=default_f32_mode(), choices=["exact", "split"],
                     help="f32 hidden-layer products: f32 emulated on bf16 MFMAs by exact 3-piece operand splits "
                          "(include/reacher_distill.h f32_split; default), or every product on the f32 MFMA")
     ap.add_argument("--no-exact-leg", action="store_true",
@@ -284,6 +290,38 @@ def exchange_latency(comm, dev, n=5060, iters=200, warmup=20):
     return {"floats": n, "us": a.elapsed_time(b) * 1e3 / iters, "iters": iters}
 
 
+def _make_comm(kind, dev, world):
+    """A native communicator of `kind` that passed its one-shot self-check on EVERY rank, or
+    (None, reason).  Collective: every rank calls it in the same order."""
+    import torch
+    import torch.distributed as dist
+    c, why = None, ""
+    if kind == "rccl" and dist.get_backend() != "nccl":
+        return None, "the process group is not RCCL (gloo rehearsal)"
+    try:
+        if kind == "rccl":
+            from reacherdistilation_amd.dist import RcclComm
+            c = RcclComm(dev)
+        else:
+            from reacherdistilation_amd.dist import XgmiComm
+            c = XgmiComm(dev)
+        ok = c.self_check()
+        if not ok:
+            why = "self-check sum mismatch"
+    except Exception as e:   # noqa: BLE001  (reported in the line, never silent)
+        ok, why = False, str(e).splitlines()[0][:200]
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return c, ""
+    if c is not None:
+        try:
+            c.close()
+        except Exception:   # noqa: BLE001
+            pass
+    return None, why or "failed its self-check on another rank"
+
+
 def strong_leg(wl, total, sdt, split, dev, lr, steps, warmup, rank, world, comm, settle_ms=0.0):
     """BASELINE config 4's own wording, "262 144 envs sharded across 8 x MI355X": the
     workload's fixed global batch split over the ranks (`n_envs_global`, contiguous shards,
@@ -416,48 +454,41 @@ def main():
             dist.init_process_group(backend)
 
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
-    # N > 1 over RCCL: the gradient all-reduce is issued by the native step on the trainer's
-    # stream (include/reacher_comm.h); RD_COMM=torch keeps torch.distributed's collective.
-    # A communicator that fails its one-shot self-check is dropped for torch's (reported).
+    # N > 1: the gradient all-reduce is issued by the native step on the trainer's stream
+    # (include/reacher_comm.h).  The default is the native RCCL communicator (north star: one
+    # RCCL all-reduce over xGMI per optimiser step); RD_COMM=xgmi binds the one-kernel xGMI push
+    # exchange instead, RD_COMM=torch keeps torch.distributed's collective.  Whatever runs, BOTH
+    # native exchanges are timed beside it (`exchange.rccl_us`, `exchange.xgmi_us`, or the
+    # reason one is unavailable).  A communicator failing its one-shot self-check is dropped
+    # for the next one (reported in config.collective).
     comm, collective = None, "none"
     exchange = None
-    want = os.environ.get("RD_COMM", "xgmi")
-    if world > 1 and want == "xgmi":
-        # the default: the one-shot xGMI push (include/reacher_comm.h rd_xcomm_*); falls back
-        # to the native RCCL communicator, then torch's collective, and says which one ran
-        from reacherdistilation_amd.dist import XgmiComm
-        try:
-            comm = XgmiComm(dev)
-            ok = comm.self_check()
-        except Exception as e:   # noqa: BLE001  (reported in the line, never silent)
-            print(f"xGMI exchange unavailable ({e}); trying RCCL", file=sys.stderr)
-            comm, ok = None, False
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 1:
-            collective = "xgmi push (native, one kernel, trainer stream)"
-            exchange = exchange_latency(comm, dev)
-        else:
-            comm = None
-            want = "rccl"
-    if world > 1 and comm is None:
-        collective = "torch.distributed"
-        if dist.get_backend() == "nccl" and want == "rccl":
-            from reacherdistilation_amd.dist import RcclComm
-            try:
-                comm = RcclComm(dev)
-                ok = comm.self_check()
-            except Exception as e:   # noqa: BLE001  (reported in the line, never silent)
-                print(f"RCCL communicator unavailable ({e}); using torch.distributed", file=sys.stderr)
-                comm, ok = None, False
-            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if int(flag.item()) == 1:
-                collective = "rccl (native, trainer stream)"
-                exchange = exchange_latency(comm, dev)
-            else:
-                comm = None
-                collective = "torch.distributed (native RCCL self-check failed)"
+    want = os.environ.get("RD_COMM", "rccl")
+    if world > 1:
+        exchange = {}
+        cands = {}
+        for kind in ("rccl", "xgmi"):
+            c, why = _make_comm(kind, dev, world)
+            if c is None:
+                exchange[f"{kind}_us"] = f"unavailable: {why}"
+                continue
+            exchange[f"{kind}_us"] = exchange_latency(c, dev)["us"]
+            cands[kind] = c
+        exchange["floats"] = 5060
+        exchange["timing"] = "200 back-to-back in-place all-reduces of 5,060 floats, HIP events, trainer stream"
+        order = [want] + [k for k in ("rccl", "xgmi") if k != want] if want != "torch" else []
+        for kind in order:
+            if kind in cands:
+                comm = cands.pop(kind)
+                collective = ("rccl (native, trainer stream)" if kind == "rccl"
+                              else "xgmi push (native, one kernel, trainer stream)")
+                break
+        for c in cands.values():   # the one not bound
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            c.close()
+        if comm is None:
+            collective = "torch.distributed" + (" (native exchanges unavailable)" if want != "torch" else "")
     wl = WORKLOADS[args.workload]
     n = args.envs_per_gpu or wl["envs"]
     sdt = wl.get("student_dtype", "f32")

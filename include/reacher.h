@@ -32,6 +32,7 @@ extern "C" {
 
 #define RD_OK 0
 #define RD_EINVAL (-100000)
+#define RD_ECOMM (-100001)   /* a gradient exchange failed (reacher_comm.h); the step's update was skipped */
 
 /* reset draw sources */
 #define RD_RESET_PHILOX 0   /* Philox4x32-10(seed, env_base + i, episode): synthetic targets */

@@ -62,11 +62,20 @@ int rd_comm_destroy(rd_comm* c);
  * each rank writes its n <= cap floats into its slot of every rank's buffer (one block per
  * destination, all xGMI links at once), raises a flag there, waits for every flag in its own
  * buffer and sums the slots in rank order -- so every rank gets bitwise the same sum.  At most
- * 8 ranks (one node).  rd_comm_check() returns nonzero if an exchange ever waited past its
- * limit (~4 s) for a peer.  The reference's exchange it replaces: MpiAdam's Allreduce(SUM)
- * (backup/student_rollout.py:658-659,709). */
+ * 8 ranks (one node).
+ * Failure: a wait that does not see a peer within timeout_s (wall clock) FAILS the
+ * communicator on every rank: the kernel leaves the buffer unsummed, raises this rank's error
+ * word and poisons every peer's buffer, so a peer that arrives later fails its exchange too
+ * instead of completing it alone.  A trainer with the communicator bound skips the Adam update
+ * of a failed exchange (no replica applies a partial sum) and its next rdd_step /
+ * rdd_allreduce_grad / counter read returns RD_ECOMM; rd_comm_check() returns RD_ECOMM without
+ * synchronising.  A failed communicator fails every later exchange: destroy it.  (A peer that
+ * completes within the last poll of the deadline can still have summed while this rank gave
+ * up: with the default 60 s limit that window is a poll interval; the replica checksum,
+ * DistillTrainer.replicas_identical, detects it.)  The reference's exchange it replaces:
+ * MpiAdam's Allreduce(SUM) (backup/student_rollout.py:658-659,709). */
 #define RD_XCOMM_HANDLE_BYTES 64
-int rd_xcomm_create(rd_comm** out, int nranks, int rank, int device, int64_t cap, uint8_t* handle);
+int rd_xcomm_create(rd_comm** out, int nranks, int rank, int device, int64_t cap, double timeout_s, uint8_t* handle);
 int rd_xcomm_connect(rd_comm* c, const uint8_t* handles);
 int rd_comm_check(rd_comm* c);
 

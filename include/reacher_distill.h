@@ -62,6 +62,10 @@ typedef struct {
                                 1: the K = 64 hidden-layer products of the f32 nets (both
                                 layer 2s; the f32 student's dH1) as f32 emulated on bf16
                                 MFMAs with three-piece operand splits (see below)        */
+    int32_t group_envs;      /* envs per producer/consumer group of the rollout: 0 = auto
+                                (64, or 32/16 when the batch cannot give every wave pair a
+                                64-env group); 16, 32 or 64 fixes it.  Changes only the
+                                order of the gradient's summation                         */
 } rdd_config;
 
 /* Student precision.  RDD_DTYPE_F32: every product exact f32 (v_mfma_f32_16x16x4_f32).

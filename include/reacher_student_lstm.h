@@ -49,7 +49,15 @@ typedef struct {
                                       {w lo, w hi, S, 4t + k/4}, key = seed), w = row_base + b */
     uint64_t seed;
     int64_t row_base;              /* global index of this rank's window 0                  */
+    int32_t kernels;               /* 0 = automatic kernel selection; RDL_KERNELS_* bits force
+                                      the general path (same results, tests compare them)    */
 } rdl_config;
+
+/* rdl_config.kernels: by default at most 32 windows run the whole recurrence / BPTT as one
+ * persistent launch each and at most 2,048 rows run the head as one launch; these bits keep
+ * the per-step recurrence launches / the per-layer head GEMMs at any size. */
+#define RDL_KERNELS_STEP_RECURRENCE 1
+#define RDL_KERNELS_LAYER_HEAD 2
 
 typedef struct rdl_trainer rdl_trainer;
 

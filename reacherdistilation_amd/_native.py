@@ -47,7 +47,7 @@ SIGNATURES = {
     "rd_comm_allreduce_f32": (INT, [P, P, I64, P]),
     "rd_comm_nranks": (INT, [P]),
     "rd_comm_destroy": (INT, [P]),
-    "rd_xcomm_create": (INT, [ctypes.POINTER(P), INT, INT, INT, I64, P]),
+    "rd_xcomm_create": (INT, [ctypes.POINTER(P), INT, INT, INT, I64, ctypes.c_double, P]),
     "rd_xcomm_connect": (INT, [P, P]),
     "rd_comm_check": (INT, [P]),
 }

@@ -1,8 +1,12 @@
 """Build the native library in-tree: reacherdistilation_amd/libreacher.so (gfx950).
 
-hipcc compiles the HIP kernels and the C ABI straight to a shared object; nothing is
-JIT-compiled at import time and nothing goes to a cache outside the repo, so the .so
-travels with the repo snapshot to the GPU box.
+hipcc compiles each HIP / C++ source to an object (in parallel), then links the shared
+object; nothing is JIT-compiled at import time and nothing goes to a cache outside the repo,
+so the .so travels with the repo snapshot to the GPU box.
+
+The product build has no run-time knobs: diagnostic and ablation paths (the consumer-side
+env step, forced group sizes, the LSTM's per-step path selection for timing, ...) exist only
+in `build_variant` builds, selected by -D macros.
 """
 from __future__ import annotations
 
@@ -11,17 +15,21 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libreacher.so")
+OBJ = os.path.join(HERE, "build")
 ARCH = os.environ.get("RD_OFFLOAD_ARCH", "gfx950")
 
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 # -O3; keep IEEE f32 semantics (no -ffast-math): parity tolerances are stated for it.
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wall",
-         "-Wno-unused-function", "-Werror=return-type", "-munsafe-fp-atomics", "-ldl"]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Werror",
+          "-Wno-unused-function", "-munsafe-fp-atomics"]
+LDFLAGS = ["-shared", f"--offload-arch={ARCH}", "-ldl"]
+FLAGS = CFLAGS + LDFLAGS   # one-command form (resource_usage, scripts)
 
 
 def sources():
@@ -40,37 +48,64 @@ def up_to_date():
     return all(os.path.getmtime(p) <= t for p in deps())
 
 
-def build(force: bool = False, verbose: bool = True, extra=()):
-    if not force and up_to_date():
-        return LIB
-    cmd = [HIPCC, *FLAGS, *extra, "-o", LIB + ".tmp", *sources()]
+def _jobs():
+    return max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+
+
+def _link(out, opts=(), verbose=True):
+    """Compile every source with `opts` in parallel, link `out` (atomically replaced)."""
+    tag = os.path.splitext(os.path.basename(out))[0]
+    odir = os.path.join(OBJ, tag)
+    os.makedirs(odir, exist_ok=True)
+    srcs = sources()
+    objs = [os.path.join(odir, os.path.basename(s) + ".o") for s in srcs]
+
+    def cc(pair):
+        s, o = pair
+        cmd = [HIPCC, *CFLAGS, *opts, "-c", "-o", o, s]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        return cmd, r
+
+    with ThreadPoolExecutor(_jobs()) as ex:
+        results = list(ex.map(cc, zip(srcs, objs)))
+    for cmd, r in results:
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        if r.returncode:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise subprocess.CalledProcessError(r.returncode, cmd)
+    cmd = [HIPCC, *LDFLAGS, "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build(force: bool = False, verbose: bool = True, extra=()):
+    if not force and up_to_date():
+        return LIB
+    return _link(LIB, tuple(extra), verbose)
 
 
 def resource_usage():
     """Print per-kernel VGPR/SGPR/LDS/occupancy (hipcc -Rpass-analysis)."""
-    cmd = [HIPCC, *FLAGS, "-Rpass-analysis=kernel-resource-usage", "-o", "/dev/null", *sources()]
-    subprocess.call(cmd)
+    for s in sources():
+        subprocess.call([HIPCC, *CFLAGS, "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/dev/null", s])
 
 
 def build_stamps():
     """Diagnostic build with per-wave phase stamps (scripts/stamps.py); never the product."""
-    out = os.path.join(HERE, "libreacher_stamps.so")
-    subprocess.check_call([HIPCC, *FLAGS, "-DRD_STAMPS", "-o", out, *sources()])
-    return out
+    return _link(os.path.join(HERE, "libreacher_stamps.so"), ("-DRD_STAMPS",))
 
 
 def build_variant(name, *defines):
-    """Diagnostic/ablation build (e.g. RD_ABL_TANH, or a compiler flag such as
-    -fno-slp-vectorize) as libreacher_<name>.so; never the product."""
-    out = os.path.join(HERE, f"libreacher_{name}.so")
-    opts = [d if d.startswith("-") else f"-D{d}" for d in defines]
-    subprocess.check_call([HIPCC, *FLAGS, *opts, "-o", out, *sources()])
-    return out
+    """Diagnostic/ablation build as libreacher_<name>.so; never the product.  Macros:
+    RD_DIAG_KNOBS (the measurement-only environment variables RDD_GROUP_ENVS, RDM_ROWS,
+    RDL_PR_DBG), RD_CP_VARIANT (the consumer-side env step, RDD_PHYS=consumer), RD_ABL_*,
+    or a compiler flag such as -fno-slp-vectorize."""
+    opts = tuple(d if d.startswith("-") else f"-D{d}" for d in defines)
+    return _link(os.path.join(HERE, f"libreacher_{name}.so"), opts)
 
 
 if __name__ == "__main__":

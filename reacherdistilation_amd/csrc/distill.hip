@@ -33,6 +33,7 @@
 #include <new>
 
 #include "../../include/reacher_distill.h"
+#include "rd_comm_impl.h"
 #include "rd_common.h"
 #include "rd_physics.h"
 
@@ -130,6 +131,7 @@ struct ReduceArgs {
     float lr, b1, b2, eps;
     float* simg;       // student LDS image, refreshed with every updated parameter
     int img_kind;      // IMG_F32 / IMG_SPLIT / IMG_BF16
+    const uint32_t* xerr;   // bound exchange's failure word (xGMI) or null: nonzero = skip Adam
 };
 
 #ifndef RDD_RED_COLS   // diagnostic builds may change the reduce blocking (A/B)
@@ -1527,6 +1529,13 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
 // Sum the rollout's per-workgroup partials (fixed order: deterministic), then TF1 Adam.
 __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
     __shared__ float part[RED_ROWS][RED_COLS];
+    if (a.adam && a.xerr && __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        // the gradient exchange before this update failed (reacher_comm.h): no replica applies
+        // a partial sum; the step is reported by the host readers (ctl[13]) and rdd_step
+        a.adam = 0;
+        a.bump_opt = 0;
+        if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl[13] = 1u;
+    }
     const uint32_t C = a.ctl[4], S = a.ctl[5];
     const float b1p = __uint_as_float(a.ctl[6]), b2p = __uint_as_float(a.ctl[7]);
     const int col = threadIdx.x & (RED_COLS - 1), row = threadIdx.x / RED_COLS;
@@ -1649,12 +1658,16 @@ namespace {
 // (measured: c3 = one 64-env group per pair 39.6 us vs 41.9 with 32-env groups); below
 // that a pair's tiles run serially while most CUs idle, so small batches use 32- or 16-env
 // groups over more pairs (c2, 4,096 envs: 19.1 us per launch vs 35.4 with 64-env groups).
-// RDD_GROUP_ENVS=16|32|64 overrides (measurement only).
-int group_envs(int64_t n, int pairs_total) {
+// rdd_config.group_envs = 16|32|64 fixes it (tests: the group size changes only the
+// summation order); diagnostic builds (RD_DIAG_KNOBS) also read RDD_GROUP_ENVS.
+int group_envs(int64_t n, int pairs_total, int fixed) {
+#ifdef RD_DIAG_KNOBS
     if (const char* e = getenv("RDD_GROUP_ENVS")) {
         const int v = atoi(e);
         if (v == 16 || v == 32 || v == 64) return v;
     }
+#endif
+    if (fixed) return fixed;
     if (n >= (int64_t)GROUP * pairs_total) return 64;
     if (n >= (int64_t)32 * pairs_total) return 32;
     return 16;
@@ -1674,17 +1687,14 @@ int image_floats(int kind, bool student) {
 // Which wave of a pair steps the envs: the producer, which computed the
 // actions and holds the state.  The consumer-side variant balances the roles better (c5
 // 39.7 vs 43.4 us, c4 split 92.1 vs 93.6 us) but its env step is not reproducible run to run
-// with the bf16 MFMA kernels: now and then the envs of lanes 48..63 of one group come out
-// different, although the actions and states they start from are verified identical
-// (scripts/det_check.py, det_probe2.py).  RDD_PHYS=consumer selects it for
-// measurement only.
-bool consumer_physics(bool bs, int64_t groups_per_pair) {
-    if (const char* e = getenv("RDD_PHYS")) {
-        if (!strcmp(e, "consumer")) return true;
-    }
-    (void)bs; (void)groups_per_pair;
-    return false;
+// with the bf16 MFMA kernels, so it is not in the product library: only a
+// diagnostic build (-DRD_CP_VARIANT) instantiates it, selected there by RDD_PHYS=consumer.
+#ifdef RD_CP_VARIANT
+bool consumer_physics() {
+    const char* e = getenv("RDD_PHYS");
+    return e && !strcmp(e, "consumer");
 }
+#endif
 
 int grid_for(int64_t n, int gs, int cap) {
     const int64_t want = ((n + gs - 1) / gs + PAIRS - 1) / PAIRS;   // one group per pair at least
@@ -1713,6 +1723,7 @@ ReduceArgs reduce_args(const rdd_trainer* t, int reduce, int adam, int accum) {
     a.eps = t->cfg.eps;
     a.simg = t->simg;
     a.img_kind = student_kind(t);
+    a.xerr = rd_comm_device_err(t->comm);
     return a;
 }
 
@@ -1738,18 +1749,18 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     int grid = t->grid;   // <= t->ws_rows, the partial rows the workspace holds
     a.gs = t->gs;
     if (obs_in) {
-        a.gs = group_envs(n_obs, t->ws_rows * PAIRS);
+        a.gs = group_envs(n_obs, t->ws_rows * PAIRS, t->cfg.group_envs);
         grid = grid_for(n_obs, a.gs, t->ws_rows);
     }
     t->last_grid = grid;
     const bool bs = t->cfg.student_dtype == RDD_DTYPE_BF16, spl = t->cfg.f32_split != 0;
-    const int64_t groups = (a.n + a.gs - 1) / a.gs;
-    const bool cp = consumer_physics(bs, groups / ((int64_t)grid * PAIRS));
-    void (*k)(RolloutArgs) = nullptr;
-    if (cp) k = bs ? (spl ? rollout_kernel<true, true, true> : rollout_kernel<true, false, true>)
-                   : (spl ? rollout_kernel<false, true, true> : rollout_kernel<false, false, true>);
-    else k = bs ? (spl ? rollout_kernel<true, true, false> : rollout_kernel<true, false, false>)
-                : (spl ? rollout_kernel<false, true, false> : rollout_kernel<false, false, false>);
+    void (*k)(RolloutArgs) = bs ? (spl ? rollout_kernel<true, true, false> : rollout_kernel<true, false, false>)
+                                : (spl ? rollout_kernel<false, true, false> : rollout_kernel<false, false, false>);
+#ifdef RD_CP_VARIANT
+    if (consumer_physics())
+        k = bs ? (spl ? rollout_kernel<true, true, true> : rollout_kernel<true, false, true>)
+               : (spl ? rollout_kernel<false, true, true> : rollout_kernel<false, false, true>);
+#endif
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
     return RD_OK;
@@ -1783,7 +1794,8 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
         (cfg->act_with != RDD_ACT_TEACHER && cfg->act_with != RDD_ACT_STUDENT) || !(cfg->lr > 0) ||
         cfg->grid < 0 || cfg->metrics_len < 0 || (cfg->stagger != 0 && cfg->stagger != 1) ||
         (cfg->student_dtype != RDD_DTYPE_F32 && cfg->student_dtype != RDD_DTYPE_BF16) || cfg->accum_steps < 0 ||
-        (cfg->f32_split != 0 && cfg->f32_split != 1))
+        (cfg->f32_split != 0 && cfg->f32_split != 1) ||
+        (cfg->group_envs != 0 && cfg->group_envs != 16 && cfg->group_envs != 32 && cfg->group_envs != 64))
         return rd::set_error(RD_EINVAL, "rdd_create: bad config");
     rd::DeviceGuard g(device);
     RD_HIP(g.err, "rdd_create: hipSetDevice");
@@ -1796,7 +1808,7 @@ int rdd_create(rdd_trainer** out, const rdd_config* cfg, int device, void* hip_s
     t->stream = (hipStream_t)hip_stream;
     const int cap = cfg->grid > 0 ? cfg->grid : num_cus(device);
     t->ws_rows = cap;
-    t->gs = group_envs(cfg->n_envs, cap * PAIRS);
+    t->gs = group_envs(cfg->n_envs, cap * PAIRS, cfg->group_envs);
     t->grid = grid_for(cfg->n_envs, t->gs, cap);
     t->last_grid = t->grid;
     const size_t netf = P_TOT + 2 * OBD;
@@ -1892,8 +1904,17 @@ int rdd_rollout(rdd_trainer* t) {
     return launch_reduce(t, 1, 0);
 }
 
+// a bound exchange that failed earlier (reacher_comm.h): no further steps on this trainer
+static int comm_ok(const rdd_trainer* t, const char* what) {
+    if (rd_comm_failed(t->comm))
+        return rd::set_error(RD_ECOMM, "%s: a gradient exchange of this trainer failed (its optimiser step was "
+                                       "skipped); destroy the communicator", what);
+    return RD_OK;
+}
+
 int rdd_apply(rdd_trainer* t) {
     if (!t) return rd::set_error(RD_EINVAL, "rdd_apply: null handle");
+    if (int rc = comm_ok(t, "rdd_apply")) return rc;
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_apply: hipSetDevice");
     return launch_reduce(t, 0, 1);
@@ -1901,6 +1922,7 @@ int rdd_apply(rdd_trainer* t) {
 
 int rdd_step(rdd_trainer* t) {
     if (!t) return rd::set_error(RD_EINVAL, "rdd_step: null handle");
+    if (int rc = comm_ok(t, "rdd_step")) return rc;
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_step: hipSetDevice");
     if (int rc = launch_rollout(t)) return rc;
@@ -1919,6 +1941,7 @@ int rdd_bind_comm(rdd_trainer* t, rd_comm* comm) {
 
 int rdd_allreduce_grad(rdd_trainer* t) {
     if (!t || !t->comm) return rd::set_error(RD_EINVAL, "rdd_allreduce_grad: no communicator bound");
+    if (int rc = comm_ok(t, "rdd_allreduce_grad")) return rc;
     return rd_comm_allreduce_f32(t->comm, t->grad, P_TOT, t->stream);
 }
 
@@ -2000,6 +2023,7 @@ static int read_ctl(rdd_trainer* t, uint32_t (&c)[16], const char* what) {
     RD_HIP(hipMemcpyAsync(c, t->ctl, sizeof(c), hipMemcpyDeviceToHost, t->stream), what);
     RD_HIP(hipStreamSynchronize(t->stream), what);
     if (c[8]) return rd::set_error(RD_EINVAL, "%s: a rollout's producer/consumer hand-off timed out", what);
+    if (c[13]) return rd::set_error(RD_ECOMM, "%s: a gradient exchange failed; its optimiser step was skipped", what);
     return RD_OK;
 }
 

@@ -15,7 +15,12 @@
 // 2(N-1) hops).  Slots and flags are double-buffered by epoch parity: a rank can only start
 // exchange e+2 (same parity) after every rank raised its flag of e+1, which each raises only
 // after it finished summing e, so no slot is overwritten while it is read.  A wait that does
-// not see a peer within ~4 s raises the device error word (rd_comm_check) and the kernel ends.
+// does not see a peer before its deadline (rd_xcomm_create's timeout_s, wall clock) FAILS
+// the communicator: it raises the error words (device + host-visible), POISONS every rank's
+// buffer (so a peer that arrives late fails its exchange too instead of completing it alone),
+// and leaves the gradient as it was.  The trainer's Adam kernel reads the device word and
+// skips its update, so no replica applies a partial sum; rdd_step / rd_comm_check report it.
+// A poisoned communicator fails every later exchange at once (destroy it, make a new one).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -30,8 +35,8 @@
 namespace {
 
 constexpr int XG_BLOCK = 256;
-constexpr int XG_FLAGS_BYTES = 256;                 // flags[2][RD_XG_MAX] (uint32), padded
-constexpr uint32_t XG_SPIN_LIMIT = 1u << 22;
+constexpr int XG_FLAGS_BYTES = 256;                 // flags[2][RD_XG_MAX] (uint32), the poison word, padded
+constexpr int XG_POISON = 2 * RD_XG_MAX;            // uint32 index of the poison word in the flags area
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int XG_UNROLL = 8;                        // float4 per thread issued at once: n <= 8,192
 
@@ -41,25 +46,48 @@ struct XgArgs {
     float* grad;              // in/out: this rank's n floats
     int64_t n, cap;
     int nranks, rank;
+    int vec;                  // n >= 4 and grad 16-B aligned: the float4 push
     uint32_t epoch;
-    uint32_t* err;            // [0] a wait timed out, [1] blocks that finished pushing (all epochs)
+    uint64_t deadline_ticks;  // wall-clock limit of each wait, in s_memrealtime ticks (100 MHz)
+    uint32_t* err;            // [0] this communicator failed, [1] blocks that finished pushing (all epochs)
+    volatile uint32_t* herr;  // host-visible copy of err[0]
 };
 
 __device__ __forceinline__ uint32_t* flags_of(char* b, uint32_t parity) {
     return reinterpret_cast<uint32_t*>(b) + parity * RD_XG_MAX;
 }
+__device__ __forceinline__ uint32_t* poison_of(char* b) { return reinterpret_cast<uint32_t*>(b) + XG_POISON; }
 __device__ __forceinline__ float* slot_of(char* b, int64_t cap, uint32_t parity, int r) {
     return reinterpret_cast<float*>(b + XG_FLAGS_BYTES) + ((int64_t)parity * RD_XG_MAX + r) * cap;
+}
+
+__device__ __forceinline__ bool poisoned(const XgArgs& a) {
+    return __hip_atomic_load(poison_of(const_cast<char*>(a.mine)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
+
+// this rank gives up: error words, and the poison word in every rank's buffer
+__device__ void fail(const XgArgs& a) {
+    __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *a.herr = 1u;
+    for (int r = 0; r < a.nranks; ++r)
+        __hip_atomic_store(poison_of(a.buf[r]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
 }
 
 __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
     const uint32_t par = a.epoch & 1u;
     const int dst = blockIdx.x;                       // one block per destination rank
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = poisoned(a) || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (bad) {   // a peer (or this rank) failed an earlier exchange: fail this one, touch nothing
+        if (threadIdx.x == 0) fail(a);
+        return;
+    }
     // 1. push: this rank's gradient -> slot[rank] of rank dst's buffer
-    {   // every load is issued before the first store (clamped indices, no branch around a
-        // load): a load -> store loop waited one memory latency per iteration.  Needs n >= 4
-        // for the clamped lanes' t4[0] (smaller n: the scalar tail below alone)
-        float* to = slot_of(a.buf[dst], a.cap, par, a.rank);
+    float* to = slot_of(a.buf[dst], a.cap, par, a.rank);
+    if (a.vec) {   // every load is issued before the first store (clamped indices, no branch
+        // around a load): a load -> store loop waited one memory latency per iteration
         const int n4 = (int)(a.n / 4);
         const f32x4* s4 = reinterpret_cast<const f32x4*>(a.grad);
         f32x4* t4 = reinterpret_cast<f32x4*>(to);
@@ -76,6 +104,8 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
         }                                // trip each); past n4 a lane rewrites t4[0] = s4[0]
         for (int i = threadIdx.x + XG_UNROLL * XG_BLOCK; i < n4; i += XG_BLOCK) t4[i] = s4[i];   // n > 8,192
         for (int64_t i = 4 * (int64_t)n4 + threadIdx.x; i < a.n; i += XG_BLOCK) to[i] = a.grad[i];
+    } else {       // n < 4 or a gradient that is not 16-B aligned
+        for (int64_t i = threadIdx.x; i < a.n; i += XG_BLOCK) to[i] = a.grad[i];
     }
     __threadfence_system();   // every thread's stores have landed (acknowledged) ...
     __syncthreads();
@@ -85,14 +115,18 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
         __hip_atomic_fetch_add(a.err + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     // 3. wait (a) until every block of this kernel has pushed (the in-place sums must not
-    // reach a block's source) and (b) for every rank's slot in this rank's buffer
+    // reach a block's source) and (b) for every rank's slot in this rank's buffer; every wait
+    // ends at the wall-clock deadline, or early once the buffer is poisoned
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == a.nranks) {
         const uint32_t want = a.epoch * (uint32_t)a.nranks;
-        for (uint32_t spins = 0;; ++spins) {
+        for (;;) {
             if ((int32_t)(__hip_atomic_load(a.err + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0)
                 break;   // wrap-safe: the count passes 2^32 after ~5e8 exchanges
-            if (spins > XG_SPIN_LIMIT) {
-                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.deadline_ticks || poisoned(a)) {
+                bad = 1;
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -100,16 +134,22 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
     }
     if (threadIdx.x < a.nranks) {
         const uint32_t* f = flags_of(const_cast<char*>(a.mine), par) + threadIdx.x;
-        for (uint32_t spins = 0;; ++spins) {
+        for (;;) {
             if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == a.epoch) break;
-            if (spins > XG_SPIN_LIMIT) {
-                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.deadline_ticks || poisoned(a)) {
+                bad = 1;
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
     }
     __syncthreads();
+    if (threadIdx.x == 0 && !bad) bad = poisoned(a);   // a peer gave up on this exchange meanwhile
+    __syncthreads();
+    if (bad) {   // the gradient keeps its input; the Adam kernel sees err[0] and skips
+        if (threadIdx.x == 0) fail(a);
+        return;
+    }
     __threadfence_system();
     // 4. this block's share of the columns: the sum over ranks in rank order
     const int64_t per = (a.n + gridDim.x - 1) / gridDim.x;
@@ -129,6 +169,9 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
 }  // namespace
 
 int xgmi_allreduce(rd_comm* c, float* buf, int64_t n, hipStream_t stream) {
+    if (rd_comm_failed(c))
+        return rd::set_error(RD_ECOMM, "rd_comm_allreduce_f32: rank %d: the exchange failed earlier (a peer did not "
+                                       "arrive within %.1f s); destroy the communicator", c->rank, c->timeout_s);
     if (n > c->cap) return rd::set_error(RD_EINVAL, "rd_comm_allreduce_f32: %lld floats > the exchange slots' %lld",
                                          (long long)n, (long long)c->cap);
     for (int r = 0; r < c->nranks; ++r)
@@ -141,8 +184,11 @@ int xgmi_allreduce(rd_comm* c, float* buf, int64_t n, hipStream_t stream) {
     a.cap = c->cap;
     a.nranks = c->nranks;
     a.rank = c->rank;
+    a.vec = n >= 4 && ((uintptr_t)buf & 15u) == 0;
     a.epoch = ++c->epoch;
+    a.deadline_ticks = (uint64_t)(c->timeout_s * 1e8);   // s_memrealtime: 100 MHz
     a.err = c->err;
+    a.herr = c->herr;
     hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(c->nranks), dim3(XG_BLOCK), 0, stream, a);
     RD_HIP(hipGetLastError(), "xgmi_allreduce_kernel launch");
     return RD_OK;
@@ -155,14 +201,17 @@ void xgmi_release(rd_comm* c) {
     }
     if (c->mine) (void)hipFree(c->mine);
     if (c->err) (void)hipFree(c->err);
+    if (c->herr) (void)hipHostFree((void*)c->herr);
     c->mine = nullptr;
     c->err = nullptr;
+    c->herr = nullptr;
 }
 
 extern "C" {
 
-int rd_xcomm_create(rd_comm** out, int nranks, int rank, int device, int64_t cap, uint8_t* handle) {
-    if (!out || !handle || nranks <= 0 || nranks > RD_XG_MAX || rank < 0 || rank >= nranks || cap <= 0)
+int rd_xcomm_create(rd_comm** out, int nranks, int rank, int device, int64_t cap, double timeout_s, uint8_t* handle) {
+    if (!out || !handle || nranks <= 0 || nranks > RD_XG_MAX || rank < 0 || rank >= nranks || cap <= 0 ||
+        !(timeout_s > 0 && timeout_s < 1e6))
         return rd::set_error(RD_EINVAL, "rd_xcomm_create: bad argument (at most %d ranks)", RD_XG_MAX);
     rd::DeviceGuard g(device);
     RD_HIP(g.err, "rd_xcomm_create: hipSetDevice");
@@ -172,13 +221,20 @@ int rd_xcomm_create(rd_comm** out, int nranks, int rank, int device, int64_t cap
     c->nranks = nranks;
     c->rank = rank;
     c->device = device;
+    c->timeout_s = timeout_s;
     c->cap = (cap + 3) / 4 * 4;   // 16-B aligned slots
     const size_t bytes = XG_FLAGS_BYTES + sizeof(float) * 2 * RD_XG_MAX * (size_t)c->cap;
-    static_assert(2 * RD_XG_MAX * sizeof(uint32_t) <= XG_FLAGS_BYTES, "flag words");
+    static_assert((XG_POISON + 1) * sizeof(uint32_t) <= XG_FLAGS_BYTES, "flag words");
     hipError_t e = hipExtMallocWithFlags((void**)&c->mine, bytes, hipDeviceMallocUncached);
     if (e == hipSuccess) e = hipMemset(c->mine, 0, bytes);
     if (e == hipSuccess) e = hipMalloc((void**)&c->err, 2 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->err, 0, 2 * sizeof(uint32_t));
+    void* hp = nullptr;   // pinned, coherent host word the kernel raises on failure
+    if (e == hipSuccess) e = hipHostMalloc(&hp, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) {
+        c->herr = (volatile uint32_t*)hp;
+        *c->herr = 0u;
+    }
     hipIpcMemHandle_t h;
     if (e == hipSuccess) e = hipIpcGetMemHandle(&h, c->mine);
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -214,12 +270,10 @@ int rd_xcomm_connect(rd_comm* c, const uint8_t* handles) {
 int rd_comm_check(rd_comm* c) {
     if (!c) return rd::set_error(RD_EINVAL, "rd_comm_check: null handle");
     if (!c->xgmi) return RD_OK;
-    rd::DeviceGuard g(c->device);
-    RD_HIP(g.err, "rd_comm_check: hipSetDevice");
-    uint32_t v = 0;
-    RD_HIP(hipMemcpy(&v, c->err, sizeof v, hipMemcpyDeviceToHost), "rd_comm_check: read");
-    if (v) return rd::set_error(RD_EINVAL, "rd_comm_check: rank %d: an exchange waited past its limit for a peer",
-                                c->rank);
+    if (rd_comm_failed(c))
+        return rd::set_error(RD_ECOMM, "rd_comm_check: rank %d: an exchange failed (a peer did not arrive within "
+                                       "%.1f s, or a peer failed first); its optimiser step was skipped", c->rank,
+                             c->timeout_s);
     return RD_OK;
 }
 

@@ -1034,26 +1034,24 @@ hipError_t colsum(rdl_trainer* t, const float* src, int64_t M, int N, int64_t ld
 
 #define RDL_CK(call, what) RD_HIP((call), what)
 
-// the persistent recurrence kernels for batches of at most PR_ROWS windows; RDL_PERSIST=0
-// keeps the per-step launches (measurement)
-int pr_dbg() {   // RDL_PR_DBG: bit 0 skip the exchange loads, 1 the MFMAs, 2 the barrier (timing only)
+// the persistent recurrence kernels for batches of at most PR_ROWS windows, and the
+// one-launch head for at most HF_MAX_ROWS rows; rdl_config.kernels can select the per-step /
+// per-layer launches instead (RDL_KERNELS_*: tests compare the two paths)
+int pr_dbg() {   // diagnostic builds: RDL_PR_DBG bit 0 skips the exchange loads, 1 the MFMAs, 2 the barrier
+#ifdef RD_DIAG_KNOBS
     const char* e = getenv("RDL_PR_DBG");
     return e ? atoi(e) : 0;
+#else
+    return 0;
+#endif
 }
 
-// the one-launch head forward for at most HF_MAX_ROWS rows; RDL_FUSED_HEAD=0 keeps the five GEMMs
-bool fused_head(int64_t R) {
-    if (const char* e = getenv("RDL_FUSED_HEAD")) {
-        if (!strcmp(e, "0")) return false;
-    }
-    return R <= HF_MAX_ROWS;
+bool fused_head(const rdl_trainer* t, int64_t R) {
+    return !(t->cfg.kernels & RDL_KERNELS_LAYER_HEAD) && R <= HF_MAX_ROWS;
 }
 
-bool persistent(int64_t B) {
-    if (const char* e = getenv("RDL_PERSIST")) {
-        if (!strcmp(e, "0")) return false;
-    }
-    return B <= PR_ROWS;
+bool persistent(const rdl_trainer* t, int64_t B) {
+    return !(t->cfg.kernels & RDL_KERNELS_STEP_RECURRENCE) && B <= PR_ROWS;
 }
 
 // forward over all T steps of B windows.  out_pdflat: where the head's output goes (the
@@ -1068,7 +1066,7 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
                        t->X, R, B, train ? t->cfg.keep_prob : 1.0f, t->cfg.seed, t->cfg.row_base,
                        (const uint32_t*)t->ctl, t->bar);
     RDL_CK(hipGetLastError(), "rdl inputs_kernel");
-    if (persistent(B)) {   // Zx, then all T recurrent steps in one launch (it writes the step-0 state rows)
+    if (persistent(t, B)) {   // Zx, then all T recurrent steps in one launch (it writes the step-0 state rows)
         RDL_CK(mm(t, (int)R, G4, XI, t->X, XLD, 0, P + OFF_WL, G4, 0, t->Z, G4, P + OFF_BL), "rdl gemm Zx");
         hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
                            (const float*)t->Z, state0, t->G, t->Cs, t->H, (int)B, T, t->bar, pr_dbg());
@@ -1105,7 +1103,7 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     }
     // head over all T x B rows (student_nn.py:42-46)
     const float* Hc = t->H + B * U;
-    if (fused_head(R)) {
+    if (fused_head(t, R)) {
         hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)((R + HF_ROWS - 1) / HF_ROWS)), dim3(256), 0, t->stream, Hc, P,
                            t->A1, t->A2, t->A3, t->A4, out_pdflat, R);
         RDL_CK(hipGetLastError(), "rdl head_fwd_kernel");
@@ -1137,7 +1135,7 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
         RDL_CK(hipGetLastError(), "rdl metrics_kernel");
     }
     const float* Hc = t->H + B * U;
-    if (fused_head(R)) {   // the head backward as two launches (head_bwd_kernel + fixed-order reduce)
+    if (fused_head(t, R)) {   // the head backward as two launches (head_bwd_kernel + fixed-order reduce)
         const unsigned nwg = (unsigned)((R + HF_ROWS - 1) / HF_ROWS);
         hipLaunchKernelGGL(head_bwd_kernel, dim3(nwg), dim3(256), 0, t->stream, Hc, P, (const float*)t->A1,
                            (const float*)t->A2, (const float*)t->A3, (const float*)t->A4, (const float*)t->dY, t->dHh,
@@ -1168,7 +1166,7 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     }
     // BPTT (the gate buffer Z is reused for dz: the forward keeps activations in G)
     float* dZl = t->Z;
-    if (persistent(B)) {
+    if (persistent(t, B)) {
         hipLaunchKernelGGL(lstm_bptt_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
                            (const float*)t->dHh, (const float*)t->G, (const float*)t->Cs, dZl, t->bpart, g + OFF_BL,
                            prev, t->qbuf, (int)B, T, t->bar, pr_dbg());
@@ -1216,8 +1214,8 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     RDL_CK(mm2(t, ga(XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4),
                ga(U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4)),
            "rdl dWl x | h");
-    if (!persistent(B)) RDL_CK(colsum(t, dZl, R, G4, G4, g + OFF_BL), "rdl dbl");   // else summed in BPTT
-    if (persistent(B)) {   // from the BPTT kernel's dbl and Q = prev^T dz: one launch
+    if (!persistent(t, B)) RDL_CK(colsum(t, dZl, R, G4, G4, g + OFF_BL), "rdl dbl");   // else summed in BPTT
+    if (persistent(t, B)) {   // from the BPTT kernel's dbl and Q = prev^T dz: one launch
         hipLaunchKernelGGL(dense32_grad_kernel, dim3(160), dim3(256), 0, t->stream, P, (const float*)t->qbuf, g);
         RDL_CK(hipGetLastError(), "rdl dense32_grad_kernel");
     } else {
@@ -1247,7 +1245,8 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     if (!out || !cfg) return rd::set_error(RD_EINVAL, "rdl_create: null argument");
     if ((cfg->loss != RDL_LOSS_MSE && cfg->loss != RDL_LOSS_KL) || !(cfg->lr > 0) || cfg->steps <= 0 ||
         cfg->max_windows <= 0 || (int64_t)cfg->steps * cfg->max_windows > ((int64_t)1 << 22) || cfg->metrics_len < 0 ||
-        !(cfg->keep_prob > 0.0f && cfg->keep_prob <= 1.0f) || cfg->row_base < 0)
+        !(cfg->keep_prob > 0.0f && cfg->keep_prob <= 1.0f) || cfg->row_base < 0 ||
+        (cfg->kernels & ~(RDL_KERNELS_STEP_RECURRENCE | RDL_KERNELS_LAYER_HEAD)))
         return rd::set_error(RD_EINVAL, "rdl_create: bad config");
     rd::DeviceGuard dg(device);
     RD_HIP(dg.err, "rdl_create: hipSetDevice");
@@ -1457,7 +1456,7 @@ int rdl_get_counter(rdl_trainer* t, int64_t* opt_steps) {
     RD_HIP(hipStreamSynchronize(t->stream), "rdl_get_counter");
     if (b[2])   // a persistent launch gave up at a grid barrier (workgroups not co-resident)
         return rd::set_error(RD_EINVAL, "rdl: a persistent recurrence launch timed out at its grid barrier; "
-                                        "the steps since are invalid (RDL_PERSIST=0 avoids the persistent kernels)");
+                                        "the steps since are invalid (rdl_config.kernels = RDL_KERNELS_STEP_RECURRENCE avoids the persistent kernels)");
     *opt_steps = c[0];
     return RD_OK;
 }

@@ -570,9 +570,11 @@ namespace {
 // step 21.8 us vs 35.8 us with 64-row blocks, 1,024 rows 27.2 vs 37.4 us).  Every workgroup
 // writes a 104 KB partial row, so once the 16-row blocks would occupy more than half of the
 // workgroups the 64-row kernel wins (4,096 rows: 51.2 vs 42.4 us).
-// RDM_ROWS=16|64 overrides (measurement only).
+// Diagnostic builds (RD_DIAG_KNOBS): RDM_ROWS=16|64 overrides (measurement only).
 bool use_small_rows(int64_t n, int grid) {
+#ifdef RD_DIAG_KNOBS
     if (const char* e = getenv("RDM_ROWS")) return atoi(e) == 16;
+#endif
     return (n + 15) / 16 <= grid / 2;
 }
 

@@ -158,9 +158,12 @@ class XgmiComm(RcclComm):
     the others'; an all-reduce then writes this rank's gradient into its slot of every rank's
     buffer, raises a flag there, waits for all flags and sums the slots in rank order (bitwise
     the same on every rank).  Created collectively like RcclComm: a failure on any rank (no
-    IPC, a buffer that cannot be mapped) raises on every rank.  `cap` = floats per exchange."""
+    IPC, a buffer that cannot be mapped) raises on every rank.  `cap` = floats per exchange;
+    `timeout` = seconds an exchange waits for a peer before the communicator fails on every
+    rank (the bound trainer then skips that optimiser step and raises NativeError on its next
+    call; include/reacher_comm.h)."""
 
-    def __init__(self, device, group=None, cap: int = 8192):
+    def __init__(self, device, group=None, cap: int = 8192, timeout: float = 60.0):
         import ctypes
 
         import torch
@@ -178,7 +181,8 @@ class XgmiComm(RcclComm):
         # 1. every rank: its exchange buffer and IPC handle (+ a success byte)
         h = ctypes.c_void_p()
         hb = (ctypes.c_uint8 * 64)()
-        rc = self._lib.rd_xcomm_create(ctypes.byref(h), self.world, self.rank, device.index, int(cap), hb)
+        rc = self._lib.rd_xcomm_create(ctypes.byref(h), self.world, self.rank, device.index, int(cap),
+                                       float(timeout), hb)
         why = "" if rc == 0 else self._lib.rd_last_error().decode(errors="replace")
         self.handle = h if rc == 0 else None
         mine = torch.tensor(list(bytes(hb)) + [1 if rc == 0 else 0], dtype=torch.uint8)
@@ -208,7 +212,8 @@ class XgmiComm(RcclComm):
                                   f"{' (this rank: ' + why + ')' if why else ''}")
 
     def check(self):
-        """Raise if an exchange of this rank ever waited past its limit for a peer."""
+        """Raise if an exchange of this rank failed (a peer missed the deadline, or a peer
+        failed first); no synchronisation."""
         from . import _native as nat
         nat.check(self._lib.rd_comm_check(self.handle), "rd_comm_check")
 

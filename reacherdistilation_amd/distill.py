@@ -35,7 +35,7 @@ class RddConfig(ctypes.Structure):
     _fields_ = [("n_envs", I64), ("n_envs_global", I64), ("env_base", I64), ("seed", U64),
                 ("loss", I32), ("act_with", I32), ("lr", F32), ("beta1", F32), ("beta2", F32),
                 ("eps", F32), ("grid", I32), ("metrics_len", I32), ("stagger", I32),
-                ("student_dtype", I32), ("accum_steps", I32), ("f32_split", I32)]
+                ("student_dtype", I32), ("accum_steps", I32), ("f32_split", I32), ("group_envs", I32)]
 
 
 nat.register({
@@ -84,7 +84,9 @@ class DistillConfig:
     stagger: bool = True               # spread episode phases over the batch (reacher_distill.h)
     student_dtype: str = "f32"         # "f32" | "bf16" (BASELINE config 5: bf16 student MLP)
     accum_steps: int = 1               # env steps per optimiser step (1 = the reference)
-    f32_split: bool = False            # f32 hidden layers on bf16 MFMAs via exact 3-piece splits (reacher_distill.h)
+    f32_split: bool = True             # f32 hidden layers on bf16 MFMAs via exact 3-piece splits (reacher_distill.h);
+    #                                    False: every product on the f32 MFMA (same tolerances, ~20 % slower)
+    group_envs: int = 0                # envs per rollout group: 0 = auto, 16 | 32 | 64 fixed (summation order only)
 
 
 class DistillTrainer:
@@ -111,7 +113,8 @@ class DistillTrainer:
                       seed=cfg.seed % 2 ** 64, loss=LOSSES[cfg.loss], act_with=ACTORS[cfg.act_with], lr=cfg.lr,
                       beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps, grid=cfg.grid, metrics_len=cfg.metrics_len,
                       stagger=int(bool(cfg.stagger)), student_dtype=DTYPES[cfg.student_dtype],
-                      accum_steps=max(1, int(cfg.accum_steps)), f32_split=int(bool(cfg.f32_split)))
+                      accum_steps=max(1, int(cfg.accum_steps)), f32_split=int(bool(cfg.f32_split)),
+                      group_envs=int(cfg.group_envs))
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             nat.check(self._lib.rdd_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,

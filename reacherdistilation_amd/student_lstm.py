@@ -35,7 +35,8 @@ LOSSES = {"mse": 0, "kl": 1}
 
 class RdlConfig(ctypes.Structure):
     _fields_ = [("loss", I32), ("lr", F32), ("beta1", F32), ("beta2", F32), ("eps", F32), ("steps", I32),
-                ("max_windows", I32), ("metrics_len", I32), ("keep_prob", F32), ("seed", U64), ("row_base", I64)]
+                ("max_windows", I32), ("metrics_len", I32), ("keep_prob", F32), ("seed", U64), ("row_base", I64),
+                ("kernels", I32)]
 
 
 nat.register({
@@ -86,6 +87,8 @@ class StudentLstmConfig:
     seed: int = 0
     init_seed: int = 3
     metrics_len: int = 4096
+    step_recurrence: bool = False     # force the per-step recurrence launches (else: persistent at <= 32 windows)
+    layer_head: bool = False          # force the per-layer head GEMMs (else: one launch at <= 2,048 rows)
 
 
 class StudentLstmTrainer:
@@ -102,7 +105,8 @@ class StudentLstmTrainer:
         c = RdlConfig(loss=LOSSES[self.cfg.loss], lr=self.cfg.lr, beta1=self.cfg.beta1, beta2=self.cfg.beta2,
                       eps=self.cfg.eps, steps=self.T, max_windows=int(self.cfg.max_windows),
                       metrics_len=self.cfg.metrics_len, keep_prob=self.cfg.keep_prob,
-                      seed=self.cfg.seed % 2 ** 64, row_base=int(row_base))
+                      seed=self.cfg.seed % 2 ** 64, row_base=int(row_base),
+                      kernels=int(bool(self.cfg.step_recurrence)) | 2 * int(bool(self.cfg.layer_head)))
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             nat.check(self._lib.rdl_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,

@@ -214,7 +214,7 @@ def _xcomm_rank(rank, world, port, out, inject=None):
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=30))
     if inject == "rank1_map":   # every rank exports a buffer; rank 1 cannot map its peer's
         lib = nat.load()
-        lib.rd_xcomm_create = lambda h, nranks, r, dev, cap, hb: 0
+        lib.rd_xcomm_create = lambda h, nranks, r, dev, cap, timeout, hb: 0
         lib.rd_xcomm_connect = (lambda c, hs: 1) if rank == 1 else (lambda c, hs: 0)
         lib.rd_last_error = lambda: b"injected map failure"
         lib.rd_comm_destroy = lambda c: 0
@@ -254,11 +254,11 @@ def test_xgmi_comm_host_contract():
     from reacherdistilation_amd import _native as nat
     lib = nat.load()
     h, hb = ctypes.c_void_p(), (ctypes.c_uint8 * 64)()
-    assert lib.rd_xcomm_create(ctypes.byref(h), 9, 0, 0, 5060, hb) != 0     # more than 8 ranks
+    assert lib.rd_xcomm_create(ctypes.byref(h), 9, 0, 0, 5060, 60.0, hb) != 0     # more than 8 ranks
     assert b"bad argument" in lib.rd_last_error()
-    assert lib.rd_xcomm_create(ctypes.byref(h), 2, 2, 0, 5060, hb) != 0     # rank out of range
-    assert lib.rd_xcomm_create(ctypes.byref(h), 2, 0, 0, 0, hb) != 0        # no capacity
+    assert lib.rd_xcomm_create(ctypes.byref(h), 2, 2, 0, 5060, 60.0, hb) != 0     # rank out of range
+    assert lib.rd_xcomm_create(ctypes.byref(h), 2, 0, 0, 0, 60.0, hb) != 0        # no capacity
     assert lib.rd_xcomm_connect(None, hb) != 0 and lib.rd_comm_check(None) != 0
     if not torch.cuda.is_available():
-        assert lib.rd_xcomm_create(ctypes.byref(h), 1, 0, 0, 5060, hb) != 0  # no HIP device here
+        assert lib.rd_xcomm_create(ctypes.byref(h), 1, 0, 0, 5060, 60.0, hb) != 0  # no HIP device here
         assert lib.rd_last_error()

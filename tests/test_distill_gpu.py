@@ -307,14 +307,13 @@ def test_accumulated_mse_normalises_over_k_rollouts():
     torch.testing.assert_close(a.grad() * K, b.grad(), rtol=1e-6, atol=1e-9)
 
 
-def test_group_size_changes_only_the_summation_order(monkeypatch):
+def test_group_size_changes_only_the_summation_order():
     """16-, 32- and 64-env groups (chosen by batch size) step every env
     identically (bitwise) and give the same gradient up to f32 reordering of the sums."""
     n = 3000
     out = {}
     for gs in (16, 32, 64):
-        monkeypatch.setenv("RDD_GROUP_ENVS", str(gs))
-        tr = _trainer(n, loss="kl")
+        tr = _trainer(n, loss="kl", group_envs=gs)
         tr.rollout()
         out[gs] = (tr.grad().cpu().numpy().astype(np.float64), tr.env_state().cpu().numpy())
         tr.close()

@@ -284,7 +284,7 @@ def test_driver_restores_and_saves_the_student(tmp_path):
 
 
 @pytest.mark.parametrize("T,B,with_state", [(10, 20, False), (10, 32, True), (1, 7, True), (3, 1, False)])
-def test_persistent_recurrence_matches_per_step_launches(monkeypatch, T, B, with_state):
+def test_persistent_recurrence_matches_per_step_launches(T, B, with_state):
     """B <= 32: the whole forward recurrence and the whole BPTT each run as one persistent
     launch (lstm_fwd_persist_kernel / lstm_bptt_persist_kernel).  Forward: bitwise the per-step
     kernels (same MFMA sequence and cell arithmetic); gradient: the dh sums over the 800 gate
@@ -293,8 +293,7 @@ def test_persistent_recurrence_matches_per_step_launches(monkeypatch, T, B, with
     st = np.random.RandomState(4).uniform(-.5, .5, (2, B, 200)).astype(np.float32) if with_state else None
     out = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("RDL_PERSIST", mode)
-        tr = _trainer(T, B, "kl")
+        tr = _trainer(T, B, "kl", step_recurrence=mode == "0")
         y, fin = tr.forward(_t(ob), _t(prev), None if st is None else _t(st))
         g = tr.rollout(_t(ob), _t(prev), _t(t), None if st is None else _t(st)).cpu().numpy()
         out[mode] = (y.cpu().numpy(), fin[0].cpu().numpy(), fin[1].cpu().numpy(), g, tr.params().cpu().numpy())
@@ -310,18 +309,17 @@ def test_persistent_recurrence_matches_per_step_launches(monkeypatch, T, B, with
 
 
 @pytest.mark.parametrize("T,B", [(10, 20), (3, 130), (1, 5)])
-def test_fused_head_matches_the_layer_gemms(monkeypatch, T, B):
+def test_fused_head_matches_the_layer_gemms(T, B):
     """At most 2,048 rows: the head's forward is one launch (head_fwd_kernel) and its backward
     two (head_bwd_kernel + a fixed-order reduce).  Same MFMA k order and epilogues as the
     per-layer GEMMs for the activations and the data gradients, so the outputs, dh_head and
     everything BPTT derives from it (the LSTM's gradients) are bitwise those of
-    RDL_FUSED_HEAD=0; the head's weight gradients sum the rows in per-16-row partials, so they
+    layer_head=True; the head's weight gradients sum the rows in per-16-row partials, so they
     agree to 1e-5 of their largest entry."""
     ob, prev, t = _batch(T, B, 21 + B)
     out = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("RDL_FUSED_HEAD", mode)
-        tr = _trainer(T, B, "mse")
+        tr = _trainer(T, B, "mse", layer_head=mode == "0")
         y, _ = tr.forward(_t(ob), _t(prev))
         g = tr.rollout(_t(ob), _t(prev), _t(t)).cpu().numpy()
         out[mode] = (y.cpu().numpy(), g)

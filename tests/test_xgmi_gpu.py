@@ -43,8 +43,10 @@ def _rank(rank, world, port, out):
         dist.destroy_process_group()
         return
     sums = []
-    for k, n in enumerate([5060, 5060, 7, 5060, 4096]):   # both parities, a ragged tail
-        x = torch.arange(n, dtype=torch.float32, device=dev) % 97 + 1000.0 * rank + k
+    for k, n in enumerate([5060, 5060, 7, 5060, 4096, 1, 3, 5059]):   # both parities, ragged tails, n < 4
+        base = torch.zeros(n + 1, dtype=torch.float32, device=dev)
+        x = base[1:] if k == 7 else base[:n]   # k = 7: a gradient that is not 16-B aligned (scalar push)
+        x.copy_(torch.arange(n, dtype=torch.float32, device=dev) % 97 + 1000.0 * rank + k)
         comm.allreduce_(x)
         want = (torch.arange(n, dtype=torch.float32, device=dev) % 97) * world + 1000.0 * (world * (world - 1) // 2) \
             + k * world
@@ -90,3 +92,70 @@ def test_xgmi_exchange_two_ranks():
     np.testing.assert_allclose(np.concatenate([st0, st1], axis=1), ref.env_state().cpu().numpy(), atol=1e-4)
     np.testing.assert_allclose(m0[:, 3] + m1[:, 3], ref.metrics(STEPS)[:, 3])
     ref.close()
+
+
+TIMEOUT_S, LATE_S = 2.0, 6.0
+
+
+def _late_rank(rank, world, port, out):
+    """Rank 1 reaches its third step LATE_S seconds after rank 0 (host skew past the
+    exchange's TIMEOUT_S deadline): rank 0's exchange times out and poisons both buffers, rank
+    1's then fails on the poison; neither applies Adam, and both raise on their next step."""
+    import time
+
+    import torch.distributed as dist
+
+    from reacherdistilation_amd._native import NativeError
+    from reacherdistilation_amd.dist import XgmiComm
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", rank % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = XgmiComm(dev, timeout=TIMEOUT_S)
+    except NativeError as e:
+        out[rank] = ("skip", str(e))
+        dist.destroy_process_group()
+        return
+    tr = DistillTrainer(DistillConfig(n_envs_global=4096, seed=7, lr=1e-3), device=dev, rank=rank,
+                        world_size=world, comm=comm)
+    for _ in range(2):
+        tr.step()
+    torch.cuda.synchronize(dev)
+    before = tr.student_params().cpu().numpy()
+    dist.barrier()
+    if rank == 1:
+        time.sleep(LATE_S)
+    t0 = time.perf_counter()
+    tr.step()            # rank 0: times out after TIMEOUT_S; rank 1: fails on the poison
+    torch.cuda.synchronize(dev)
+    waited = time.perf_counter() - t0
+    after = tr.student_params().cpu().numpy()
+    errs = []
+    for call in (tr.step, comm.check, tr.counters):
+        try:
+            call()
+            errs.append(None)
+        except NativeError as e:
+            errs.append(str(e))
+    out[rank] = ("ok", before, after, errs, waited)
+    dist.barrier()
+    tr.close()
+    comm.close()
+    dist.destroy_process_group()
+
+
+def test_xgmi_exchange_late_peer_fails_both_ranks_and_skips_adam():
+    out = mp.get_context("spawn").Manager().dict()
+    mp.start_processes(_late_rank, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
+    r0, r1 = out[0], out[1]
+    if r0[0] == "skip" or r1[0] == "skip":
+        pytest.skip(f"xGMI exchange unavailable here: {r0[1] if r0[0] == 'skip' else r1[1]}")
+    for r in (r0, r1):
+        _, before, after, errs, _ = r
+        assert np.array_equal(before, after)          # Adam skipped: parameters unchanged
+        assert all(e is not None for e in errs), errs  # rdd_step, rd_comm_check, the counters
+    assert np.array_equal(r0[1], r1[1])
+    assert TIMEOUT_S * 0.8 <= r0[4] < LATE_S + TIMEOUT_S   # rank 0 waited for its deadline
+    assert r1[4] < TIMEOUT_S                               # rank 1 failed at once on the poison
