@@ -15,14 +15,17 @@ and its truncated-BPTT training step.
   Dropout mask on ob (tf.nn.dropout, keep_prob): Philox4x32-10 keyed like the MLP student's
   (refnet_np.dropout) with counter word 3 = 4 t + q, so the oracle reproduces it exactly.
 
-Parity status: UNPINNED beyond the formulas (TensorFlow absent; no reference test covers the
-LSTM); checked by finite differences in tests/test_lstm_oracle.py.
+Parity status: the cell (forward), its constants and the kl loss gradient are pinned to the
+reference's logged GraphDef; the backward's building blocks -- bptt / cell_backward (the
+cell's generated BPTT over T = 2 steps), refnet_np.dense_backward, tanh_grad -- are pinned to
+the graph's own TF-generated gradients of all 30 ApplyAdam inputs (tests/test_graph_pins.py);
+this 200-unit composition is checked by finite differences in tests/test_lstm_oracle.py.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from oracle.refnet_np import M32, philox4x32_10
+from oracle.refnet_np import M32, dense_backward, philox4x32_10, tanh_grad
 
 UNITS = 200
 IN_X = 11 + 32
@@ -132,43 +135,69 @@ def loss_and_dout(pdflat, t_pdflat, loss, n_global):
     return L, d.reshape(T, B, 4), sq
 
 
+def cell_backward(s, dh, dc_next):
+    """Backward of one TF1 LSTMCell step (the cell's generated gradient ops: TanhGrad,
+    SigmoidGrad, the f + forget_bias Add, Split_grad = concat of the gate gradients).
+    s: that step's cache (gi, gj, gf, go = the gate activations, c = c_t, cprev = c_{t-1});
+    dh: dL/dh_t (all consumers), dc_next: dL/dc_t from step t+1.
+    Returns (dz [B, 4U] in (i, j, f, o) order, dc_prev = dL/dc_{t-1} through this step)."""
+    gi, gj, gf, go = s["gi"], s["gj"], s["gf"], s["go"]
+    tc = np.tanh(s["c"])
+    dc = dh * go * (1 - tc ** 2) + dc_next
+    dzo = dh * tc * go * (1 - go)
+    dzi = dc * gj * gi * (1 - gi)
+    dzj = dc * gi * (1 - gj ** 2)
+    dzf = dc * s["cprev"] * gf * (1 - gf)
+    return np.concatenate([dzi, dzj, dzf, dzo], 1), dc * gf
+
+
+def bptt(steps, Wl, dh_out):
+    """Back-propagation through time of the TF1 LSTMCell over T steps: steps[t] = the cache of
+    step t (x, hprev, cprev, gates, c), dh_out[t] = dL/dh_t from the step's non-recurrent
+    consumers (the head).  Returns (dWl, dbl, [dL/dx_t], dL/dc_0, dL/dh_0): the cell kernel's
+    gradient is the sum over steps of [x_t, h_{t-1}]^T dz_t (TF: MatMul_grad per step, AddN),
+    its bias's the sum of dz_t (BiasAddGrad, AddN).  Pinned to the reference graph's own
+    generated BPTT (adam/gradients/AddN_6, AddN_7; tests/test_graph_pins.py)."""
+    T = len(steps)
+    nx = steps[0]["x"].shape[1]
+    dWl, dbl = np.zeros_like(Wl), np.zeros(Wl.shape[1])
+    dxs = [None] * T
+    dh_next = np.zeros_like(np.asarray(steps[-1]["hprev"], np.float64))
+    dc_next = np.zeros_like(dh_next)
+    for t in range(T - 1, -1, -1):
+        s = steps[t]
+        dz, dc_next = cell_backward(s, dh_out[t] + dh_next, dc_next)
+        xin = np.concatenate([s["x"], s["hprev"]], 1)
+        dW, db, dxin = dense_backward(xin, dz, Wl)
+        dWl += dW
+        dbl += db
+        dxs[t], dh_next = dxin[:, :nx], dxin[:, nx:]
+    return dWl, dbl, dxs, dc_next, dh_next
+
+
 def backward(p, fw, dout):
     W = unpack(p)
     g = {k: np.zeros(s) for k, (_, s) in LAYOUT.items()}
     C = fw["cache"]
     T = len(C["x"])
-    B = dout.shape[1]
-    dh_next = np.zeros((B, UNITS))
-    dc_next = np.zeros((B, UNITS))
-    for t in range(T - 1, -1, -1):
+    dh_out = []
+    for t in range(T):   # the head of every step (no recurrence through it)
         a = C["acts"][t]
-        dz = dout[t]
-        g["W5"] += a[4].T @ dz
-        g["b5"] += dz.sum(0)
-        da = dz @ W["W5"].T
+        gW, gb, da = dense_backward(a[4], dout[t], W["W5"])
+        g["W5"] += gW
+        g["b5"] += gb
         for k in range(4, 0, -1):
-            dz = da * (1 - a[k] ** 2)
-            g[f"W{k}"] += a[k - 1].T @ dz
-            g[f"b{k}"] += dz.sum(0)
-            da = dz @ W[f"W{k}"].T
-        dh = da + dh_next
-        gi, gj, gf, go, c = C["gi"][t], C["gj"][t], C["gf"][t], C["go"][t], C["c"][t]
-        tc = np.tanh(c)
-        dc = dh * go * (1 - tc ** 2) + dc_next
-        dzo = dh * tc * go * (1 - go)
-        dzi = dc * gj * gi * (1 - gi)
-        dzj = dc * gi * (1 - gj ** 2)
-        dzf = dc * C["cprev"][t] * gf * (1 - gf)
-        dc_next = dc * gf
-        dzl = np.concatenate([dzi, dzj, dzf, dzo], 1)
-        xin = np.concatenate([C["x"][t], C["hprev"][t]], 1)
-        g["Wl"] += xin.T @ dzl
-        g["bl"] += dzl.sum(0)
-        dxin = dzl @ W["Wl"].T
-        dh_next = dxin[:, IN_X:]
-        dp = dxin[:, 11:IN_X]
-        g["Wp"] += fw["prev"][t].T @ dp
-        g["bp"] += dp.sum(0)
+            gW, gb, da = dense_backward(a[k - 1], tanh_grad(a[k], da), W[f"W{k}"])
+            g[f"W{k}"] += gW
+            g[f"b{k}"] += gb
+        dh_out.append(da)
+    steps = [dict(x=C["x"][t], hprev=C["hprev"][t], cprev=C["cprev"][t], gi=C["gi"][t], gj=C["gj"][t],
+                  gf=C["gf"][t], go=C["go"][t], c=C["c"][t]) for t in range(T)]
+    g["Wl"], g["bl"], dxs, _, _ = bptt(steps, W["Wl"], dh_out)
+    for t in range(T):   # the prev_pdflat projection feeds x_t[11:43]
+        gW, gb, _ = dense_backward(fw["prev"][t], dxs[t][:, 11:IN_X], W["Wp"])
+        g["Wp"] += gW
+        g["bp"] += gb
     return np.concatenate([g[k].ravel() for k in LAYOUT])
 
 

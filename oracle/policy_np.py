@@ -18,9 +18,11 @@ Parity status: PINNED to the reference's own GraphDefs (src/~/reacher/data/viz/1
 files, parsed and evaluated by oracle/tfgraph.py; goldens tests/golden/graph_golden.npz):
 the MlpPolicy forward incl. the observation filter (pi/pol/concat on the teacher's own
 initial weights and on seeded weights), the kl loss and TF's gradient of it, the Adam
-constants and beta-power schedule (tests/test_graph_pins.py).  The backward is pinned
-through the forward: it is checked against finite differences of the pinned forward
-(tests/test_policy_oracle.py).  TensorFlow/baselines themselves are not installed.
+constants and beta-power schedule (tests/test_graph_pins.py).  The backward is built from
+refnet_np.dense_backward / tanh_grad, which are pinned to the TF-generated gradients of the
+logged LSTM graph (adam/gradients/*: MatMul_grad, BiasAddGrad, TanhGrad), and is checked
+against finite differences of the pinned forward (tests/test_policy_oracle.py).
+TensorFlow/baselines themselves are not installed.
 """
 from __future__ import annotations
 
@@ -125,14 +127,14 @@ def loss_and_dmean(fs, ft, loss, n_global):
 
 
 def backward(p, fs, dmean, dls):
+    """The MlpPolicy backward from the pinned building blocks (refnet_np.dense_backward =
+    TF's MatMul_grad + BiasAddGrad, refnet_np.tanh_grad = TanhGrad)."""
+    from oracle.refnet_np import dense_backward, tanh_grad
     q = unpack(p)
-    g = dict(W3=fs["h2"].T @ dmean, b3=dmean.sum(0), ls=np.asarray(dls, np.float64))
-    dz2 = (dmean @ q["W3"].T) * (1 - fs["h2"] ** 2)
-    g["W2"] = fs["h1"].T @ dz2
-    g["b2"] = dz2.sum(0)
-    dz1 = (dz2 @ q["W2"].T) * (1 - fs["h1"] ** 2)
-    g["W1"] = fs["z"].T @ dz1
-    g["b1"] = dz1.sum(0)
+    g = dict(ls=np.asarray(dls, np.float64))
+    g["W3"], g["b3"], dh2 = dense_backward(fs["h2"], dmean, q["W3"])
+    g["W2"], g["b2"], dh1 = dense_backward(fs["h1"], tanh_grad(fs["h2"], dh2), q["W2"])
+    g["W1"], g["b1"], _ = dense_backward(fs["z"], tanh_grad(fs["h1"], dh1), q["W1"])
     return pack(g["W1"], g["b1"], g["W2"], g["b2"], g["W3"], g["b3"], g["ls"])
 
 
