@@ -22,10 +22,11 @@ import os
 
 import torch
 
-from .config import LSTM_BATCH_SIZE, STEPS_UNROLLED, TOTAL_EPISODES
+from .config import LSTM_BATCH_SIZE, MAX_CAPACITY, STEPS_UNROLLED, TOTAL_EPISODES
 from .dataset import DeviceDataset
 from .distill import DistillConfig, DistillTrainer
 from .driver_env import DriverEnv, episode_loss
+from .pages import PageStore
 from .policy import TeacherAgent
 from .student_lstm import StudentLstmConfig, StudentLstmTrainer
 
@@ -44,8 +45,11 @@ def _restore(st, restore: bool, path: str | None, log):
 def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EPISODES, loss: str = "kl",
           lr: float = 1e-3, keep_prob: float = 1.0, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
           warmup_episodes: int = 2 * LSTM_BATCH_SIZE, student_path: str | None = None, log=print,
-          gym_env: bool = False):
-    """Returns (student trainer, dataset, per-episode summed training loss).  With
+          gym_env: bool = False, store_dir: str | None = None, pool: str = "reference"):
+    """Returns (student trainer, dataset, per-episode summed training loss).  ``store_dir``:
+    the dataset's page directory (lstm_train.py:104-109); episodes are dumped to it every
+    MAX_CAPACITY episodes (:200) and its stored pages join the training pool (dataset.py:
+    164-177); ``pool="ring"`` draws windows uniformly from the device ring instead.  With
     ``student_path`` the student (params + Adam slots) is restored from it when ``restore``
     (lstm_train.py:102-107) and saved to it after every episode (:199).  Env I/O on the device
     (driver_env.DriverEnv; gym_env=True through the gym-API env), window losses read once per
@@ -55,7 +59,8 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
     tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
     st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
                                               steps=STEPS_UNROLLED, max_windows=LSTM_BATCH_SIZE), device=device)
-    dataset = DeviceDataset(device=device, seed=seed, batch_size=LSTM_BATCH_SIZE, steps_unrolled=STEPS_UNROLLED)
+    dataset = DeviceDataset(device=device, seed=seed, batch_size=LSTM_BATCH_SIZE, steps_unrolled=STEPS_UNROLLED,
+                            store=PageStore(store_dir) if store_dir else None, pool=pool)
     _restore(st, restore, student_path, log)
     losses = []
     if not train:
@@ -95,6 +100,8 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
             losses.append(total_loss)
             opt_steps = 0
             dataset.flush()
+            if dataset.store is not None and dataset.num_episodes() % MAX_CAPACITY == 0:
+                dataset.dump()          # lstm_train.py:200
             if student_path:
                 st.save(student_path)   # saver.save every episode (lstm_train.py:199)
             if dataset.num_episodes() >= episodes:
@@ -105,7 +112,7 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
 def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EPISODES, loss: str = "kl",
                lr: float = 1e-3, keep_prob: float = 1.0, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
                warmup_episodes: int = 2 * LSTM_BATCH_SIZE, student_path: str | None = None, log=print,
-               gym_env: bool = False):
+               gym_env: bool = False, store_dir: str | None = None, pool: str = "reference"):
     """The truncated-BPTT variant of the driver (reference backup/lstm_bbpt.py:18-208), same
     graph, loss and Adam.  After the teacher warm-up (:115-139) each round is
       * one BPTT pass (:141-158): ``dataset.bptt_batches()`` -- LSTM_BATCH_SIZE episodes, the
@@ -121,7 +128,8 @@ def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOT
     tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
     st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
                                               steps=STEPS_UNROLLED, max_windows=LSTM_BATCH_SIZE), device=device)
-    dataset = DeviceDataset(device=device, seed=seed, batch_size=LSTM_BATCH_SIZE, steps_unrolled=STEPS_UNROLLED)
+    dataset = DeviceDataset(device=device, seed=seed, batch_size=LSTM_BATCH_SIZE, steps_unrolled=STEPS_UNROLLED,
+                            store=PageStore(store_dir) if store_dir else None, pool=pool)
     _restore(st, restore, student_path, log)
     losses = []
     if not train:
@@ -163,6 +171,8 @@ def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOT
         log("recent loss: %f " % total_loss)
         losses.append(total_loss)
         dataset.flush()
+        if dataset.store is not None and dataset.num_episodes() % MAX_CAPACITY == 0:
+            dataset.dump()              # backup/lstm_bbpt.py:207
         if student_path:
             st.save(student_path)
         if dataset.num_episodes() >= episodes:

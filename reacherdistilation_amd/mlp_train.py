@@ -28,6 +28,7 @@ import torch
 
 from .config import MLP_BATCH_SIZE, MLP_EPISODE_BUDGET, OBSPACE_SHAPE
 from .dataset import DeviceDataset
+from .pages import PageStore
 from .distill import DistillConfig, DistillTrainer
 from .driver_env import DriverEnv, episode_loss
 from .policy import TeacherAgent
@@ -37,12 +38,15 @@ from .student_mlp import StudentMlpConfig, StudentMlpTrainer, rows
 def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPISODE_BUDGET,
           loss: str = "kl", lr: float = 1e-4, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
           warmup_episodes: int = 2 * MLP_BATCH_SIZE, student: str = "policy", keep_prob: float = 1.0,
-          log=print, gym_env: bool = False):
+          log=print, gym_env: bool = False, store_dir: str | None = None, pool: str = "reference"):
     """Returns (trainer, dataset, per-episode summed training loss); the trainer is the
     DistillTrainer (student="policy") or the StudentMlpTrainer (student="mlp").  The env I/O
     stays on the device (driver_env.DriverEnv; gym_env=True: through the gym-API env, numpy
     every step) and the window losses are read from the trainer's metrics ring once per
-    episode, so nothing waits on the GPU inside an episode."""
+    episode, so nothing waits on the GPU inside an episode.  ``store_dir``: the dataset's page
+    directory (mlp_train.py:105-110); episodes are dumped to it every 5 episodes (:203) and its
+    stored pages join the training pool (dataset.py:164-177); ``pool="ring"`` draws windows
+    uniformly from the device ring instead."""
     if student not in ("policy", "mlp"):
         raise ValueError(f"unknown student {student!r}")
     env = DriverEnv(seed, device, gym_api=gym_env)
@@ -50,7 +54,7 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
     tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr), device=device, teacher=teacher.pi)
     sm = StudentMlpTrainer(StudentMlpConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed),
                            device=device) if student == "mlp" else None
-    dataset = DeviceDataset(device=device, seed=seed)
+    dataset = DeviceDataset(device=device, seed=seed, store=PageStore(store_dir) if store_dir else None, pool=pool)
     ob = env.reset()                                  # [1, 11] on the device
     reward = torch.zeros(1, device=env.device)
     losses = []
@@ -92,6 +96,8 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
             losses.append(total_loss)
             opt_steps = 0
             dataset.flush()
+            if dataset.store is not None and dataset.num_episodes() % 5 == 0:
+                dataset.dump()          # mlp_train.py:203
             if dataset.num_episodes() >= episodes:
                 break
     return (sm or tr), dataset, losses

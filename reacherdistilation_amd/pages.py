@@ -55,10 +55,13 @@ def _scalar(v) -> float:
     return float(v[0]) if isinstance(v, (list, tuple)) else float(v)
 
 
-def episodes_to_records(episodes) -> np.ndarray:
-    """[E, EPISODE_STEPS, 21] f64 records (ob | rew | t | s | with) of the complete episodes."""
-    full = [e for e in episodes if len(e) == EPISODE_STEPS]
+def episodes_to_records(episodes, with_lengths: bool = False):
+    """[E, EPISODE_STEPS, 21] f64 records (ob | rew | t | s | with) of the complete episodes;
+    with_lengths=True: of EVERY episode (an incomplete one zero-padded, as the reference's
+    flush stores them, dataset.py:146-149), and their lengths [E]."""
+    full = [e for e in episodes if len(e) <= EPISODE_STEPS and (with_lengths or len(e) == EPISODE_STEPS)]
     out = np.zeros((len(full), EPISODE_STEPS, REC))
+    lens = np.array([len(e) for e in full], np.int64)
     for i, ep in enumerate(full):
         for k, st in enumerate(ep):
             out[i, k, F_OB:F_REW] = st["ob"]
@@ -66,17 +69,18 @@ def episodes_to_records(episodes) -> np.ndarray:
             out[i, k, F_T:F_S] = st["t"]
             out[i, k, F_S:F_WITH] = st.get("s", [0.0] * PDFLAT_SHAPE)
             out[i, k, F_WITH] = 1.0 if st.get("with", "t") == "s" else 0.0
-    return out
+    return (out, lens) if with_lengths else out
 
 
-def records_to_episodes(rec) -> list:
+def records_to_episodes(rec, lens=None) -> list:
     """Inverse of episodes_to_records, with the prev / prew fields the reference derives
-    (previous record's teacher pdflat and reward, zeros at t = 0; dataset.py:132-133,152-163)."""
+    (previous record's teacher pdflat and reward, zeros at t = 0; dataset.py:132-133,152-163);
+    lens: each episode's record count (default: all EPISODE_STEPS)."""
     rec = np.asarray(rec, np.float64)
     eps = []
-    for ep in rec:
+    for i, ep in enumerate(rec):
         steps = []
-        for k, r in enumerate(ep):
+        for k, r in enumerate(ep[:EPISODE_STEPS if lens is None else int(lens[i])]):
             prev = ep[k - 1, F_T:F_S].tolist() if k > 0 else [0.0] * PDFLAT_SHAPE
             prew = [float(ep[k - 1, F_REW])] if k > 0 else [0]
             steps.append({"ob": r[F_OB:F_REW].tolist(), "rew": [float(r[F_REW])], "t": r[F_T:F_S].tolist(),

@@ -23,7 +23,14 @@ Output (data only: constants, shapes, and input/output vectors):
               (adam/gradients/LSTM/split{,_1}_grad/concat), 64 instances of the graph's
               [T=2, B=1] shape;
       cell_*  one LSTM/unique_lstm_cell step (c', h') on seeded x, c, h, kernel, bias;
-      drop_*  LSTM/dropout/mul with the RandomUniform draw fed.
+      drop_*  LSTM/dropout/mul with the RandomUniform draw fed;
+      bptt{k}_*  the graph's WHOLE TF-generated backward: the gradient input of every one of
+              its 30 ApplyAdam nodes (adam/gradients/AddN_6, AddN_7 -- the cell's BPTT over the
+              T = 2 unrolled steps -- and each dense layer's MatMul_grad / BiasAddGrad, through
+              TanhGrad, SigmoidGrad, the kl and reward losses) with every LSTM/* variable and
+              placeholder fed from a seed (keep_prob 1).  k = 0 at the logged shapes (1 unit,
+              B = 1, heads 128/64/32/64); k = 1..3 with narrower heads, which the graph's ops accept
+              (heads 16/8/4/8; the unit count and B = 1 are baked into its Reshape constants).
 """
 import json
 import os
@@ -161,6 +168,58 @@ def goldens(g):
     out.update(drop_x=xo, drop_u=u, drop_kp=np.float64(kp),
                drop_out=g.run("LSTM/dropout/mul", {"LSTM/ob_combined_ph": xo, "LSTM/keep_prob": kp,
                                                    "LSTM/dropout/random_uniform/RandomUniform": u}))
+    out.update(bptt_goldens(g, rng))
+    return out
+
+
+# the logged graph's trainable LSTM/* variables, in creation order (= its ApplyAdam order)
+def lstm_variables(g):
+    return [n for n, d in g.nodes.items() if d["op"] == "VariableV2" and n.startswith("LSTM/") and "/Adam" not in n]
+
+
+def bptt_feeds(g, rng, units, B, heads):
+    """Seeded values for every LSTM/* variable and placeholder.  heads = (step, reward hid 1,
+    2, 3, action) widths; units = the cell's.  Values are float32-representable."""
+    H, R1, R2, R3, A = heads
+    shapes = {"unique_lstm_cell/kernel": (13 + units, 4 * units), "unique_lstm_cell/bias": (4 * units,)}
+    for k in (1, 2):
+        for name, a, b in (("lstm_step", units, H), ("reward_hid", H, R1), ("reward_2hid", R1, R2),
+                           ("reward_3hid", R2, R3), ("reward_out", R3, 1), ("lstm_action", H, A), ("pd_step", A, 4)):
+            shapes[f"{name}{k}/kernel"], shapes[f"{name}{k}/bias"] = (a, b), (b,)
+    f = {}
+    for v in lstm_variables(g):
+        shp = shapes[v[len("LSTM/"):]]
+        scale = 1.5 / np.sqrt(shp[0]) if len(shp) == 2 else 0.3
+        f[v] = (rng.standard_normal(shp) * scale).astype(np.float32).astype(np.float64)
+    tl = rng.uniform(-1.5, 0.5, (2, B, 2)).astype(np.float32).astype(np.float64)
+    f.update({"LSTM/ob_combined_ph": rng.standard_normal((2, B, 11)).astype(np.float32).astype(np.float64),
+              "LSTM/action_combined_ph": rng.uniform(-1, 1, (2, B, 2)).astype(np.float32).astype(np.float64),
+              "LSTM/Placeholder": (rng.standard_normal((2, B, units)) * 0.5).astype(np.float32).astype(np.float64),
+              "LSTM/t_mean_combined": rng.uniform(-1, 1, (2, B, 2)).astype(np.float32).astype(np.float64),
+              "LSTM/t_logstd_combined": tl, "LSTM/t_std_combined": np.exp(tl),
+              "LSTM/reward_target": rng.standard_normal((2, 1)).astype(np.float32).astype(np.float64)})
+    return f
+
+
+def bptt_goldens(g, rng):
+    names = lstm_variables(g)
+    adam = {g.nodes[n]["inputs"][0]: g.nodes[n]["inputs"][9] for n, d in g.nodes.items() if d["op"] == "ApplyAdam"}
+    assert sorted(adam) == sorted(names) and len(names) == 30
+    out = {"bptt_vars": np.array(names), "bptt_grad_nodes": np.array([adam[v] for v in names])}
+    cases = [(1, 1, (128, 64, 32, 64, 64))] + [(1, 1, (16, 8, 4, 8, 8))] * 3   # B, units baked into Reshape consts
+    for k, (units, B, heads) in enumerate(cases):
+        f = bptt_feeds(g, rng, units, B, heads)
+        feeds = dict(f, **{"LSTM/keep_prob": 1.0,
+                           "LSTM/dropout/random_uniform/RandomUniform": rng.uniform(0, 1, (2, B, 11))})
+        vals = g.run([adam[v] for v in names] + ["LSTM/kstm_kl_loss", "LSTM/Sum"], feeds)
+        for j, v in enumerate(names):
+            out[f"bptt{k}_var{j}"] = f[v].astype(np.float32)   # f32-representable by construction
+            out[f"bptt{k}_grad{j}"] = np.asarray(vals[j], np.float64)
+        for ph in ("ob_combined_ph", "action_combined_ph", "Placeholder", "t_mean_combined", "t_logstd_combined",
+                   "reward_target"):
+            out[f"bptt{k}_{ph}"] = f[f"LSTM/{ph}"]
+        out[f"bptt{k}_kl"], out[f"bptt{k}_rloss"] = np.float64(vals[-2]), np.float64(vals[-1])
+    out["bptt_cases"] = np.array(len(cases))
     return out
 
 

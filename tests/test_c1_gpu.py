@@ -72,6 +72,20 @@ def test_reference_shaped_driver_runs():
     assert env_steps == 0 and opt_steps == 2 * 50
 
 
+def test_reference_shaped_driver_dumps_pages_and_trains_on_them(tmp_path):
+    """store_dir: the driver dumps every 5 episodes (mlp_train.py:203); once data_in_memory
+    holds MAX_CAPACITY episodes the page closes, and the pool refreshes (every 25 records)
+    draw from data_in_memory plus the stored pages (dataset.py:164-182)."""
+    from reacherdistilation_amd import mlp_train, pages
+    from reacherdistilation_amd.config import MAX_CAPACITY
+    tr, ds, losses = mlp_train.train(episodes=13, warmup_episodes=1, loss="mse", lr=1e-3, log=lambda *a: None,
+                                     store_dir=str(tmp_path))
+    assert ds.num_episodes() == 13 and len(losses) == 11 and all(np.isfinite(losses))
+    assert len(ds.store.pages) == 1 and len(pages.read_page(ds.store.pages[0])) == MAX_CAPACITY
+    # the last refresh (25 records into episode 13): episodes 11, 12 in memory + page 0
+    assert ds.pool_pages == ds.store.pages and ds.pool_size() == MAX_CAPACITY + 2 and len(ds._mem_slots) == 3
+
+
 def test_reference_shaped_driver_with_the_reference_student():
     """student="mlp": the reference's own student_mlp_graph on ob | prev_pdflat | prev_rew rows,
     kl_loss on the recorded teacher pdflat, dropout keep_prob 0.5 (reference KEEP_PROB)."""

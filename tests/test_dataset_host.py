@@ -43,12 +43,18 @@ def test_ring_overwrites_oldest_episode():
     assert eps == [2, 3, 4]
 
 
-def test_partial_episode_not_stored():
+def test_partial_episode_is_stored_like_the_reference():
+    """flush() stores an incomplete episode with its record count (reference dataset.py:
+    146-149); a training window drawn past its end raises IndexError, as the reference's
+    episode[i] does; more than EPISODE_STEPS records in one episode is refused."""
     ds = DeviceDataset(capacity=3, device="cpu")
     for k in range(7):
         ds.write(ob=np.ones(11))
     ds.flush()
-    assert ds.num_episodes() == 1 and float(ds.ring.abs().sum()) == 0.0
+    assert ds.num_episodes() == 1 and ds.lens[0] == 7
+    assert float(ds.ring[0, :7, :11].sum()) == 77.0 and float(ds.ring[0, 7:].abs().sum()) == 0.0
+    with pytest.raises(IndexError):
+        list(ds.training_batches())
     with pytest.raises(RuntimeError):
         for k in range(51):
             ds.write(ob=np.ones(11))

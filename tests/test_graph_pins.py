@@ -206,3 +206,88 @@ def test_kernel_forward_matches_reference_graph(gg, which):
         np.testing.assert_allclose(got[:, :2], want[:, :2], atol=5e-5, rtol=2e-5)
         assert np.array_equal(got[:, 2:], want[:, 2:].astype(np.float32))
     tr.close()
+
+
+def _variant_grads(v, ph):
+    """The logged LSTM graph (1-unit TF1 LSTMCell over T = 2 steps; per step a tanh 'lstm_step'
+    layer feeding a reward head 64-32-64-1 and an action head 64-4 = pdflat; loss = kl_loss +
+    the reward squared error) forward AND backward, built only from the oracle's primitives:
+    lstm_np.cell / bptt, refnet_np.dense_backward / tanh_grad / loss_and_dout."""
+    Wl, bl = v["unique_lstm_cell/kernel"], v["unique_lstm_cell/bias"]
+    ob, act, P = ph["ob_combined_ph"], ph["action_combined_ph"], ph["Placeholder"]
+    c, h = P[0], P[1]
+    steps, heads, pd = [], [], []
+    for t in range(2):
+        x = np.concatenate([ob[t], act[t]], 1)      # dropout at keep_prob 1 is the identity
+        cprev, hprev = c, h
+        c, h, (gi, gj, gf, go) = lstm_np.cell(x, cprev, hprev, Wl, bl)
+        steps.append(dict(x=x, hprev=hprev, cprev=cprev, gi=gi, gj=gj, gf=gf, go=go, c=c))
+        k = t + 1
+        a = np.tanh(h @ v[f"lstm_step{k}/kernel"] + v[f"lstm_step{k}/bias"])
+        r = [a]
+        for name in ("reward_hid", "reward_2hid", "reward_3hid"):
+            r.append(np.tanh(r[-1] @ v[f"{name}{k}/kernel"] + v[f"{name}{k}/bias"]))
+        rew = r[-1] @ v[f"reward_out{k}/kernel"] + v[f"reward_out{k}/bias"]
+        q = np.tanh(a @ v[f"lstm_action{k}/kernel"] + v[f"lstm_action{k}/bias"])
+        pd.append(q @ v[f"pd_step{k}/kernel"] + v[f"pd_step{k}/bias"])
+        heads.append((h, a, r, rew, q))
+    tp = np.concatenate([ph["t_mean_combined"], ph["t_logstd_combined"]], 2).reshape(2, 4)
+    kl, dpd, _ = refnet_np.loss_and_dout(np.concatenate(pd, 0), tp, "kl", 2)
+    rews = np.array([heads[t][3].item() for t in range(2)])
+    diff = rews[None, :] - ph["reward_target"]            # [2 targets, 2 steps]: the graph's broadcast
+    rloss, drew = float((diff ** 2).sum()), 2.0 * diff.sum(0)
+    g, dh_out = {}, []
+    for t in range(2):
+        k = t + 1
+        h, a, r, rew, q = heads[t]
+        g[f"pd_step{k}/kernel"], g[f"pd_step{k}/bias"], dq = dense_backward(q, dpd[t:t + 1], v[f"pd_step{k}/kernel"])
+        g[f"lstm_action{k}/kernel"], g[f"lstm_action{k}/bias"], da = dense_backward(
+            a, refnet_np.tanh_grad(q, dq), v[f"lstm_action{k}/kernel"])
+        g[f"reward_out{k}/kernel"], g[f"reward_out{k}/bias"], dr = dense_backward(
+            r[3], np.array([[drew[t]]]), v[f"reward_out{k}/kernel"])
+        for j, name in ((3, "reward_3hid"), (2, "reward_2hid"), (1, "reward_hid")):
+            g[f"{name}{k}/kernel"], g[f"{name}{k}/bias"], dr = dense_backward(
+                r[j - 1], refnet_np.tanh_grad(r[j], dr), v[f"{name}{k}/kernel"])
+        g[f"lstm_step{k}/kernel"], g[f"lstm_step{k}/bias"], dh = dense_backward(
+            h, refnet_np.tanh_grad(a, da + dr), v[f"lstm_step{k}/kernel"])
+        dh_out.append(dh)
+    g["unique_lstm_cell/kernel"], g["unique_lstm_cell/bias"], _, _, _ = lstm_np.bptt(steps, Wl, dh_out)
+    return g, kl, rloss
+
+
+def dense_backward(a, dz, W):
+    return refnet_np.dense_backward(a, dz, W)
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_oracle_backward_reproduces_tf_generated_gradients(gg, case):
+    """the TF-generated backward of the reference's logged LSTM graph --
+    the gradient input of each of its 30 ApplyAdam nodes (adam/gradients/AddN_6, AddN_7 = the
+    cell's BPTT over two steps; every dense layer's MatMul_grad + BiasAddGrad through TanhGrad;
+    the kl + reward losses), evaluated from the graph (tests/golden/make_graph_consts.py) --
+    equals the oracle's own backward primitives composed the same way.  These primitives ARE
+    lstm_np.backward (bptt, cell_backward), refnet_np.backward and policy_np.backward
+    (dense_backward, tanh_grad, loss_and_dout), so the oracle backward that checks every GPU
+    gradient rests on reference-held vectors.  Tolerance: rtol 1e-10 (both f64)."""
+    names = [str(n) for n in gg["bptt_vars"]]
+    v = {n[len("LSTM/"):]: gg[f"bptt{case}_var{j}"].astype(np.float64) for j, n in enumerate(names)}
+    ph = {k: gg[f"bptt{case}_{k}"] for k in ("ob_combined_ph", "action_combined_ph", "Placeholder",
+                                              "t_mean_combined", "t_logstd_combined", "reward_target")}
+    g, kl, rloss = _variant_grads(v, ph)
+    assert abs(kl - float(gg[f"bptt{case}_kl"])) <= 1e-10 * abs(kl)
+    assert abs(rloss - float(gg[f"bptt{case}_rloss"])) <= 1e-10 * abs(rloss)
+    assert sorted(g) == sorted(v)
+    for j, n in enumerate(names):
+        want = gg[f"bptt{case}_grad{j}"]
+        got = g[n[len("LSTM/"):]]
+        assert got.shape == want.shape, n
+        np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-12 * np.abs(want).max(), err_msg=n)
+
+
+def test_tf_gradient_goldens_cover_every_apply_adam(gg):
+    """All 30 ApplyAdam gradient inputs of the logged graph are in the goldens (the cell's two
+    AddN sums are its BPTT over the two unrolled steps)."""
+    nodes = [str(n) for n in gg["bptt_grad_nodes"]]
+    assert len(nodes) == 30 and int(gg["bptt_cases"]) == 4
+    assert nodes[:2] == ["adam/gradients/AddN_7", "adam/gradients/AddN_6"]
+    assert all(("MatMul_grad" in n) == ("kernel" in str(v)) for n, v in zip(nodes[2:], gg["bptt_vars"][2:]))
