@@ -89,8 +89,9 @@ def parse():
                     help="skip the secondary timing of the exact-f32-MFMA kernel beside the split one")
     ap.add_argument("--no-strong", action="store_true",
                     help="at N > 1 skip the strong-scaling leg (the workload's fixed global batch over the ranks)")
-    ap.add_argument("--conv-small-envs", type=int, default=256,
-                    help="env count of the second convergence run (the env-step reading of the budget)")
+    ap.add_argument("--conv-small-envs", type=int, default=64,
+                    help="env count of the second convergence run (the env-step reading of the budget: "
+                         "scripts/conv_sweep.py measured 16/32/64/128 envs within it at lr 1e-4, 256 not)")
     return ap.parse_args()
 
 
@@ -430,6 +431,27 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
             "student_mse_final": mse, "opt_steps_run": steps, "seconds": el}
 
 
+def convergence_driver(dev, lr, max_episodes=5000, target=1e-3):
+    """The env-step reading of the budget on the reference's OWN loop shape: mlp_train.train
+    (one env, per env step one Adam step on a 200-row window from the dataset's training pool,
+    the 2x64 student, MSE) until an episode's mean window action-MSE is < 1e-3; env steps
+    counted from the first teacher warm-up step (mlp_train.py:116-204)."""
+    from reacherdistilation_amd import mlp_train
+    t0 = time.perf_counter()
+    tr, ds, losses = mlp_train.train(episodes=max_episodes, loss="mse", lr=lr, log=lambda *a: None, device=dev,
+                                     stop_loss=target)
+    el = time.perf_counter() - t0
+    hit = bool(losses) and losses[-1] / 50 < target
+    env_steps = ds.num_episodes() * 50
+    tr.close()
+    budget = 5000 * 50
+    return {"target_mse": target, "lr": lr, "loss": "mse", "driver": "mlp_train.train (1 env, 200-row windows)",
+            "episodes": ds.num_episodes(), "env_steps_to_target": env_steps if hit else None,
+            "opt_steps_to_target": 50 * len(losses) if hit else None, "reference_budget_env_steps": budget,
+            "within_env_step_budget": hit and env_steps <= budget,
+            "student_mse_final": losses[-1] / 50 if losses else None, "seconds": el}
+
+
 def main():
     args = parse()
     import torch
@@ -668,6 +690,8 @@ def main():
         if conv is not None:
             out["convergence"] = conv
             out["convergence_small_batch"] = conv_small
+            if world == 1:
+                out["convergence_reference_driver"] = convergence_driver(dev, args.lr)
         out["roofline_env"] = env_roofline(dev)
         out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / copy_gbs
         if world == 1 and not args.no_cpu_baseline:

@@ -38,7 +38,8 @@ from .student_mlp import StudentMlpConfig, StudentMlpTrainer, rows
 def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPISODE_BUDGET,
           loss: str = "kl", lr: float = 1e-4, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
           warmup_episodes: int = 2 * MLP_BATCH_SIZE, student: str = "policy", keep_prob: float = 1.0,
-          log=print, gym_env: bool = False, store_dir: str | None = None, pool: str = "reference"):
+          log=print, gym_env: bool = False, store_dir: str | None = None, pool: str = "reference",
+          stop_loss: float | None = None):
     """Returns (trainer, dataset, per-episode summed training loss); the trainer is the
     DistillTrainer (student="policy") or the StudentMlpTrainer (student="mlp").  The env I/O
     stays on the device (driver_env.DriverEnv; gym_env=True: through the gym-API env, numpy
@@ -46,7 +47,8 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
     episode, so nothing waits on the GPU inside an episode.  ``store_dir``: the dataset's page
     directory (mlp_train.py:105-110); episodes are dumped to it every 5 episodes (:203) and its
     stored pages join the training pool (dataset.py:164-177); ``pool="ring"`` draws windows
-    uniformly from the device ring instead."""
+    uniformly from the device ring instead.  ``stop_loss``: also stop after the first DAgger
+    episode whose mean window loss falls below it (convergence measurements)."""
     if student not in ("policy", "mlp"):
         raise ValueError(f"unknown student {student!r}")
     env = DriverEnv(seed, device, gym_api=gym_env)
@@ -94,10 +96,11 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
             total_loss = episode_loss(m)
             log("recent loss: %f " % total_loss)
             losses.append(total_loss)
+            done = stop_loss is not None and opt_steps and total_loss / opt_steps < stop_loss
             opt_steps = 0
             dataset.flush()
             if dataset.store is not None and dataset.num_episodes() % 5 == 0:
                 dataset.dump()          # mlp_train.py:203
-            if dataset.num_episodes() >= episodes:
+            if dataset.num_episodes() >= episodes or done:
                 break
     return (sm or tr), dataset, losses
