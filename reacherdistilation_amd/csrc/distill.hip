@@ -171,8 +171,48 @@ struct RolloutArgs {
     const float* simg;
 };
 
+// f32 MFMA.  FENCE: an empty asm that reads the result and clobbers memory follows it, so the
+// MFMA has completed (the compiler waits for its result) before any later LDS / global load
+// issues.  Needed wherever the compiler would otherwise issue a load into a register that an
+// in-flight 8-pass v_mfma_f32_16x16x4_f32 still reads as SrcC: ROCm 7.2 protects that WAR
+// for the XDL (bf16) MFMAs but emits such loads 0-1 wait states after the f32 form, and a
+// load returning there is lost for the lanes of the MFMA's last row group (rows 12-15 =
+// lanes 48-63) when the MFMA is still reading (found statically with
+// scripts/isa/hazards.py, confirmed with profiles/r03_srcc_probe_*.txt; the consumer-side env
+// step of the bf16-student kernel fences its teacher's f32 layer 1).  -DRD_MFMA_SRCC_FENCE
+// fences every f32 MFMA (diagnostic builds).
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// SrcC fence around a group of four f32 MFMAs (FENCE): the group's accumulators pass through
+// an empty asm before and after it (so its MFMAs stay between them, and no load -- the asm
+// clobbers memory -- moves into the group), and each result is read by a VALU before the
+// closing asm, so the compiler waits for every MFMA of the group to complete first.
+// Needed wherever the compiler would otherwise issue a load into a register that an in-flight
+// 8-pass v_mfma_f32_16x16x4_f32 still reads as SrcC: ROCm 7.2 protects that WAR for the XDL
+// (bf16) MFMAs but emits such loads 0-1 wait states after the f32 form, and a load returning
+// there is lost for the lanes of the MFMA's last row group (rows 12-15 = lanes 48-63) while
+// the MFMA still reads (found statically with scripts/isa/hazards.py, confirmed
+// by profiles/r03_srcc_probe_*.txt).  The consumer-side-env-step kernels (bf16 student) fence
+// their teacher's f32 MFMAs; -DRD_MFMA_SRCC_FENCE fences every group (diagnostic builds).
+#ifdef RD_MFMA_SRCC_FENCE
+constexpr bool kFenceAll = true;
+#else
+constexpr bool kFenceAll = false;
+#endif
+template <bool FENCE>
+__device__ __forceinline__ void fence_begin(f32x4 (&acc)[4]) {   // the group's MFMAs read acc: they follow
+    if constexpr (FENCE || kFenceAll)
+        asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])::"memory");
+}
+template <bool FENCE>
+__device__ __forceinline__ void fence_end(f32x4 (&acc)[4]) {   // every MFMA of the group precedes it
+    if constexpr (FENCE || kFenceAll) {
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) acc[fb][3] = __builtin_amdgcn_fmed3f(acc[fb][3], acc[fb][3], acc[fb][3]);
+        asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])::"memory");
+    }
 }
 
 // Forward weight images are pre-scaled by 2 log2(e), so a layer's accumulator is already
@@ -305,6 +345,7 @@ __device__ void load_net(float* L, const float* g, bool transposed, int nthreads
 // wave's obs scratch (row stride SOS, component 11 = 1).  Lane (j, g):
 // H1, H2 = hidden activations, features 16 fb + 4 g + r of env j; (m0, m1) = action mean
 // of env j (identical in the four k-groups).
+template <bool FENCE = false>
 __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int j, int g, f32x4 (&H1)[4],
                                             f32x4 (&H2)[4], float& m0, float& m1) {
     f32x4 acc[4];
@@ -316,8 +357,10 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
         const int k = 4 * s + g;
         const float z = fminf(fmaxf((ob[j * SOS + k] - L[N_MU + k]) * L[N_RS + k], -5.0f), 5.0f);
         const f32x4 w = ld4(L + N_W1 + k * HID + 4 * j);
+        fence_begin<FENCE>(acc);
 #pragma unroll
         for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], z, acc[fb]);
+        fence_end<FENCE>(acc);
     }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
@@ -336,8 +379,10 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
                 const int kn = (r == 3) ? 16 * (kb + 1) + 4 * g : 16 * kb + 4 * g + r + 1;
                 wn = ld4(L + N_W2 + kn * HID + 4 * j);
             }
+            fence_begin<FENCE>(acc);
 #pragma unroll
             for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], H1[kb][r], acc[fb]);
+            fence_end<FENCE>(acc);
         }
     float p0 = 0.0f, p1 = 0.0f;
 #pragma unroll
@@ -675,7 +720,7 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
 
 // One net's forward with a split image (the teacher beside the bf16 student; HO: also
 // return the hidden activations).
-template <bool HO>
+template <bool HO, bool FENCE = false>
 __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float* ob, int j, int g, f32x4 (&H1)[4],
                                                     f32x4 (&H2)[4], float& m0, float& m1) {
     f32x4 acc[4];
@@ -686,8 +731,10 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
         const int k = 4 * s + g;
         const float z = fminf(fmaxf((ob[j * SOS + k] - L[NX_MU + k]) * L[NX_RS + k], -5.0f), 5.0f);
         const f32x4 w = ld4(L + NX_W1 + k * HID + 4 * j);
+        fence_begin<FENCE>(acc);
 #pragma unroll
         for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], z, acc[fb]);
+        fence_end<FENCE>(acc);
     }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
@@ -721,9 +768,10 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
     m0 = xsum32(xsum16(p0)) + L[NX_B3];
     m1 = xsum32(xsum16(p1)) + L[NX_B3 + 1];
 }
+template <bool FENCE = false>
 __device__ __forceinline__ void mlp_forward_split(const float* L, const float* ob, int j, int g, float& m0, float& m1) {
     f32x4 h1[4], h2[4];
-    mlp_forward_split_t<false>(L, ob, j, g, h1, h2, m0, m1);
+    mlp_forward_split_t<false, FENCE>(L, ob, j, g, h1, h2, m0, m1);
 }
 
 
@@ -1125,8 +1173,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 float mt0, mt1, ms0, ms1;
                 STAMP(10);
                 if constexpr (BS) {
-                    if constexpr (SPL) mlp_forward_split(LT, obt, j, g, mt0, mt1);
-                    else mlp_forward(LT, obt, j, g, H1, H2, mt0, mt1);
+                    // CP: in this kernel's schedule the compiler issues loads into the SrcC
+                    // registers of the teacher's f32 layer-1 MFMAs: fenced (see mfma())
+                    if constexpr (SPL) mlp_forward_split<CP>(LT, obt, j, g, mt0, mt1);
+                    else mlp_forward<CP>(LT, obt, j, g, H1, H2, mt0, mt1);
                     mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
                 } else {
                     if constexpr (SPL) mlp_forward_pair_split(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
@@ -1684,11 +1734,14 @@ int image_floats(int kind, bool student) {
     return student ? NET_S : NET;
 }
 
-// Which wave of a pair steps the envs: the producer, which computed the
-// actions and holds the state.  The consumer-side variant balances the roles better (c5
-// 39.7 vs 43.4 us, c4 split 92.1 vs 93.6 us) but its env step is not reproducible run to run
-// with the bf16 MFMA kernels, so it is not in the product library: only a
-// diagnostic build (-DRD_CP_VARIANT) instantiates it, selected there by RDD_PHYS=consumer.
+// Which wave of a pair steps the envs.  The bf16 student (BASELINE config 5):
+// the consumer, after its last tile of a group (the actions travel with each tile's slot):
+// this balances the roles, since the producer's forward (f32 teacher + bf16 student) is the
+// longer one.  Its MFMAs are all bf16 (XDL: the compiler protects their SrcC) except the
+// teacher's f32 layer 1, which is SrcC-fenced (mfma<true>).  The f32 student: the producer
+// steps the envs it computed the actions for; a consumer-side step there would need the
+// consumer's 80 f32 MFMAs per tile fenced (diagnostic builds: -DRD_CP_VARIANT selects it with
+// RDD_PHYS=consumer, -DRD_MFMA_SRCC_FENCE fences every f32 MFMA).
 #ifdef RD_CP_VARIANT
 bool consumer_physics() {
     const char* e = getenv("RDD_PHYS");
@@ -1754,12 +1807,10 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     }
     t->last_grid = grid;
     const bool bs = t->cfg.student_dtype == RDD_DTYPE_BF16, spl = t->cfg.f32_split != 0;
-    void (*k)(RolloutArgs) = bs ? (spl ? rollout_kernel<true, true, false> : rollout_kernel<true, false, false>)
+    void (*k)(RolloutArgs) = bs ? (spl ? rollout_kernel<true, true, true> : rollout_kernel<true, false, true>)
                                 : (spl ? rollout_kernel<false, true, false> : rollout_kernel<false, false, false>);
 #ifdef RD_CP_VARIANT
-    if (consumer_physics())
-        k = bs ? (spl ? rollout_kernel<true, true, true> : rollout_kernel<true, false, true>)
-               : (spl ? rollout_kernel<false, true, true> : rollout_kernel<false, false, true>);
+    if (!bs && consumer_physics()) k = spl ? rollout_kernel<false, true, true> : rollout_kernel<false, false, true>;
 #endif
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");

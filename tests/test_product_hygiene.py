@@ -5,8 +5,14 @@ byte for byte, and the bench's headline mode is the library's default mode.
 - libreacher.so imports no getenv: every measurement-only switch (RDD_PHYS, RDD_GROUP_ENVS,
   RDM_ROWS, RDL_PR_DBG) exists only in build_variant builds (-DRD_DIAG_KNOBS / -DRD_CP_VARIANT);
   the tests' path selections are config fields (rdd_config.group_envs, rdl_config.kernels).
-- The consumer-side env step (rollout_kernel<*, *, CP = true>, DESIGN.md §3: not reproducible
-  run to run with the bf16 MFMA kernels) is not instantiated in the product.
+- The consumer-side env step is instantiated only for the bf16 student (rollout_kernel<true, *,
+  true>), whose f32 MFMAs (the teacher's) are SrcC-fenced; the f32 student's consumer-side step
+  (its consumer runs 80 unfenced f32 MFMAs per tile) exists only in diagnostic
+  builds.
+- Statically, in the product's ISA no LDS / global load is issued into a register that an
+  in-flight f32 MFMA (8 passes) still reads as SrcC within 5 wait states -- the pattern that
+  made the unfenced consumer-side step lose loaded values in lanes 48-63
+  (scripts/isa/hazards.py, profiles/r03_srcc_probe_*.txt).
 """
 import ctypes
 import os
@@ -33,12 +39,35 @@ def test_product_library_reads_no_environment(libpath):
     assert not {"getenv", "secure_getenv", "__secure_getenv"} & syms
 
 
-def test_product_library_has_no_consumer_side_step(libpath):
+def test_consumer_side_step_only_for_the_bf16_student(libpath):
     blob = open(libpath, "rb").read()
     names = set(re.findall(rb"rollout_kernelILb[01]ELb[01]ELb[01]E", blob))
     assert names, "rollout_kernel instantiations not found in the offload bundle"
-    assert all(n.endswith(b"ELb0E") for n in names), sorted(names)
-    assert len(names) == 4   # {f32, bf16 student} x {exact, split}
+    # <bf16 student, f32 mode, consumer-side step>: f32 student -> producer-side, bf16 -> consumer-side
+    assert names == {b"rollout_kernelILb0ELb0ELb0E", b"rollout_kernelILb0ELb1ELb0E",
+                     b"rollout_kernelILb1ELb0ELb1E", b"rollout_kernelILb1ELb1ELb1E"}, sorted(names)
+
+
+def test_no_load_into_an_inflight_f32_mfma_srcc():
+    """The product's rollout kernels, compiled to ISA here: every LDS / global load whose
+    destination is the SrcC of an earlier v_mfma_f32_16x16x4_f32 issues >= 5 wait states after
+    it; in the fenced bf16-student kernels >= 10, i.e. after the MFMA completed (the compiler's
+    RAW wait for an 8-pass result, NumPasses + 2)."""
+    import importlib.util
+    from reacherdistilation_amd import build
+    out = os.path.join(ROOT, "oracle", "_build", "distill_isa.s")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    subprocess.run([build.HIPCC, "-O3", "-std=c++17", f"--offload-arch={build.ARCH}", "-munsafe-fp-atomics",
+                    "--cuda-device-only", "-S", "-o", out, os.path.join(build.CSRC, "distill.hip")],
+                   check=True, capture_output=True)
+    spec = importlib.util.spec_from_file_location("hz", os.path.join(ROOT, "scripts", "isa", "hazards.py"))
+    hz = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(hz)
+    for sym, floor in (("rollout_kernelILb0ELb0ELb0E", 5), ("rollout_kernelILb0ELb1ELb0E", 5),
+                       ("rollout_kernelILb1ELb0ELb1E", 10), ("rollout_kernelILb1ELb1ELb1E", 10)):
+        hits = [h for h in hz.scan(out, sym, 40)[0] if h[0] == "WARc" and "16x16x4" in h[4]
+                and h[6].split()[0].startswith(("ds_read", "global_load", "buffer_load"))]
+        assert all(h[1] >= floor for h in hits), (sym, [h[:6] for h in hits if h[1] < floor][:5])
 
 
 def _c_layout(struct, header, fields):
