@@ -89,11 +89,7 @@ constexpr int P_H1T = P_ACT + 2 * GROUP * 2;    // slot: H1^T [16][SAS]
 constexpr int P_DZT = P_H1T + TILE * SAS;       // slot: dZ2^T [16][SAS]
 constexpr int P_SA = P_DZT + TILE * SAS;        // consumer-private: dZ1^T [16][SAS]
 constexpr int P_SACT = P_SA + TILE * SAS;       // slot: the tile's actions [16][2] (CP: for the consumer's env step)
-#ifdef RD_DEBUG_SLOT   // diagnostic build: a tile tag beside the slot's actions (scripts/det_slot.py)
-constexpr int P_FLAGS = P_SACT + TILE * 3;
-#else
 constexpr int P_FLAGS = P_SACT + TILE * 2;      // u32 [0] tiles published [1] tiles consumed [2] groups done
-#endif
 constexpr int PSCR = P_FLAGS + 4;
 constexpr int LDS_FLOATS = NET + NET_S + PAIRS * PSCR;
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
@@ -1237,11 +1233,6 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 if (CP && g == 0) {   // the consumer steps these envs: their actions travel with the slot
                     PS[P_SACT + 2 * j] = a.act_student ? ms0 : mt0;
                     PS[P_SACT + 2 * j + 1] = a.act_student ? ms1 : mt1;
-#ifdef RD_DEBUG_SLOT
-                    PS[P_SACT + 2 * TILE + j] = __uint_as_float(tiles);
-                    act[(TILE * t + j) * 2] = a.act_student ? ms0 : mt0;
-                    act[(TILE * t + j) * 2 + 1] = a.act_student ? ms1 : mt1;
-#endif
                 }
                 publish(flags, ++tiles);
             }
@@ -1315,9 +1306,6 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         // backward of tile t of the group whose observations are at obs: its slot is taken
         // (tiles + 1 published), read, freed, and its gradients accumulated
         float act0 = 0.0f, act1 = 0.0f;   // CP: the action of this lane's env (taken from its tile's slot)
-#ifdef RD_DEBUG_SLOT
-        int dbg_t = -1;
-#endif
         auto bwd_tile = [&](const float* obs, int t) -> bool {
             STAMP(2);
             if (!wait_ge(flags, tiles + 1, err)) return false;
@@ -1349,15 +1337,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 if (CP && (lane >> 4) == t) {
                     act0 = PS[P_SACT + 2 * (lane & 15)];
                     act1 = PS[P_SACT + 2 * (lane & 15) + 1];
-#ifdef RD_DEBUG_SLOT
-                    if (__float_as_uint(PS[P_SACT + 2 * TILE + (lane & 15)]) != tiles)
-                        __hip_atomic_fetch_add(a.ctl + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    dbg_t = t;
-#endif
                 }
-#ifdef RD_CP_WAIT   // diagnostic: every outstanding slot read has returned before the slot is freed
-                __builtin_amdgcn_s_waitcnt(0);
-#endif
                 publish(flags + 1, ++tiles);
                 STAMP(13);
 #pragma unroll
@@ -1391,15 +1371,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 if (CP && (lane >> 4) == t) {
                     act0 = PS[P_SACT + 2 * (lane & 15)];
                     act1 = PS[P_SACT + 2 * (lane & 15) + 1];
-#ifdef RD_DEBUG_SLOT
-                    if (__float_as_uint(PS[P_SACT + 2 * TILE + (lane & 15)]) != tiles)
-                        __hip_atomic_fetch_add(a.ctl + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    dbg_t = t;
-#endif
                 }
-#ifdef RD_CP_WAIT   // diagnostic: every outstanding slot read has returned before the slot is freed
-                __builtin_amdgcn_s_waitcnt(0);
-#endif
                 publish(flags + 1, ++tiles);
                 STAMP(13);
                 // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
@@ -1492,28 +1464,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 if (a.obs_in) {
                     if (lvalid) met_n += 1.0f;
                 } else if (lane < gs) {   // act[] rows: published with the group's tiles
-#ifdef RD_DEBUG_SLOT   // the slot's copy vs the producer's act rows (written before the same publish)
-                    {
-                        const float* ar = PS + P_ACT + (k & 1) * GROUP * 2 + lane * 2;
-                        if (ar[0] != act0 || ar[1] != act1)
-                            __hip_atomic_fetch_add(a.ctl + 10, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (dbg_t != (lane >> 4))
-                            __hip_atomic_fetch_add(a.ctl + 11, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-#endif
                     rd::State st{};
                     if (lvalid) load_state(a.state, a.n, i, st);
-#ifdef RD_DEBUG_SLOT   // the state this wave loaded vs the observations the producer formed from its load
-                    if (lvalid) {
-                        float ob2[OBD];
-                        rd::observe<false>(st, ob2);
-                        const float* orow = PS + P_SO + (k & 1) * GROUP * SOS + lane * SOS;
-                        bool same = true;
-#pragma unroll
-                        for (int q = 0; q < OBD; ++q) same = same && (__float_as_uint(ob2[q]) == __float_as_uint(orow[q]));
-                        if (!same) __hip_atomic_fetch_add(a.ctl + 13, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-#endif
                     met_r += env_step_group(a, C, i, lvalid, act0, act1, st, met_n);
                 }
                 STAMP(5);
@@ -2117,16 +2069,6 @@ int rdd_read_metrics(rdd_trainer* t, int64_t count, double* out) {
     return RD_OK;
 }
 
-#ifdef RD_DEBUG_SLOT
-// Diagnostic build only: the 16 control words (slot-tag mismatches in [9], act-copy
-// mismatches in [10], lanes that never took an action in [11]).
-int rdd_debug_ctl(rdd_trainer* t, uint32_t* out) {
-    if (!t || !out) return rd::set_error(RD_EINVAL, "rdd_debug_ctl: bad argument");
-    RD_HIP(hipStreamSynchronize(t->stream), "rdd_debug_ctl");
-    RD_HIP(hipMemcpy(out, t->ctl, sizeof(uint32_t) * 16, hipMemcpyDeviceToHost), "rdd_debug_ctl");
-    return RD_OK;
-}
-#endif
 
 #ifdef RD_STAMPS
 // Diagnostic build only: copy (and zero) the per-wave stamp sums [grid*8][16] to the host.

@@ -70,14 +70,6 @@ __device__ __forceinline__ void sincos_acc(float x, float* s, float* c) {
     *c = ((q + 1) & 2) ? -cv : cv;
 }
 
-// A transcendental's result routed through an s_nop tied to the value, so that its first
-// VALU reader issues at least 5 wait states after it (RD_TRANS_NOP builds).
-__device__ __forceinline__ float trans_fence(float x) {
-#ifdef RD_TRANS_NOP
-    asm volatile("s_nop 4" : "+v"(x));
-#endif
-    return x;
-}
 
 // One MuJoCo forward pass -> constrained qacc of the two arm dofs; (s, c) = sin, cos q1.
 __device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, float v1, float c0, float c1,
@@ -90,7 +82,7 @@ __device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, fl
     const float b1 = HC * s * v0 * v0;
     const float t0 = 200.0f * c0 - v0 - b0;
     const float t1 = 200.0f * c1 - v1 - b1;
-    const float rdet = trans_fence(__builtin_amdgcn_rcpf(m11 * m22 - m12 * m12));   // 1 ulp
+    const float rdet = __builtin_amdgcn_rcpf(m11 * m22 - m12 * m12);   // 1 ulp
     const float i11 = m22 * rdet, i12 = -m12 * rdet, i22 = m11 * rdet;
     a0 = i11 * t0 + i12 * t1;
     a1 = i12 * t0 + i22 * t1;
@@ -103,8 +95,8 @@ __device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, fl
         const float y = x <= 0.5f ? 2.0f * x * x : 1.0f - 2.0f * (1.0f - x) * (1.0f - x);
         const float d = 0.9f + y * 0.05f;
         const float aref = -(float)kBref * (J * v1) - (float)kKref * d * dist;
-        const float R = (1.0f - d) * trans_fence(__builtin_amdgcn_rcpf(d)) * (float)kInvW0;
-        const float f = fmaxf(0.0f, (aref - J * a1) * trans_fence(__builtin_amdgcn_rcpf(i22 + R)));
+        const float R = (1.0f - d) * __builtin_amdgcn_rcpf(d) * (float)kInvW0;
+        const float f = fmaxf(0.0f, (aref - J * a1) * __builtin_amdgcn_rcpf(i22 + R));
         a0 += i12 * J * f;
         a1 += i22 * J * f;
     }
@@ -122,7 +114,7 @@ __device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, flo
 template <bool kWideRange = true>
 __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
     const float h = 0.01f;
-    const float r = -trans_fence(__builtin_amdgcn_sqrtf(st.dx * st.dx + st.dy * st.dy)) - (a0 * a0 + a1 * a1);   // 1 ulp
+    const float r = -__builtin_amdgcn_sqrtf(st.dx * st.dx + st.dy * st.dy) - (a0 * a0 + a1 * a1);   // 1 ulp
     const float c0 = fminf(fmaxf(a0, -1.0f), 1.0f);   // ctrlrange +-1 (ctrllimited)
     const float c1 = fminf(fmaxf(a1, -1.0f), 1.0f);
     float q0 = st.q0, q1 = st.q1, v0 = st.v0, v1 = st.v1;

@@ -65,6 +65,7 @@ def main():
         "producer_fwd_tiles": d(10, 12, prod),
         "producer_wait": d(2, 3, prod),
         "producer_physics": d(4, 5, prod),
+        "consumer_physics": d(4, 5, ~prod),
         "consumer_wait": d(2, 3, ~prod),
         "consumer_slot_read": d(3, 13, ~prod),
         "consumer_dw2_dh1": d(13, 14, ~prod),
