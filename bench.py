@@ -214,6 +214,30 @@ def mixed_peak(sdt, split):
     return PEAK_F32_TFLOPS
 
 
+SIMDS = 256 * 4             # MI355X: 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4             # the clock the dense TFLOP/s peaks assume (MI355X_MICROARCH.md)
+
+
+def issue_roofline(avg, launch_s):
+    """The rollout kernel's real bound on gfx950: one instruction stream per SIMD shared by the
+    VALU and the MFMAs (an f32 MFMA holds it 32 cycles, a bf16 16x16x32 16 -- measured,
+    scripts/micro/mfma_mix.hip; each VALU instruction >= 4 cycles, a transcendental 8).
+    issue cycles >= SQ_VALU_MFMA_BUSY_CYCLES + 4 (SQ_INSTS_VALU - SQ_INSTS_MFMA) per launch
+    (rocprofv3 PMC pass of this workload, profiles/pmc_*.json; transcendentals counted at 4),
+    against the SIMDs' cycles over the live launch time at 2.4 GHz."""
+    try:
+        mfma_cyc = float(avg["SQ_VALU_MFMA_BUSY_CYCLES"])
+        valu = float(avg["SQ_INSTS_VALU"]) - float(avg["SQ_INSTS_MFMA"])
+    except (KeyError, TypeError):
+        return None
+    need = mfma_cyc + 4.0 * valu
+    have = SIMDS * launch_s * CLOCK_GHZ * 1e9
+    return {"bound": "simd-issue", "issue_cycles_per_launch": need, "available_cycles": have, "frac": need / have,
+            "mfma_cycles": mfma_cyc, "valu_instructions": valu, "valu_per_mfma": valu / max(1.0, float(avg["SQ_INSTS_MFMA"])),
+            "model": "MFMA busy cycles (counter) + 4 cycles per non-MFMA VALU instruction; 1,024 SIMDs x launch "
+                     "time x 2.4 GHz; counters from the committed PMC pass (traffic_source)"}
+
+
 def settle(step, dev, ms, world=1):
     """Untimed steps for about `ms` of wall time: on a GPU that idled (trainer set-up, the
     convergence leg's teardown) the first ~100 ms of steps run at ramping clocks -- c4 measured
@@ -634,7 +658,7 @@ def main():
         # HBM bytes per rollout launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
         # MI355X_MICROARCH.md §HBM); counters cannot be read from inside this process, so the
         # committed profile of this workload is used and named in traffic_source
-        traffic, traffic_src = None, None
+        traffic, traffic_src, issue = None, None, None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}_{args.f32_mode}.json")
         if not os.path.exists(pmc) and not split:
             pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{n}.json")   # round-1 name
@@ -642,6 +666,7 @@ def main():
             with open(pmc) as fh:
                 pj = json.load(fh)
             traffic = pj.get("hbm_bytes_per_launch")
+            issue = issue_roofline(pj.get("avg", {}), launch_s)
             traffic_src = {"file": os.path.relpath(pmc, ROOT), "measured": pj.get("measured", "round 1 (r01i/r01q)"),
                            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes "
                                      "(scripts/profile_workload.sh, scripts/pmc_traffic.py)"}
@@ -679,6 +704,8 @@ def main():
                          "hbm_peak_gbs": PEAK_HBM_GBS, "hbm_copy_gbs_measured": copy_gbs},
             "replicas_identical": replicas,
         }
+        if issue is not None:
+            out["roofline_issue"] = issue
         if other is not None:
             out["other_f32_mode"] = other
         if strong is not None:
