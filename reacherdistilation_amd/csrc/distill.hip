@@ -192,6 +192,14 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // the MFMA still reads (found statically with scripts/isa/hazards.py, confirmed
 // by profiles/r03_srcc_probe_*.txt).  The consumer-side-env-step kernels (bf16 student) fence
 // their teacher's f32 MFMAs; -DRD_MFMA_SRCC_FENCE fences every group (diagnostic builds).
+#ifndef RDD_DW2_SPLIT   // f32_split: dW2 on split bf16 MFMAs (dw2_split; 0: f32 MFMAs, A/B builds)
+#define RDD_DW2_SPLIT 1
+#endif
+constexpr bool kDw2Split = RDD_DW2_SPLIT != 0;
+#ifndef RDD_L1_SPLIT    // f32_split teacher beside the bf16 student: layer 1 on split bf16 MFMAs
+#define RDD_L1_SPLIT 1      // (layer1_split; 0: f32 MFMAs, SrcC-fenced in the consumer-side-step kernels)
+#endif
+constexpr bool kL1Split = RDD_L1_SPLIT != 0;
 #ifdef RD_MFMA_SRCC_FENCE
 constexpr bool kFenceAll = true;
 #else
@@ -601,6 +609,60 @@ __device__ __forceinline__ void split8(f32x4 lo, f32x4 hi, bf16x8 (&p)[3]) {
     p[2] = __builtin_bit_cast(bf16x8, q2);
 }
 
+// split1 on four values, as bit patterns whose high halves are the pieces (split8's arithmetic)
+__device__ __forceinline__ void split4(const float (&x)[4], uint32_t (&u0)[4], uint32_t (&u1)[4],
+                                       uint32_t (&u2)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+        const f32x2 xv = {x[i], x[i + 1]};
+        const uint32_t ua = __float_as_uint(x[i]), ub = __float_as_uint(x[i + 1]);
+        const f32x2 r = xv - f32x2{__uint_as_float(ua & 0xffff0000u), __uint_as_float(ub & 0xffff0000u)};
+        const uint32_t ra = __float_as_uint(r[0]), rb = __float_as_uint(r[1]);
+        const f32x2 l = r - f32x2{__uint_as_float(ra & 0xffff0000u), __uint_as_float(rb & 0xffff0000u)};
+        u0[i] = ua; u0[i + 1] = ub; u1[i] = ra; u1[i + 1] = rb;
+        u2[i] = __float_as_uint(l[0]); u2[i + 1] = __float_as_uint(l[1]);
+    }
+}
+// one bf16 pair (lo = high half of a, hi = high half of b)
+__device__ __forceinline__ uint32_t pair_hi(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+
+// dW2 += H1^T dZ2 over a tile's 16 envs (K = env) as f32 emulated on v_mfma_f32_16x16x32_bf16
+// (f32_split).  x[b][e] = H1[16b + j][env 4g + e], y[b][e] = dZ2[16b + j][env 4g + e]: lane
+// group g holds envs 4g..4g+3 and a K = 32 step carries two pieces of each of them (slots 2e,
+// 2e + 1 of the lane's eight), so the six products of order >= 2^-16 take three MFMAs per
+// block: x0y2 + x2y0, x0y1 + x1y1, x0y0 + x1y0 (smallest first) -- 48 bf16 MFMAs per tile
+// instead of 64 f32 ones, which on gfx950 hold the SIMD's VALU issue for their whole 32 cycles.
+__device__ __forceinline__ void dw2_split(const float (&x)[4][4], const float (&y)[4][4], f32x4 (&gW2)[4][4]) {
+    u32x4 a02[4], a01[4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+        uint32_t u0[4], u1[4], u2[4];
+        split4(x[mb], u0, u1, u2);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            a02[mb][e] = pair_hi(u0[e], u2[e]);
+            a01[mb][e] = pair_hi(u0[e], u1[e]);
+        }
+    }
+    uint32_t v0[4][4], v1[4][4], v2[4][4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) split4(y[nb], v0[nb], v1[nb], v2[nb]);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+            u32x4 bq;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                bq[e] = q == 0 ? pair_hi(v2[nb][e], v0[nb][e]) : q == 1 ? pair_hi(v1[nb][e], v1[nb][e])
+                                                                       : pair_hi(v0[nb][e], v0[nb][e]);
+            const bf16x8 b = __builtin_bit_cast(bf16x8, bq);
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+                gW2[mb][nb] = mfma_k32(__builtin_bit_cast(bf16x8, q == 0 ? a02[mb] : a01[mb]), b, gW2[mb][nb]);
+        }
+}
+
 // acc += W . X over one K = 32 step from split pieces w[3] (A) and x[3] (B)
 __device__ __forceinline__ f32x4 mfma_split(const bf16x8 (&w)[3], const bf16x8 (&x)[3], f32x4 c) {
     c = mfma_k32(w[2], x[0], c);
@@ -627,8 +689,13 @@ constexpr int NX_W2F = NX_RS + 12;                // 988
 constexpr int NETX = NX_W2F + 3 * SP_PIECE / 2;   // 7132
 constexpr int NX_W2B = NETX;                      // student only
 constexpr int NETX_S = NX_W2B + 3 * SP_PIECE / 2; // 13276
-static_assert(NX_W3 % 4 == 0 && NX_B2 % 4 == 0 && NX_W2F % 4 == 0 && NETX % 4 == 0 && NETX_S % 4 == 0,
-              "16-B aligned split images");
+// teacher only: layer 1 on split bf16 MFMAs (layer1_split), the A operands of its two piece
+// pairings [v 2][g 4][fb 4][i 16][jj 8]: slot jj = 2s + c (s < 3) holds piece (v ? (0,1) : (0,2))[c]
+// of kTanhScale W1[4s + g][16fb + i] (row 11 = b1), slots 6, 7 zero
+constexpr int NX_W1S = NETX;
+constexpr int NETX_T = NX_W1S + 2 * 4 * 4 * 16 * 8 / 2;   // 9180
+static_assert(NX_W3 % 4 == 0 && NX_B2 % 4 == 0 && NX_W2F % 4 == 0 && NETX % 4 == 0 && NETX_S % 4 == 0 &&
+              NETX_T % 4 == 0, "16-B aligned split images");
 
 // the student image's W3 / filter offsets by kind: exact f32 (N_*), split (NX_*), bf16 (NB_*)
 template <int K> struct Off;
@@ -640,6 +707,40 @@ __device__ __forceinline__ void ld_pieces(const float* L, int base, int o, bf16x
     const unsigned short* h = reinterpret_cast<const unsigned short*>(L + base);
 #pragma unroll
     for (int q = 0; q < 3; ++q) w[q] = *reinterpret_cast<const bf16x8*>(h + q * SP_PIECE + o);
+}
+
+// Layer 1 of a split image's net on v_mfma_f32_16x16x32_bf16 (f32 emulated, as dw2_split):
+// lane group g's inputs 4s + g (s < 3; input 11 is the bias input 1) as three pieces each, a
+// K = 32 step carrying two pieces of each input (slots 2s, 2s + 1), the six products of order
+// >= 2^-16 in three MFMAs per output block: w0z2 + w2z0, w0z1 + w1z1, w0z0 + w1z0.  12 bf16
+// MFMAs instead of 12 f32 ones, which hold the SIMD's VALU issue for 32 cycles each and read
+// their SrcC for 8 passes (the hazard the consumer-side-step kernels had to fence).
+__device__ __forceinline__ void split_bits(float x, uint32_t& u0, uint32_t& u1, uint32_t& u2) {
+    u0 = __float_as_uint(x);
+    const float r = x - __uint_as_float(u0 & 0xffff0000u);
+    u1 = __float_as_uint(r);
+    u2 = __float_as_uint(r - __uint_as_float(u1 & 0xffff0000u));
+}
+__device__ __forceinline__ void layer1_split(const float* L, const float* ob, int j, int g, f32x4 (&acc)[4]) {
+    u32x4 b[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        const int k = 4 * s + g;
+        const float z = fminf(fmaxf((ob[j * SOS + k] - L[NX_MU + k]) * L[NX_RS + k], -5.0f), 5.0f);
+        uint32_t z0, z1, z2;
+        split_bits(z, z0, z1, z2);
+        b[0][s] = pair_hi(z2, z0);
+        b[1][s] = pair_hi(z1, z1);
+        b[2][s] = pair_hi(z0, z0);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        b[q][3] = 0u;
+        const bf16x8 bq = __builtin_bit_cast(bf16x8, b[q]);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb)
+            acc[fb] = mfma_k32(ldbf8(L + NX_W1S, ((((q ? 1 : 0) * 4 + g) * 4 + fb) * 16 + j) * 8), bq, acc[fb]);
+    }
 }
 
 // Teacher and student forwards of one tile with split images (both nets, interleaved):
@@ -722,6 +823,9 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
     f32x4 acc[4];
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (kL1Split) {
+        layer1_split(L, ob, j, g, acc);
+    } else {
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
         const int k = 4 * s + g;
@@ -731,6 +835,7 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
 #pragma unroll
         for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], z, acc[fb]);
         fence_end<FENCE>(acc);
+    }
     }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
@@ -784,12 +889,16 @@ __device__ __forceinline__ void pack_param(float* img, int p, float v, bool stud
     if (kind == IMG_SPLIT) {
         unsigned short* h = reinterpret_cast<unsigned short*>(img);
         unsigned short q[3];
-        if (p < P_B1) {
-            const int k = p >> 6, f = p & 63;
+        if (p < P_W2) {   // W1 rows 0..10, b1 as row 11
+            const int k = p < P_B1 ? p >> 6 : OBD, f = p < P_B1 ? p & 63 : p - P_B1;
             img[NX_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
-        } else if (p < P_W2) {
-            const int f = p - P_B1;
-            img[NX_W1 + OBD * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+            if (!student) {   // layer1_split's A operands: slots 2s, 2s + 1 of lane group k & 3
+                split1(kTanhScale * v, q);
+                const int o = 2 * NX_W1S + (((k & 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + 2 * (k >> 2);
+                constexpr int V1 = 4 * 4 * 16 * 8;   // the (0,1) pairing follows the (0,2) one
+                h[o] = q[0]; h[o + 1] = q[2];
+                h[o + V1] = q[0]; h[o + V1 + 1] = q[1];
+            }
         } else if (p < P_B2) {
             const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
             {   // forward: k is the permuted K index (as NB_W2F), pieces of the scaled weight
@@ -1060,16 +1169,16 @@ __device__ __forceinline__ void bump_ctl(const ReduceArgs& a, uint32_t C, uint32
 }
 
 // LDS floats of the teacher / student images of a rollout instance
-constexpr int img_t(bool SPL) { return SPL ? NETX : NET; }
+constexpr int img_t(bool BS, bool SPL) { return SPL ? (BS && kL1Split ? NETX_T : NETX) : NET; }
 constexpr int img_s(bool BS, bool SPL) { return BS ? NETB_S : (SPL ? NETX_S : NET_S); }
-static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NETB_S + PAIRS * PSCR) * 4 <= 160 * 1024,
+static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX_T + NETB_S + PAIRS * PSCR) * 4 <= 160 * 1024,
               "LDS budget (split images)");
 
 // BS: bf16 student (RDD_DTYPE_BF16); SPL: split-bf16 f32 hidden layers; CP: the consumer wave
 // steps the envs (else the producer does, from the state it loaded for the observations)
 template <bool BS, bool SPL, bool CP>
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
-    constexpr int TN = img_t(SPL), SN = img_s(BS, SPL);
+    constexpr int TN = img_t(BS, SPL), SN = img_s(BS, SPL);
     __shared__ __attribute__((aligned(16))) float lds[TN + SN + PAIRS * PSCR];
     float* LT = lds;
     float* LS = lds + TN;
@@ -1355,13 +1464,21 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                         acc[mb] = mfma_k32(ldbf8(LS + NB_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8), db, acc[mb]);
                 }
             } else {
+                // S2: dW2 on split bf16 MFMAs, x[b][e] / y[b][e] over envs 4g+e (dw2_split);
+                // else f32 MFMAs, x[s][b] / y[s][b] over env 4s+g (k-step s)
+                constexpr bool S2 = SPL && kDw2Split;
                 float x[4][4], y[4][4];
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
-                        x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
-                        y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
+                        if constexpr (S2) {
+                            x[b][s] = h1t[(4 * g + s) * SAS + 16 * b + j];   // H1[16b + j][env 4g+s]
+                            y[b][s] = dzt[(4 * g + s) * SAS + 16 * b + j];   // dZ2[16b + j][env 4g+s]
+                        } else {
+                            x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
+                            y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
+                        }
                     }
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
@@ -1375,6 +1492,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 publish(flags + 1, ++tiles);
                 STAMP(13);
                 // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
+                if constexpr (S2) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) gb2[b] += (y[b][0] + y[b][1]) + (y[b][2] + y[b][3]);
+                    dw2_split(x, y, gW2);
+                } else {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
 #pragma unroll
@@ -1383,6 +1505,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
                         for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[s][mb], y[s][nb], gW2[mb][nb]);
+                }
                 }
                 // dH1 = W2 . dZ2 (A = W2^T image)
 #pragma unroll
@@ -1681,7 +1804,7 @@ int student_kind(const rdd_trainer* t) {
     return t->cfg.student_dtype == RDD_DTYPE_BF16 ? IMG_BF16 : (t->cfg.f32_split ? IMG_SPLIT : IMG_F32);
 }
 int image_floats(int kind, bool student) {
-    if (kind == IMG_SPLIT) return student ? NETX_S : NETX;
+    if (kind == IMG_SPLIT) return student ? NETX_S : NETX_T;
     if (kind == IMG_BF16) return NETB_S;
     return student ? NET_S : NET;
 }
