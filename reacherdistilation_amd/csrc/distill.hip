@@ -83,17 +83,19 @@ static_assert(N_B2 % 4 == 0 && N_W3 % 4 == 0 && NET % 4 == 0, "16-B aligned LDS 
 constexpr int PAIRS = WAVES / 2;
 constexpr int SOS = 12;                         // raw obs rows (11 + the bias input = 1)
 constexpr int SAS = 68;                         // transposed activation rows [env][64 + pad]
-constexpr int P_SO = 0;                         // [2][64][12] raw obs, by group parity
-constexpr int P_ACT = P_SO + 2 * GROUP * SOS;   // [2][64][2] actions, by group parity
-constexpr int P_H1T = P_ACT + 2 * GROUP * 2;    // slot: H1^T [16][SAS]
+constexpr int P_SO = 0;                         // [64][12] raw obs of the producer's group (its own)
+constexpr int P_ACT = P_SO + GROUP * SOS;       // [64][2] actions (the producer's env step)
+constexpr int P_H1T = P_ACT + GROUP * 2;        // slot: H1^T [16][SAS]
 constexpr int P_DZT = P_H1T + TILE * SAS;       // slot: dZ2^T [16][SAS]
 constexpr int P_SA = P_DZT + TILE * SAS;        // consumer-private: dZ1^T [16][SAS]
-constexpr int P_SACT = P_SA + TILE * SAS;       // slot: the tile's actions [16][2] (CP: for the consumer's env step)
-constexpr int P_FLAGS = P_SACT + TILE * 2;      // u32 [0] tiles published [1] tiles consumed [2] groups done
+constexpr int P_SOB = P_SA + TILE * SAS;        // slot: the tile's raw obs rows [16][12] (the consumer's dW1 inputs)
+constexpr int P_SACT = P_SOB + TILE * SOS;      // slot: the tile's actions [16][2] (CP: for the consumer's env step)
+constexpr int P_FLAGS = P_SACT + TILE * 2;      // u32 [0] tiles published [1] tiles consumed
 constexpr int PSCR = P_FLAGS + 4;
 constexpr int LDS_FLOATS = NET + NET_S + PAIRS * PSCR;
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
-static_assert(PSCR % 4 == 0 && P_H1T % 4 == 0 && P_DZT % 4 == 0 && P_SA % 4 == 0, "16-B aligned scratch");
+static_assert(PSCR % 4 == 0 && P_H1T % 4 == 0 && P_DZT % 4 == 0 && P_SA % 4 == 0 && P_SOB % 4 == 0,
+              "16-B aligned scratch");
 // Final per-workgroup reduction: pair p fills LDS region p.  The 76 rows of 64 that hold
 // W1 (with b1 as row 11) and W2 are stored with a row stride of 68 floats, so that the
 // consumer's register-layout writes (lane (g, j) -> row 4g + r, column j) hit 64 distinct
@@ -673,29 +675,28 @@ __device__ __forceinline__ f32x4 mfma_split(const bf16x8 (&w)[3], const bf16x8 (
     return mfma_k32(w[0], x[0], c);
 }
 
-// Split-mode image of a net (offsets in floats): W1 [12][16][4] f32 (as N_W1, scaled) and the
-// small vectors first, then the three pieces of the scaled W2 in the bf16 student's permuted
-// forward order [q][s 2][g 4][fb 4][i 16][jj 8] = piece q of kTanhScale W2[kperm(s,g,jj)][16fb+i];
-// the student adds the pieces of the unscaled W2 for dH1 in the NB_W2B order.
+// Split-mode image of a net (offsets in floats): the small vectors first, then the three
+// pieces of the scaled W2 in the bf16 student's permuted forward order
+// [q][s 2][g 4][fb 4][i 16][jj 8] = piece q of kTanhScale W2[kperm(s,g,jj)][16fb+i], then layer 1:
+// with kL1Split (the product) the A operands of layer1_split's two piece pairings
+// [v 2][g 4][fb 4][i 16][jj 8]: slot jj = 2s + c (s < 3) holds piece (v ? (0,1) : (0,2))[c] of
+// kTanhScale W1[4s + g][16fb + i] (row 11 = b1), slots 6, 7 zero; else W1 [12][16][4] f32 (as
+// N_W1, scaled).  The student adds the pieces of the unscaled W2 for dH1 in the NB_W2B order.
 constexpr int SP_PIECE = 2 * 4 * 4 * 16 * 8;      // bf16 elements per piece
-constexpr int NX_W1 = 0;
-constexpr int NX_B2 = NX_W1 + 12 * HID;           // 768
-constexpr int NX_W3 = NX_B2 + HID;                // 832
-constexpr int NX_B3 = NX_W3 + HID * ACD;          // 960
+constexpr int NX_B2 = 0;
+constexpr int NX_W3 = NX_B2 + HID;                // 64
+constexpr int NX_B3 = NX_W3 + HID * ACD;          // 192
 constexpr int NX_LS = NX_B3 + ACD;
 constexpr int NX_MU = NX_LS + ACD;
 constexpr int NX_RS = NX_MU + 12;
-constexpr int NX_W2F = NX_RS + 12;                // 988
-constexpr int NETX = NX_W2F + 3 * SP_PIECE / 2;   // 7132
+constexpr int NX_W2F = NX_RS + 12;                // 220
+constexpr int NX_W1S = NX_W2F + 3 * SP_PIECE / 2; // 6364 (kL1Split)
+constexpr int NX_W1 = NX_W1S;                     // (RDD_L1_SPLIT=0 builds)
+constexpr int NETX = NX_W1 + (kL1Split ? 2 * 4 * 4 * 16 * 8 / 2 : 12 * HID);   // 8412 (7132)
 constexpr int NX_W2B = NETX;                      // student only
-constexpr int NETX_S = NX_W2B + 3 * SP_PIECE / 2; // 13276
-// teacher only: layer 1 on split bf16 MFMAs (layer1_split), the A operands of its two piece
-// pairings [v 2][g 4][fb 4][i 16][jj 8]: slot jj = 2s + c (s < 3) holds piece (v ? (0,1) : (0,2))[c]
-// of kTanhScale W1[4s + g][16fb + i] (row 11 = b1), slots 6, 7 zero
-constexpr int NX_W1S = NETX;
-constexpr int NETX_T = NX_W1S + 2 * 4 * 4 * 16 * 8 / 2;   // 9180
-static_assert(NX_W3 % 4 == 0 && NX_B2 % 4 == 0 && NX_W2F % 4 == 0 && NETX % 4 == 0 && NETX_S % 4 == 0 &&
-              NETX_T % 4 == 0, "16-B aligned split images");
+constexpr int NETX_S = NX_W2B + 3 * SP_PIECE / 2; // 14556 (13276)
+static_assert(NX_W3 % 4 == 0 && NX_B2 % 4 == 0 && NX_W2F % 4 == 0 && NX_W1 % 4 == 0 && NETX % 4 == 0 &&
+              NETX_S % 4 == 0, "16-B aligned split images");
 
 // the student image's W3 / filter offsets by kind: exact f32 (N_*), split (NX_*), bf16 (NB_*)
 template <int K> struct Off;
@@ -744,13 +745,18 @@ __device__ __forceinline__ void layer1_split(const float* L, const float* ob, in
 }
 
 // Teacher and student forwards of one tile with split images (both nets, interleaved):
-// layer 1 exact f32 (K = 12, as mlp_forward_pair), layer 2 on split bf16 MFMAs.
+// layer 1 on split bf16 MFMAs (layer1_split; RDD_L1_SPLIT=0 builds: exact f32, K = 12, as
+// mlp_forward_pair), layer 2 on split bf16 MFMAs.
 __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const float* LS, const float* ob, int j, int g,
                                                        f32x4 (&H1)[4], f32x4 (&H2)[4], float& mt0, float& mt1,
                                                        float& ms0, float& ms1) {
     f32x4 at[4], as[4];
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) at[fb] = as[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (kL1Split) {
+        layer1_split(LT, ob, j, g, at);
+        layer1_split(LS, ob, j, g, as);
+    } else
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
         const int k = 4 * s + g;
@@ -891,13 +897,14 @@ __device__ __forceinline__ void pack_param(float* img, int p, float v, bool stud
         unsigned short q[3];
         if (p < P_W2) {   // W1 rows 0..10, b1 as row 11
             const int k = p < P_B1 ? p >> 6 : OBD, f = p < P_B1 ? p & 63 : p - P_B1;
-            img[NX_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
-            if (!student) {   // layer1_split's A operands: slots 2s, 2s + 1 of lane group k & 3
+            if constexpr (kL1Split) {   // layer1_split's A operands: slots 2s, 2s + 1 of lane group k & 3
                 split1(kTanhScale * v, q);
                 const int o = 2 * NX_W1S + (((k & 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + 2 * (k >> 2);
                 constexpr int V1 = 4 * 4 * 16 * 8;   // the (0,1) pairing follows the (0,2) one
                 h[o] = q[0]; h[o + 1] = q[2];
                 h[o + V1] = q[0]; h[o + V1 + 1] = q[1];
+            } else {
+                img[NX_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
             }
         } else if (p < P_B2) {
             const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
@@ -1169,16 +1176,16 @@ __device__ __forceinline__ void bump_ctl(const ReduceArgs& a, uint32_t C, uint32
 }
 
 // LDS floats of the teacher / student images of a rollout instance
-constexpr int img_t(bool BS, bool SPL) { return SPL ? (BS && kL1Split ? NETX_T : NETX) : NET; }
+constexpr int img_t(bool SPL) { return SPL ? NETX : NET; }
 constexpr int img_s(bool BS, bool SPL) { return BS ? NETB_S : (SPL ? NETX_S : NET_S); }
-static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX_T + NETB_S + PAIRS * PSCR) * 4 <= 160 * 1024,
+static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NETB_S + PAIRS * PSCR) * 4 <= 160 * 1024,
               "LDS budget (split images)");
 
 // BS: bf16 student (RDD_DTYPE_BF16); SPL: split-bf16 f32 hidden layers; CP: the consumer wave
 // steps the envs (else the producer does, from the state it loaded for the observations)
 template <bool BS, bool SPL, bool CP>
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
-    constexpr int TN = img_t(BS, SPL), SN = img_s(BS, SPL);
+    constexpr int TN = img_t(SPL), SN = img_s(BS, SPL);
     __shared__ __attribute__((aligned(16))) float lds[TN + SN + PAIRS * PSCR];
     float* LT = lds;
     float* LS = lds + TN;
@@ -1214,7 +1221,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         } else {
             rd::observe<false>(st, ob);
         }
-        float* o = PS + P_SO + (k & 1) * GROUP * SOS + lane * SOS;
+        float* o = PS + P_SO + lane * SOS;
         st4(o, f32x4{ob[0], ob[1], ob[2], ob[3]});
         st4(o + 4, f32x4{ob[4], ob[5], ob[6], ob[7]});
         st4(o + 8, f32x4{ob[8], ob[9], ob[10], 1.0f});
@@ -1253,14 +1260,12 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         uint32_t k = 0;
         bool ok = true;
         for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
-            // the consumer is done with group k-2 (same obs/action buffers)
-            if (k >= 2 && !(ok = wait_ge(flags + 2, k - 1, err))) break;
             STAMP(8);
             const uint32_t base = grp * (uint32_t)gs;
             const uint32_t i = base + (uint32_t)lane;   // n <= 2^31 (rdd_create)
             const bool lvalid = lane < gs && i < n32;   // this lane has an env
-            float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
-            float* act = PS + P_ACT + (k & 1) * GROUP * 2;
+            float* obs = PS + P_SO;
+            float* act = PS + P_ACT;
             rd::State st{};   // this lane's env, kept in registers for the env.step after the tiles
             if (k == 0) {
                 st = st0;   // observations formed in the prologue
@@ -1339,6 +1344,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     st4(h1t + j * SAS + 16 * fb + 4 * g, H1[fb]);
                     st4(dzt + j * SAS + 16 * fb + 4 * g, dZ[fb]);
                 }
+                if (lane < TILE * SOS / 4) st4(PS + P_SOB + 4 * lane, ld4(obt + 4 * lane));
                 if (CP && g == 0) {   // the consumer steps these envs: their actions travel with the slot
                     PS[P_SACT + 2 * j] = a.act_student ? ms0 : mt0;
                     PS[P_SACT + 2 * j + 1] = a.act_student ? ms1 : mt1;
@@ -1412,16 +1418,20 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         float met_r = 0.0f, met_n = 0.0f;   // CP: reward and env count of the envs this wave steps
         uint32_t tiles = 0;   // tiles taken from the slot (the pair's global tile count)
         bool ok = true;
-        // backward of tile t of the group whose observations are at obs: its slot is taken
-        // (tiles + 1 published), read, freed, and its gradients accumulated
+        // backward of the pair's next tile (tile t of its group): its slot is taken (tiles + 1
+        // published), read, freed, and its gradients accumulated
         float act0 = 0.0f, act1 = 0.0f;   // CP: the action of this lane's env (taken from its tile's slot)
-        auto bwd_tile = [&](const float* obs, int t) -> bool {
+        auto bwd_tile = [&](int t) -> bool {
             STAMP(2);
             if (!wait_ge(flags, tiles + 1, err)) return false;
             STAMP(3);
             // read the whole slot, then free it for the producer's next tile
             const float* h1t = PS + P_H1T;
             const float* dzt = PS + P_DZT;
+            // dW1 inputs: raw input j of the tile's envs 4g + e (BS) / 4e + g, e < 4
+            float xin[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xin[e] = PS[P_SOB + (BS ? 4 * g + e : 4 * e + g) * SOS + (j < 12 ? j : 0)];
             f32x4 H1[4], dZ[4], acc[4];
             if constexpr (BS) {
                 // dW2 operands over the tile's envs 4g..4g+3 (K = 16 envs), rounded to bf16
@@ -1524,19 +1534,29 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                         }
                     }
                 } else {
-                f32x4 wn = ld4(LS + N_W2T + (4 * g) * HID + 4 * j);
+                // exact f32, k-step (fb, r) = W2^T row 16fb + 4g + r.  Each fb group of 16 MFMAs is
+                // SrcC-fenced and its operands are loaded one group ahead, before the previous
+                // group's fence: no load issues while an f32 MFMA of this loop is in flight (the
+                // one-step-ahead prefetch let the compiler issue W2^T loads into in-flight SrcC
+                // registers 4-5 wait states after the MFMA; see mfma()).
+                f32x4 wc[4], wn[4];
 #pragma unroll
-                for (int fb = 0; fb < 4; ++fb)
+                for (int r = 0; r < 4; ++r) wc[r] = ld4(LS + N_W2T + (4 * g + r) * HID + 4 * j);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const f32x4 w = wn;
-                        if (fb * 4 + r < 15) {
-                            const int kn = (r == 3) ? 16 * (fb + 1) + 4 * g : 16 * fb + 4 * g + r + 1;
-                            wn = ld4(LS + N_W2T + kn * HID + 4 * j);
-                        }
+                for (int fb = 0; fb < 4; ++fb) {
+                    if (fb < 3) {
 #pragma unroll
-                        for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(w[mb], dZ[fb][r], acc[mb]);
+                        for (int r = 0; r < 4; ++r) wn[r] = ld4(LS + N_W2T + (16 * (fb + 1) + 4 * g + r) * HID + 4 * j);
                     }
+                    fence_begin<true>(acc);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma(wc[r][mb], dZ[fb][r], acc[mb]);
+                    fence_end<true>(acc);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) wc[r] = wn[r];
+                }
                 }
             }
             STAMP(14);
@@ -1549,13 +1569,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             }
             wave_sync();
             // dW1 (+ db1 as input row 11) += z^T dZ1; A = student-filtered inputs of env 4s+g
-            const float* obt = obs + TILE * t * SOS;
             if constexpr (BS) {   // K = the tile's 16 envs (4g + jj), operands rounded to bf16
                 float zz[4];
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
-                    const float xv = obt[(4 * g + jj) * SOS + (j < 12 ? j : 0)];
-                    zz[jj] = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
+                    zz[jj] = j < 12 ? fminf(fmaxf((xin[jj] - smu) * srs, -5.0f), 5.0f) : 0.0f;
                 }
                 const s16x4 za = pack4(zz[0], zz[1], zz[2], zz[3]);
 #pragma unroll
@@ -1567,8 +1585,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             } else {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
-                    const float xv = obt[(4 * s + g) * SOS + (j < 12 ? j : 0)];
-                    const float z = j < 12 ? fminf(fmaxf((xv - smu) * srs, -5.0f), 5.0f) : 0.0f;
+                    const float z = j < 12 ? fminf(fmaxf((xin[s] - smu) * srs, -5.0f), 5.0f) : 0.0f;
 #pragma unroll
                     for (int nb = 0; nb < 4; ++nb) gW1[nb] = mfma(z, sa[(4 * s + g) * SAS + 16 * nb + j], gW1[nb]);
                 }
@@ -1577,9 +1594,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             STAMP(15);
             return true;
         };
-        // after the last tile of group k (envs base ...): CP steps the envs; the group's
-        // obs/act buffers are then free
-        auto end_group = [&](uint32_t k, uint32_t base) {
+        // after the last tile of a group (envs base ...): CP steps the envs
+        auto end_group = [&](uint32_t base) {
             const uint32_t i = base + (uint32_t)lane;
             const bool lvalid = lane < gs && i < n32;
             if constexpr (CP) {
@@ -1593,16 +1609,13 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 }
                 STAMP(5);
             }
-            publish(flags + 2, k + 1);   // the obs/act buffers of group k may be reused
         };
-        uint32_t k = 0;
-        for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
+        for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride) {
             const uint32_t base = grp * (uint32_t)gs;
-            const float* obs = PS + P_SO + (k & 1) * GROUP * SOS;
             const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
-            for (int t = 0; ok && t < ntile; ++t) ok = bwd_tile(obs, t);
+            for (int t = 0; ok && t < ntile; ++t) ok = bwd_tile(t);
             if (!ok) break;
-            end_group(k, base);
+            end_group(base);
         }
         // ------------------------------------------------------------ this wave's share
 #pragma unroll
@@ -1804,7 +1817,7 @@ int student_kind(const rdd_trainer* t) {
     return t->cfg.student_dtype == RDD_DTYPE_BF16 ? IMG_BF16 : (t->cfg.f32_split ? IMG_SPLIT : IMG_F32);
 }
 int image_floats(int kind, bool student) {
-    if (kind == IMG_SPLIT) return student ? NETX_S : NETX_T;
+    if (kind == IMG_SPLIT) return student ? NETX_S : NETX;
     if (kind == IMG_BF16) return NETB_S;
     return student ? NET_S : NET;
 }

@@ -10,9 +10,10 @@ byte for byte, and the bench's headline mode is the library's default mode.
   (its consumer runs 80 unfenced f32 MFMAs per tile) exists only in diagnostic
   builds.
 - Statically, in the product's ISA no LDS / global load is issued into a register that an
-  in-flight f32 MFMA (8 passes) still reads as SrcC within 5 wait states -- the pattern that
-  made the unfenced consumer-side step lose loaded values in lanes 48-63
-  (scripts/isa/hazards.py, profiles/r03_srcc_probe_*.txt).
+  in-flight f32 MFMA (8 passes) still reads as SrcC: every such load comes >= 10 wait states
+  after the MFMA, i.e. after it completed -- the pattern that made the unfenced consumer-side
+  step lose loaded values in lanes 48-63 (scripts/isa/hazards.py, profiles/r03_srcc_probe_*.txt).
+  The split kernels (the default mode) have no f32 MFMA followed by such a load at all.
 """
 import ctypes
 import os
@@ -50,9 +51,10 @@ def test_consumer_side_step_only_for_the_bf16_student(libpath):
 
 def test_no_load_into_an_inflight_f32_mfma_srcc():
     """The product's rollout kernels, compiled to ISA here: every LDS / global load whose
-    destination is the SrcC of an earlier v_mfma_f32_16x16x4_f32 issues >= 5 wait states after
-    it; in the fenced bf16-student kernels >= 10, i.e. after the MFMA completed (the compiler's
-    RAW wait for an 8-pass result, NumPasses + 2)."""
+    destination is the SrcC of an earlier v_mfma_f32_16x16x4_f32 issues >= 10 wait states after
+    it, i.e. after the MFMA completed (the compiler's RAW wait for an 8-pass result, NumPasses +
+    2; ROCm 7.2 itself only keeps 3-5 for this WAR).  In the split kernels no load follows an
+    f32 MFMA into its SrcC within the scan window at all (their f32 MFMAs are dW1 only)."""
     import importlib.util
     from reacherdistilation_amd import build
     out = os.path.join(ROOT, "oracle", "_build", "distill_isa.s")
@@ -63,11 +65,13 @@ def test_no_load_into_an_inflight_f32_mfma_srcc():
     spec = importlib.util.spec_from_file_location("hz", os.path.join(ROOT, "scripts", "isa", "hazards.py"))
     hz = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(hz)
-    for sym, floor in (("rollout_kernelILb0ELb0ELb0E", 5), ("rollout_kernelILb0ELb1ELb0E", 5),
-                       ("rollout_kernelILb1ELb0ELb1E", 10), ("rollout_kernelILb1ELb1ELb1E", 10)):
+    for sym, split in (("rollout_kernelILb0ELb0ELb0E", False), ("rollout_kernelILb0ELb1ELb0E", True),
+                       ("rollout_kernelILb1ELb0ELb1E", False), ("rollout_kernelILb1ELb1ELb1E", True)):
         hits = [h for h in hz.scan(out, sym, 40)[0] if h[0] == "WARc" and "16x16x4" in h[4]
                 and h[6].split()[0].startswith(("ds_read", "global_load", "buffer_load"))]
-        assert all(h[1] >= floor for h in hits), (sym, [h[:6] for h in hits if h[1] < floor][:5])
+        assert all(h[1] >= 10 for h in hits), (sym, [h[:6] for h in hits if h[1] < 10][:5])
+        if split:
+            assert not hits, (sym, [h[:6] for h in hits][:5])
 
 
 def _c_layout(struct, header, fields):
