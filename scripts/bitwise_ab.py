@@ -16,6 +16,8 @@ CASES = {   # name: DistillConfig overrides
     "grid7_kl": dict(n_envs=3000, loss="kl", grid=7),
     "grid300": dict(n_envs=300 * 4 * 64, grid=300),
     "accum3": dict(n_envs=20000, accum_steps=3),
+    "c3_exact": dict(n_envs=65536, loss="kl", f32_split=False),
+    "c5_exact": dict(n_envs=131072, act_with="student", student_dtype="bf16", f32_split=False),
 }
 
 
