@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include <new>
+#include <type_traits>
 
 #include "../../include/reacher_distill.h"
 #include "rd_comm_impl.h"
@@ -315,6 +316,36 @@ __device__ __forceinline__ void load_state(const float* s, int64_t n, uint32_t i
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// Global stores, plain or non-temporal (NT).  The rollout writes its partial row with NT
+// stores from WS_NT_MIN_GRID workgroups up (profiles/r03k_nt_stores.txt: c5
+// step -0.55 us, c3 -0.25, c4 -0.2; at c2's 64 workgroups +0.2 us, so plain there).  Diagnostic
+// builds make the reduce+Adam kernel's stores (-DRD_NT_RED) or the rollout's state stores
+// (-DRD_NT_STATE) NT as well: neither gained, so the product keeps them plain.
+#ifdef RD_NT_RED
+constexpr bool kNtRed = true;
+#else
+constexpr bool kNtRed = false;
+#endif
+#ifdef RD_NT_STATE
+constexpr bool kNtState = true;
+#else
+constexpr bool kNtState = false;
+#endif
+#ifndef RD_WS_NT_MIN_GRID
+#define RD_WS_NT_MIN_GRID 128
+#endif
+constexpr unsigned WS_NT_MIN_GRID = RD_WS_NT_MIN_GRID;   // 0: always NT (compile-time), 1u<<30: never
+template <bool NT, class T>
+__device__ __forceinline__ void gst(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+// a non-temporal 16-B vector store the compiler cannot merge with a plain one (tail merging of
+// the two variants of a store burst drops the nt hint of one of them)
+__device__ __forceinline__ void st4_nt(float* p, f32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+}
 
 // global net = params[P] | mu[11] | sd[11]  ->  LDS image (+ W2^T if `transposed`); the
 // forward images of W1, b1, W2, b2 carry the tanh scale (kTanhScale)
@@ -901,10 +932,10 @@ __device__ __forceinline__ void pack_param(float* img, int p, float v, bool stud
                 split1(kTanhScale * v, q);
                 const int o = 2 * NX_W1S + (((k & 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + 2 * (k >> 2);
                 constexpr int V1 = 4 * 4 * 16 * 8;   // the (0,1) pairing follows the (0,2) one
-                h[o] = q[0]; h[o + 1] = q[2];
-                h[o + V1] = q[0]; h[o + V1 + 1] = q[1];
+                gst<kNtRed>(h + (o), q[0]); gst<kNtRed>(h + (o + 1), q[2]);
+                gst<kNtRed>(h + (o + V1), q[0]); gst<kNtRed>(h + (o + V1 + 1), q[1]);
             } else {
-                img[NX_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+                gst<kNtRed>(img + (NX_W1 + k * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
             }
         } else if (p < P_B2) {
             const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
@@ -912,73 +943,73 @@ __device__ __forceinline__ void pack_param(float* img, int p, float v, bool stud
                 const int s = k >> 5, r = k & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
                 const int o = 2 * NX_W2F + (((s * 4 + gg) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + jj;
                 split1(kTanhScale * v, q);
-                h[o] = q[0]; h[o + SP_PIECE] = q[1]; h[o + 2 * SP_PIECE] = q[2];
+                gst<kNtRed>(h + (o), q[0]); gst<kNtRed>(h + (o + SP_PIECE), q[1]); gst<kNtRed>(h + (o + 2 * SP_PIECE), q[2]);
             }
             if (student) {   // dH1: f is the permuted K index (as NB_W2B), unscaled
                 const int s = f >> 5, r = f & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
                 const int o = 2 * NX_W2B + (((s * 4 + gg) * 4 + (k >> 4)) * 16 + (k & 15)) * 8 + jj;
                 split1(v, q);
-                h[o] = q[0]; h[o + SP_PIECE] = q[1]; h[o + 2 * SP_PIECE] = q[2];
+                gst<kNtRed>(h + (o), q[0]); gst<kNtRed>(h + (o + SP_PIECE), q[1]); gst<kNtRed>(h + (o + 2 * SP_PIECE), q[2]);
             }
         } else if (p < P_W3) {
-            img[NX_B2 + (p - P_B2)] = kTanhScale * v;
+            gst<kNtRed>(img + (NX_B2 + (p - P_B2)), kTanhScale * v);
         } else if (p < P_B3) {
-            img[NX_W3 + (p - P_W3)] = v;
+            gst<kNtRed>(img + (NX_W3 + (p - P_W3)), v);
         } else if (p < P_LS) {
-            img[NX_B3 + (p - P_B3)] = v;
+            gst<kNtRed>(img + (NX_B3 + (p - P_B3)), v);
         } else if (p < P_TOT) {
-            img[NX_LS + (p - P_LS)] = v;
+            gst<kNtRed>(img + (NX_LS + (p - P_LS)), v);
         }
         return;
     }
     if (kind == IMG_F32) {
         if (p < P_B1) {
             const int k = p >> 6, f = p & 63;
-            img[N_W1 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+            gst<kNtRed>(img + (N_W1 + k * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
         } else if (p < P_W2) {
             const int f = p - P_B1;
-            img[N_W1 + OBD * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
+            gst<kNtRed>(img + (N_W1 + OBD * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
         } else if (p < P_B2) {
             const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
-            img[N_W2 + k * HID + (f & 15) * 4 + (f >> 4)] = kTanhScale * v;
-            if (student) img[N_W2T + f * HID + (k & 15) * 4 + (k >> 4)] = v;
+            gst<kNtRed>(img + (N_W2 + k * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
+            if (student) gst<kNtRed>(img + (N_W2T + f * HID + (k & 15) * 4 + (k >> 4)), v);
         } else if (p < P_W3) {
-            img[N_B2 + (p - P_B2)] = kTanhScale * v;
+            gst<kNtRed>(img + (N_B2 + (p - P_B2)), kTanhScale * v);
         } else if (p < P_B3) {
-            img[N_W3 + (p - P_W3)] = v;
+            gst<kNtRed>(img + (N_W3 + (p - P_W3)), v);
         } else if (p < P_LS) {
-            img[N_B3 + (p - P_B3)] = v;
+            gst<kNtRed>(img + (N_B3 + (p - P_B3)), v);
         } else if (p < P_TOT) {
-            img[N_LS + (p - P_LS)] = v;
+            gst<kNtRed>(img + (N_LS + (p - P_LS)), v);
         }
         return;
     }
     unsigned short* h = reinterpret_cast<unsigned short*>(img);
     if (p < P_B1) {
         const int k = p >> 6, f = p & 63;   // k = 8gg + jj
-        h[2 * NB_W1 + (((k >> 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + (k & 7)] = bf16_bits(v);
+        gst<kNtRed>(h + (2 * NB_W1 + (((k >> 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + (k & 7)), bf16_bits(v));
     } else if (p < P_W2) {
-        img[NB_B1 + (p - P_B1)] = v;
+        gst<kNtRed>(img + (NB_B1 + (p - P_B1)), v);
     } else if (p < P_B2) {
         const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
         // forward image: k (H1 feature) is the permuted K index, f the output row
         {
             const int s = k >> 5, r = k & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
-            h[2 * NB_W2F + (((s * 4 + gg) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + jj] = bf16_bits(v);
+            gst<kNtRed>(h + (2 * NB_W2F + (((s * 4 + gg) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + jj), bf16_bits(v));
         }
         // dH1 image: f (dZ2 feature) is the permuted K index, k the output row
         {
             const int s = f >> 5, r = f & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
-            h[2 * NB_W2B + (((s * 4 + gg) * 4 + (k >> 4)) * 16 + (k & 15)) * 8 + jj] = bf16_bits(v);
+            gst<kNtRed>(h + (2 * NB_W2B + (((s * 4 + gg) * 4 + (k >> 4)) * 16 + (k & 15)) * 8 + jj), bf16_bits(v));
         }
     } else if (p < P_W3) {
-        img[NB_B2 + (p - P_B2)] = v;
+        gst<kNtRed>(img + (NB_B2 + (p - P_B2)), v);
     } else if (p < P_B3) {
-        img[NB_W3 + (p - P_W3)] = bf16_round(v);
+        gst<kNtRed>(img + (NB_W3 + (p - P_W3)), bf16_round(v));
     } else if (p < P_LS) {
-        img[NB_B3 + (p - P_B3)] = v;
+        gst<kNtRed>(img + (NB_B3 + (p - P_B3)), v);
     } else if (p < P_TOT) {
-        img[NB_LS + (p - P_LS)] = v;
+        gst<kNtRed>(img + (NB_LS + (p - P_LS)), v);
     }
 }
 
@@ -1107,9 +1138,10 @@ __device__ __forceinline__ float env_step_group(const RolloutArgs& a, uint32_t C
     if (!valid) return 0.0f;
     float* s = a.state;
     const int64_t n = a.n;
-    (s + 0 * n)[iu] = st.q0; (s + 1 * n)[iu] = st.q1; (s + 2 * n)[iu] = st.v0; (s + 3 * n)[iu] = st.v1;
-    if (done_step) { (s + 4 * n)[iu] = st.tx; (s + 5 * n)[iu] = st.ty; }
-    (s + 6 * n)[iu] = st.dx; (s + 7 * n)[iu] = st.dy;
+    gst<kNtState>(s + 0 * n + iu, st.q0); gst<kNtState>(s + 1 * n + iu, st.q1);
+    gst<kNtState>(s + 2 * n + iu, st.v0); gst<kNtState>(s + 3 * n + iu, st.v1);
+    if (done_step) { gst<kNtState>(s + 4 * n + iu, st.tx); gst<kNtState>(s + 5 * n + iu, st.ty); }
+    gst<kNtState>(s + 6 * n + iu, st.dx); gst<kNtState>(s + 7 * n + iu, st.dy);
     met_n += 1.0f;
     return rew;
 }
@@ -1144,10 +1176,10 @@ __device__ __forceinline__ void col_finish(const ReduceArgs& a, int p, const flo
         g = (q[0] + q[1]) + (q[2] + q[3]);
         if (p < P_TOT) {
             if (a.accum) g += a.grad[p];
-            a.grad[p] = g;
+            gst<kNtRed>(a.grad + p, g);
         } else {
             float* h = a.hist + (int64_t)(S % (uint32_t)a.hist_len) * N_MET + (p - P_TOT);
-            *h = a.accum ? *h + g : g;
+            gst<kNtRed>(h, a.accum ? *h + g : g);
         }
     } else {
         g = p < P_TOT ? a.grad[p] : 0.f;
@@ -1157,10 +1189,10 @@ __device__ __forceinline__ void col_finish(const ReduceArgs& a, int p, const flo
         float m = m_p, v = v_p;
         m += (g - m) * (1.0f - a.b1);
         v += (g * g - v) * (1.0f - a.b2);
-        a.m[p] = m;
-        a.v[p] = v;
+        gst<kNtRed>(a.m + p, m);
+        gst<kNtRed>(a.v + p, v);
         const float w = w_p - (m * alpha) / (sqrtf(v) + a.eps);
-        a.params[p] = w;
+        gst<kNtRed>(a.params + p, w);
         pack_param(a.simg, p, w, true, a.img_kind);
     }
 }
@@ -1651,15 +1683,22 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     // two call sites pair up); this second one publishes the regions.
     __syncthreads();
     static_assert(RED_COLS % 4 == 0, "a 16-B store stays inside one workspace chunk");
+    // the row's stores as one straight burst per variant (a branch per store measured no gain)
+    auto store_row = [&](auto nt) {
 #pragma unroll
-    for (int u = 0; u < (P_PAD / 4 + BLOCK - 1) / BLOCK; ++u) {
-        const int p4 = threadIdx.x + u * BLOCK;
-        if (p4 < P_PAD / 4) {
-            const int q = ridx(4 * p4);   // 4 | 64: the four entries stay contiguous
-            st4(a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x),
-                (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q)));
+        for (int u = 0; u < (P_PAD / 4 + BLOCK - 1) / BLOCK; ++u) {
+            const int p4 = threadIdx.x + u * BLOCK;
+            if (p4 < P_PAD / 4) {
+                const int q = ridx(4 * p4);   // 4 | 64: the four entries stay contiguous
+                float* w = a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x);
+                const f32x4 v = (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q));
+                if constexpr (decltype(nt)::value) st4_nt(w, v);
+                else st4(w, v);
+            }
         }
-    }
+    };
+    if (WS_NT_MIN_GRID == 0 || gridDim.x >= WS_NT_MIN_GRID) store_row(std::true_type{});
+    else store_row(std::false_type{});
     STAMP(7);
     RTSTAMP(17);
 }
