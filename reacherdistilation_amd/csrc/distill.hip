@@ -285,9 +285,14 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // state row k of env i: (state + k n)[i] -- uniform 64-bit row base, 32-bit lane offset
+#ifdef RD_NT_LDSTATE   // diagnostic build: the state read as a non-temporal stream
+__device__ __forceinline__ float ldst(const float* p) { return __builtin_nontemporal_load(p); }
+#else
+__device__ __forceinline__ float ldst(const float* p) { return *p; }
+#endif
 __device__ __forceinline__ void load_state(const float* s, int64_t n, uint32_t i, rd::State& st) {
-    st.q0 = (s + 0 * n)[i]; st.q1 = (s + 1 * n)[i]; st.v0 = (s + 2 * n)[i]; st.v1 = (s + 3 * n)[i];
-    st.tx = (s + 4 * n)[i]; st.ty = (s + 5 * n)[i]; st.dx = (s + 6 * n)[i]; st.dy = (s + 7 * n)[i];
+    st.q0 = ldst(s + 0 * n + i); st.q1 = ldst(s + 1 * n + i); st.v0 = ldst(s + 2 * n + i); st.v1 = ldst(s + 3 * n + i);
+    st.tx = ldst(s + 4 * n + i); st.ty = ldst(s + 5 * n + i); st.dx = ldst(s + 6 * n + i); st.dy = ldst(s + 7 * n + i);
 }
 
 // Diagnostic build only (-DRD_STAMPS, libreacher_stamps.so): per-wave s_memtime stamps

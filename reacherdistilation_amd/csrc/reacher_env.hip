@@ -22,6 +22,16 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// The step's outputs (state, obs, rew, done) are written once per step and read by a later
+// kernel, so they are stored non-temporal: +1 % at 16.8M envs, +3.5 % at 4.2M, +4.5 % at 1M
+// against plain stores (profiles/r03n_env_nt.txt; same bits).
+template <class T> __device__ __forceinline__ void ost(T* p, T v) { __builtin_nontemporal_store(v, p); }
+#ifdef RD_ENV_NTLD   // diagnostic build: the state and action read as non-temporal streams
+template <class T> __device__ __forceinline__ T ild(const T* p) { return __builtin_nontemporal_load(p); }
+#else
+template <class T> __device__ __forceinline__ T ild(const T* p) { return *p; }
+#endif
+
 struct ResetSrc {
     int mode;              // RD_RESET_PHILOX / RD_RESET_TABLE
     const float* table;    // [n_episodes][N][6]
@@ -43,16 +53,16 @@ __device__ __forceinline__ void draw_reset(const ResetSrc& src, int64_t n, int64
 
 __device__ __forceinline__ rd::State load_state(const float* __restrict__ s, int64_t n, int64_t i) {
     rd::State st;
-    st.q0 = s[0 * n + i]; st.q1 = s[1 * n + i]; st.v0 = s[2 * n + i]; st.v1 = s[3 * n + i];
-    st.tx = s[4 * n + i]; st.ty = s[5 * n + i]; st.dx = s[6 * n + i]; st.dy = s[7 * n + i];
+    st.q0 = ild(s + 0 * n + i); st.q1 = ild(s + 1 * n + i); st.v0 = ild(s + 2 * n + i); st.v1 = ild(s + 3 * n + i);
+    st.tx = ild(s + 4 * n + i); st.ty = ild(s + 5 * n + i); st.dx = ild(s + 6 * n + i); st.dy = ild(s + 7 * n + i);
     return st;
 }
 
 __device__ __forceinline__ void store_state(float* __restrict__ s, int64_t n, int64_t i, const rd::State& st,
                                             bool target_too) {
-    s[0 * n + i] = st.q0; s[1 * n + i] = st.q1; s[2 * n + i] = st.v0; s[3 * n + i] = st.v1;
-    if (target_too) { s[4 * n + i] = st.tx; s[5 * n + i] = st.ty; }
-    s[6 * n + i] = st.dx; s[7 * n + i] = st.dy;
+    ost(s + 0 * n + i, st.q0); ost(s + 1 * n + i, st.q1); ost(s + 2 * n + i, st.v0); ost(s + 3 * n + i, st.v1);
+    if (target_too) { ost(s + 4 * n + i, st.tx); ost(s + 5 * n + i, st.ty); }
+    ost(s + 6 * n + i, st.dx); ost(s + 7 * n + i, st.dy);
 }
 
 // Write this block's obs rows [base, base+cnt) x 11 via an LDS transpose: lane-strided
@@ -66,11 +76,12 @@ __device__ __forceinline__ void write_obs(float* __restrict__ obs, int64_t base,
     __syncthreads();
     float* dst = obs + base * 11;
     if (cnt == kBlock) {
-        const float4* src4 = reinterpret_cast<const float4*>(lds);
-        float4* dst4 = reinterpret_cast<float4*>(dst);
-        for (int j = t; j < kBlock * 11 / 4; j += kBlock) dst4[j] = src4[j];
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f* src4 = reinterpret_cast<const v4f*>(lds);
+        v4f* dst4 = reinterpret_cast<v4f*>(dst);
+        for (int j = t; j < kBlock * 11 / 4; j += kBlock) ost(dst4 + j, src4[j]);
     } else {
-        for (int j = t; j < cnt * 11; j += kBlock) dst[j] = lds[j];
+        for (int j = t; j < cnt * 11; j += kBlock) ost(dst + j, lds[j]);
     }
 }
 
@@ -107,8 +118,9 @@ __global__ __launch_bounds__(kBlock) void rd_step_kernel(int64_t n, float* __res
     float ob[11];
     if (i < n) {
         rd::State st = load_state(state, n, i);
-        const float2 a = reinterpret_cast<const float2*>(act)[i];
-        const float r = rd::env_step(st, a.x, a.y);
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        const v2f a = ild(reinterpret_cast<const v2f*>(act) + i);
+        const float r = rd::env_step(st, a[0], a[1]);
         if (done_step) {
             float d[6];
             draw_reset(src, n, i, next_episode, d);
@@ -116,8 +128,8 @@ __global__ __launch_bounds__(kBlock) void rd_step_kernel(int64_t n, float* __res
         }
         store_state(state, n, i, st, done_step != 0);
         rd::observe(st, ob);
-        rew[i] = r;
-        done[i] = (uint8_t)(done_step != 0);
+        ost(rew + i, r);
+        ost(done + i, (uint8_t)(done_step != 0));
     }
     write_obs(obs, base, cnt, ob, lds);
 }

@@ -240,6 +240,13 @@ __device__ __forceinline__ void wgrad_layer(const float* H, const float* D, f32x
     }
 }
 
+// partial-row stores: -DRD_MLP_NT (diagnostic build) makes them non-temporal
+#ifdef RD_MLP_NT
+__device__ __forceinline__ void wst(float* p, float v) { __builtin_nontemporal_store(v, p); }
+#else
+__device__ __forceinline__ void wst(float* p, float v) { *p = v; }
+#endif
+
 template <int L>
 __device__ __forceinline__ void store_wgrad(float* ws, const f32x4 (&G)[WG<L>::Q], int wave, int i, int g) {
     using W = WG<L>;
@@ -249,7 +256,7 @@ __device__ __forceinline__ void store_wgrad(float* ws, const f32x4 (&G)[WG<L>::Q
         if (W::ok(wave, t))
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                ws[GW[L] + (16 * W::kb(wave, t) + 4 * g + q) * MP[L] + 16 * cb + i] = G[t][q];
+                wst(ws + GW[L] + (16 * W::kb(wave, t) + 4 * g + q) * MP[L] + 16 * cb + i, G[t][q]);
 }
 
 // bias gradient: thread t < OUT[L] sums column t of dZ_L over the block's rows
@@ -407,11 +414,11 @@ __global__ __launch_bounds__(BLOCK) void student_mlp_kernel(SmArgs a) {
         store_wgrad<2>(ws, G2, wave, i, g);
         store_wgrad<3>(ws, G3, wave, i, g);
         store_wgrad<4>(ws, G4, wave, i, g);
-        if (tid < OUT[0]) ws[GB[0] + tid] = gb0;
-        if (tid < OUT[1]) ws[GB[1] + tid] = gb1;
-        if (tid < OUT[2]) ws[GB[2] + tid] = gb2;
-        if (tid < OUT[3]) ws[GB[3] + tid] = gb3;
-        if (tid < OUT[4]) ws[GB[4] + tid] = gb4;
+        if (tid < OUT[0]) wst(ws + GB[0] + tid, gb0);
+        if (tid < OUT[1]) wst(ws + GB[1] + tid, gb1);
+        if (tid < OUT[2]) wst(ws + GB[2] + tid, gb2);
+        if (tid < OUT[3]) wst(ws + GB[3] + tid, gb3);
+        if (tid < OUT[4]) wst(ws + GB[4] + tid, gb4);
         if (wave == 0) {
             lsum = wave_sum(lsum);
             ssum = wave_sum(ssum);
