@@ -52,9 +52,9 @@ WORKLOADS = {
 FLOP_TEACHER = 2 * (11 * 64 + 64 * 64 + 64 * 2)
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 # f32_split: the f32 products emulated on bf16 MFMAs (the K = 64 products -- teacher + student
-# layer 2, student dH1 -- and the env-K dW2; beside the bf16 student the teacher's layer 1 too)
-# take six bf16 partial products each, so their f32-equivalent peak is the bf16 peak / 6; the
-# rest stays on the f32 MFMA (layer 1 of the f32-student pair, dW1) or VALU (the 64x2 layer)
+# layer 2, student dH1 -- the env-K dW2 and both nets' layer 1; beside the bf16 student the
+# teacher's layers 1 and 2) take six bf16 partial products each, so their f32-equivalent peak is
+# the bf16 peak / 6; the rest stays on the f32 MFMA (dW1) or VALU (the 64x2 layer)
 FLOP_SPLIT_PER_NET_L2 = 2 * 64 * 64
 FLOP_L1 = 2 * 11 * 64
 PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
@@ -210,8 +210,8 @@ def mixed_peak(sdt, split):
         f_split = FLOP_SPLIT_PER_NET_L2 + FLOP_L1 if split else 0
         f_f32 = FLOP_TEACHER - f_split
         return FLOP_PER_ENV_STEP / (f_f32 / PEAK_F32_TFLOPS + f_split / PEAK_SPLIT_TFLOPS + f_s / PEAK_BF16_TFLOPS)
-    if split:           # teacher L2 + student L2 + student dH1 + student dW2
-        f_split = 4 * FLOP_SPLIT_PER_NET_L2
+    if split:           # teacher L2 + student L2 + student dH1 + student dW2 + both nets' layer 1
+        f_split = 4 * FLOP_SPLIT_PER_NET_L2 + 2 * FLOP_L1
         return FLOP_PER_ENV_STEP / ((FLOP_PER_ENV_STEP - f_split) / PEAK_F32_TFLOPS + f_split / PEAK_SPLIT_TFLOPS)
     return PEAK_F32_TFLOPS
 

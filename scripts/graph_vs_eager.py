@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Step time of the fused rollout+distill step, eager launches vs one HIP graph of K steps,
-per env count (diagnostic: is the small-N step launch-bound?).
-usage: python scripts/graph_vs_eager.py [N ...]"""
+per workload (diagnostic: does the host launch path or the inter-kernel gap show in the step?).
+usage: python scripts/graph_vs_eager.py [workload ...]   (c2 c3 c4 c5)"""
 import json
 import os
 import sys
@@ -11,6 +11,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from reacherdistilation_amd.distill import DistillConfig, DistillTrainer  # noqa: E402
+
+CFG = {"c2": dict(n_envs=4096), "c3": dict(n_envs=65536, loss="kl"), "c4": dict(n_envs=262144),
+       "c5": dict(n_envs=131072, act_with="student", student_dtype="bf16")}
 
 
 def timed(fn, reps):
@@ -23,17 +26,19 @@ def timed(fn, reps):
 
 
 def main():
-    ns = [int(x) for x in sys.argv[1:]] or [4096, 65536, 262144]
-    K = 50
-    for n in ns:
-        tr = DistillTrainer(DistillConfig(n_envs=n, seed=0), device="cuda:0")
-        for _ in range(20):
+    K = 200
+    for wl in sys.argv[1:] or ["c2", "c5", "c4"]:
+        tr = DistillTrainer(DistillConfig(seed=0, **CFG[wl]), device="cuda:0")
+        for _ in range(300):
             tr.step()
-        eager = timed(lambda: [tr.step() for _ in range(K)], 4) / K
         g = tr.capture(K)
         g.replay()
-        graph = timed(g.replay, 4) / K
-        print(json.dumps({"n": n, "eager_us": eager * 1e6, "graph_us": graph * 1e6}), flush=True)
+        res = {"workload": wl}
+        for rep in range(3):   # alternate, after the clock has settled
+            res[f"eager_us_{rep}"] = timed(lambda: [tr.step() for _ in range(K)], 5) / K * 1e6
+            res[f"graph_us_{rep}"] = timed(g.replay, 5) / K * 1e6
+        print(json.dumps(res), flush=True)
+        del g
         tr.close()
 
 
