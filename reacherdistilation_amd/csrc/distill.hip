@@ -31,7 +31,6 @@
 #include <string.h>
 
 #include <new>
-#include <type_traits>
 
 #include "../../include/reacher_distill.h"
 #include "rd_comm_impl.h"
@@ -203,6 +202,29 @@ constexpr bool kDw2Split = RDD_DW2_SPLIT != 0;
 #define RDD_L1_SPLIT 1      // (layer1_split; 0: f32 MFMAs, SrcC-fenced in the consumer-side-step kernels)
 #endif
 constexpr bool kL1Split = RDD_L1_SPLIT != 0;
+// The f32-split consumer's backward as one scheduling region: the dH1 operand split is issued
+// ahead of the dW2 MFMAs and an interleave pattern (sched_group_barrier: RD_CS_HEAD VALU, then
+// RD_CS_N x (one MFMA, RD_CS_PER VALU)) puts the splits' VALU in the bf16 MFMAs' issue gaps
+// instead of in runs between them: c4 82.5 -> 80.7 us per step, c3 -1.5 %, c2 -1.5 %
+// (profiles/r03v_cons_sched.txt).  Diagnostic builds: 0 = the previous schedule (the split per
+// K step behind a sched_barrier), 1 = the reordering without the pattern (no gain).
+#ifndef RD_CONS_SCHED
+#define RD_CONS_SCHED 2
+#endif
+constexpr int kConsSched = RD_CONS_SCHED;
+#ifndef RD_CS_HEAD      // kConsSched == 2's pattern: VALU ahead of the first MFMA, then RD_CS_N x (one MFMA,
+#define RD_CS_HEAD 40   // RD_CS_PER VALU)
+#endif
+#ifndef RD_CS_PER
+#define RD_CS_PER 3
+#endif
+#ifndef RD_CS_N
+#define RD_CS_N 80
+#endif
+#ifndef RD_PROD_SCHED   // diagnostic builds: the split pair forward's layer 2 as one scheduling region with
+#define RD_PROD_SCHED 0 // an interleave pattern (1): measured slower, c4 +1.4 us (profiles/r03v_cons_sched.txt)
+#endif
+constexpr int kProdSched = RD_PROD_SCHED;
 #ifdef RD_MFMA_SRCC_FENCE
 constexpr bool kFenceAll = true;
 #else
@@ -322,11 +344,12 @@ __device__ __forceinline__ void load_state(const float* s, int64_t n, uint32_t i
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
-// Global stores, plain or non-temporal (NT).  The rollout writes its partial row with NT
-// stores from WS_NT_MIN_GRID workgroups up (profiles/r03k_nt_stores.txt: c5
-// step -0.55 us, c3 -0.25, c4 -0.2; at c2's 64 workgroups +0.2 us, so plain there).  Diagnostic
-// builds make the reduce+Adam kernel's stores (-DRD_NT_RED) or the rollout's state stores
-// (-DRD_NT_STATE) NT as well: neither gained, so the product keeps them plain.
+// Global stores, plain or non-temporal (NT).  Diagnostic builds: -DRD_WS_NT makes the rollout's
+// partial row NT (-0.5 us per c5 step, +0.2 at c2; DESIGN.md §3, profiles/r03k_nt_stores.txt),
+// -DRD_NT_RED the reduce+Adam kernel's stores, -DRD_NT_STATE the rollout's state stores (no gain).
+// The product writes the partial row with plain stores: the inline-asm NT form that kept the hint
+// through a runtime choice made the first rollout of a process differ from the later ones in one
+// lanes-48-63 gradient entry once the consumer's schedule changed (profiles/r03x_nt_asm_rejected.txt).
 #ifdef RD_NT_RED
 constexpr bool kNtRed = true;
 #else
@@ -337,19 +360,15 @@ constexpr bool kNtState = true;
 #else
 constexpr bool kNtState = false;
 #endif
-#ifndef RD_WS_NT_MIN_GRID
-#define RD_WS_NT_MIN_GRID 128
+#ifdef RD_WS_NT
+constexpr bool kWsNt = true;
+#else
+constexpr bool kWsNt = false;
 #endif
-constexpr unsigned WS_NT_MIN_GRID = RD_WS_NT_MIN_GRID;   // 0: always NT (compile-time), 1u<<30: never
 template <bool NT, class T>
 __device__ __forceinline__ void gst(T* p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
-}
-// a non-temporal 16-B vector store the compiler cannot merge with a plain one (tail merging of
-// the two variants of a store burst drops the nt hint of one of them)
-__device__ __forceinline__ void st4_nt(float* p, f32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
 }
 
 // global net = params[P] | mu[11] | sd[11]  ->  LDS image (+ W2^T if `transposed`); the
@@ -818,9 +837,47 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
         at[fb] = ld4(LT + NX_B2 + 16 * fb + 4 * g);
         as[fb] = ld4(LS + NX_B2 + 16 * fb + 4 * g);
     }
+    if constexpr (kProdSched == 2) {   // three regions: split s0 | s0 MFMAs + split s1 | s1 MFMAs + tanh
+        bf16x8 tp[2][3], sp[2][3];
+        __builtin_amdgcn_sched_barrier(0);
+        split8(T1[0], T1[1], tp[0]);
+        split8(H1[0], H1[1], sp[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        split8(T1[2], T1[3], tp[1]);
+        split8(H1[2], H1[3], sp[1]);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            const int o = (((0 * 4 + g) * 4 + fb) * 16 + j) * 8;
+            bf16x8 wt[3], ws[3];
+            ld_pieces(LT, NX_W2F, o, wt);
+            ld_pieces(LS, NX_W2F, o, ws);
+            at[fb] = mfma_split(wt, tp[0], at[fb]);
+            as[fb] = mfma_split(ws, sp[0], as[fb]);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 2);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            if (fb < 3) __builtin_amdgcn_sched_group_barrier(0x100, 6, 2);
+#pragma unroll
+            for (int m = 0; m < 12; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 2);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            const int o = (((1 * 4 + g) * 4 + fb) * 16 + j) * 8;
+            bf16x8 wt[3], ws[3];
+            ld_pieces(LT, NX_W2F, o, wt);
+            ld_pieces(LS, NX_W2F, o, ws);
+            at[fb] = mfma_split(wt, tp[1], at[fb]);
+            as[fb] = mfma_split(ws, sp[1], as[fb]);
+        }
+    } else
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
+        if constexpr (kProdSched == 0) __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
         bf16x8 tp[3], sp[3];
         split8(T1[2 * s], T1[2 * s + 1], tp);
         split8(H1[2 * s], H1[2 * s + 1], sp);
@@ -832,6 +889,18 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
             ld_pieces(LS, NX_W2F, o, ws);
             at[fb] = mfma_split(wt, tp, at[fb]);
             as[fb] = mfma_split(ws, sp, as[fb]);
+        }
+    }
+    if constexpr (kProdSched == 1) {   // the first K step's splits, then per net block: its pieces, each MFMA with 2 VALU
+        __builtin_amdgcn_sched_group_barrier(0x002, 88, 1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 1);
+#pragma unroll
+            for (int m = 0; m < 6; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 1);
+            }
         }
     }
     float pt0 = 0.0f, pt1 = 0.0f, ps0 = 0.0f, ps1 = 0.0f;
@@ -1539,9 +1608,14 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 publish(flags + 1, ++tiles);
                 STAMP(13);
                 // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
+                bf16x8 dpre[2][3];   // kConsSched: the dH1 operand pieces, made before the dW2 MFMAs
                 if constexpr (S2) {
 #pragma unroll
                     for (int b = 0; b < 4; ++b) gb2[b] += (y[b][0] + y[b][1]) + (y[b][2] + y[b][3]);
+                    if constexpr (kConsSched > 0) {
+                        split8(dZ[0], dZ[1], dpre[0]);
+                        split8(dZ[2], dZ[3], dpre[1]);
+                    }
                     dw2_split(x, y, gW2);
                 } else {
 #pragma unroll
@@ -1557,7 +1631,25 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 // dH1 = W2 . dZ2 (A = W2^T image)
 #pragma unroll
                 for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if constexpr (SPL) {   // two K = 32 steps on split pieces (dZ2 in accumulator layout = B)
+                if constexpr (SPL && S2 && kConsSched > 0) {
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+                        for (int mb = 0; mb < 4; ++mb) {
+                            bf16x8 w[3];
+                            ld_pieces(LS, NX_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8, w);
+                            acc[mb] = mfma_split(w, dpre[s], acc[mb]);
+                        }
+                    }
+                    if constexpr (kConsSched == 2) {   // splits first, then each MFMA with up to three VALU
+                        __builtin_amdgcn_sched_group_barrier(0x002, RD_CS_HEAD, 0);
+#pragma unroll
+                        for (int i = 0; i < RD_CS_N; ++i) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x002, RD_CS_PER, 0);
+                        }
+                    }
+                } else if constexpr (SPL) {   // two K = 32 steps on split pieces (dZ2 in accumulator layout = B)
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
@@ -1688,22 +1780,15 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     // two call sites pair up); this second one publishes the regions.
     __syncthreads();
     static_assert(RED_COLS % 4 == 0, "a 16-B store stays inside one workspace chunk");
-    // the row's stores as one straight burst per variant (a branch per store measured no gain)
-    auto store_row = [&](auto nt) {
 #pragma unroll
-        for (int u = 0; u < (P_PAD / 4 + BLOCK - 1) / BLOCK; ++u) {
-            const int p4 = threadIdx.x + u * BLOCK;
-            if (p4 < P_PAD / 4) {
-                const int q = ridx(4 * p4);   // 4 | 64: the four entries stay contiguous
-                float* w = a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x);
-                const f32x4 v = (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q));
-                if constexpr (decltype(nt)::value) st4_nt(w, v);
-                else st4(w, v);
-            }
+    for (int u = 0; u < (P_PAD / 4 + BLOCK - 1) / BLOCK; ++u) {
+        const int p4 = threadIdx.x + u * BLOCK;
+        if (p4 < P_PAD / 4) {
+            const int q = ridx(4 * p4);   // 4 | 64: the four entries stay contiguous
+            gst<kWsNt>(reinterpret_cast<f32x4*>(a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x)),
+                       (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q)));
         }
-    };
-    if (WS_NT_MIN_GRID == 0 || gridDim.x >= WS_NT_MIN_GRID) store_row(std::true_type{});
-    else store_row(std::false_type{});
+    }
     STAMP(7);
     RTSTAMP(17);
 }
