@@ -221,8 +221,14 @@ constexpr int kConsSched = RD_CONS_SCHED;
 #ifndef RD_CS_N
 #define RD_CS_N 80
 #endif
-#ifndef RD_PROD_SCHED   // diagnostic builds: the split pair forward's layer 2 as one scheduling region with
-#define RD_PROD_SCHED 0 // an interleave pattern (1): measured slower, c4 +1.4 us (profiles/r03v_cons_sched.txt)
+// The split pair forward's layer 2 (producer) in three scheduling regions: the first K step's
+// splits | its MFMAs with the second step's splits in their gaps (pattern: per output block its
+// six piece loads, then 12 x (one MFMA, two VALU)) | the second step's MFMAs: c4 80.9 -> 79.7 us
+// per step (profiles/r03y_sched_nt.txt).  Diagnostic builds: 0 = one region per K step behind a
+// sched_barrier (the previous schedule), 1 = one region for both steps with a pattern (slower:
+// its hoisted piece loads, profiles/r03v_cons_sched.txt).
+#ifndef RD_PROD_SCHED
+#define RD_PROD_SCHED 2
 #endif
 constexpr int kProdSched = RD_PROD_SCHED;
 #ifdef RD_MFMA_SRCC_FENCE
@@ -344,12 +350,15 @@ __device__ __forceinline__ void load_state(const float* s, int64_t n, uint32_t i
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
-// Global stores, plain or non-temporal (NT).  Diagnostic builds: -DRD_WS_NT makes the rollout's
-// partial row NT (-0.5 us per c5 step, +0.2 at c2; DESIGN.md §3, profiles/r03k_nt_stores.txt),
-// -DRD_NT_RED the reduce+Adam kernel's stores, -DRD_NT_STATE the rollout's state stores (no gain).
-// The product writes the partial row with plain stores: the inline-asm NT form that kept the hint
-// through a runtime choice made the first rollout of a process differ from the later ones in one
-// lanes-48-63 gradient entry once the consumer's schedule changed (profiles/r03x_nt_asm_rejected.txt).
+// Global stores, plain or non-temporal (NT).  The bf16-student kernels (c5) write the rollout's
+// partial row NT (__builtin_nontemporal_store): the rows no longer wait dirty in the writer's L2
+// for the end-of-kernel writeback, c5 -0.5 us per step; the f32-student kernels keep plain stores
+// (neutral at c4, -0.25 us at c3, +0.25 at c2's 64 workgroups; DESIGN.md §3,
+// profiles/r03k_nt_stores.txt, profiles/r03y_sched_nt.txt).  An inline-asm NT store that chose per
+// launch made the first rollout of a process differ in one lanes-48-63 gradient entry beside the
+// rescheduled consumer and is gone (profiles/r03x_nt_asm_rejected.txt).  Diagnostic builds:
+// -DRD_WS_NT (every kernel's row NT), -DRD_NT_RED (the reduce+Adam kernel's stores), -DRD_NT_STATE
+// (the rollout's state stores): no gain.
 #ifdef RD_NT_RED
 constexpr bool kNtRed = true;
 #else
@@ -1785,7 +1794,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         const int p4 = threadIdx.x + u * BLOCK;
         if (p4 < P_PAD / 4) {
             const int q = ridx(4 * p4);   // 4 | 64: the four entries stay contiguous
-            gst<kWsNt>(reinterpret_cast<f32x4*>(a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x)),
+            gst<kWsNt || BS>(reinterpret_cast<f32x4*>(a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x)),
                        (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q)));
         }
     }
