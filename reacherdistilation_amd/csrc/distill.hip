@@ -230,6 +230,13 @@ constexpr int kConsSched = RD_CONS_SCHED;
 #ifndef RD_PROD_SCHED
 #define RD_PROD_SCHED 2
 #endif
+// The split teacher's layer 2 beside the bf16 student (c5) in the pair's three scheduling regions,
+// its second K step's splits in the first step's MFMA gaps: c5 37.2-37.6 -> 36.6 us per step
+// (profiles/r03za_tsched.txt).  Diagnostic builds: 0 = the compiler's own schedule.
+#ifndef RD_TSCHED
+#define RD_TSCHED 1
+#endif
+constexpr int kTSched = RD_TSCHED;
 constexpr int kProdSched = RD_PROD_SCHED;
 #ifdef RD_MFMA_SRCC_FENCE
 constexpr bool kFenceAll = true;
@@ -846,7 +853,7 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
         at[fb] = ld4(LT + NX_B2 + 16 * fb + 4 * g);
         as[fb] = ld4(LS + NX_B2 + 16 * fb + 4 * g);
     }
-    if constexpr (kProdSched == 2) {   // three regions: split s0 | s0 MFMAs + split s1 | s1 MFMAs + tanh
+    if constexpr (kProdSched >= 2) {   // three regions: split s0 | s0 MFMAs + split s1 | s1 MFMAs + tanh
         bf16x8 tp[2][3], sp[2][3];
         __builtin_amdgcn_sched_barrier(0);
         split8(T1[0], T1[1], tp[0]);
@@ -882,6 +889,18 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
             ld_pieces(LS, NX_W2F, o, ws);
             at[fb] = mfma_split(wt, tp[1], at[fb]);
             as[fb] = mfma_split(ws, sp[1], as[fb]);
+        }
+        if constexpr (kProdSched == 3) {   // (diagnostic, slower: c4 +1.3 us) the last step's MFMAs with the tanh / W3 VALU in their gaps
+            __builtin_amdgcn_sched_group_barrier(0x100, 6, 4);
+#pragma unroll
+            for (int fb = 0; fb < 4; ++fb) {
+                if (fb < 3) __builtin_amdgcn_sched_group_barrier(0x100, 6, 4);
+#pragma unroll
+                for (int m = 0; m < 12; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 4);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 4);
+                }
+            }
         }
     } else
 #pragma unroll
@@ -962,6 +981,36 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
         H1[fb] = tanh4(acc[fb]);
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NX_B2 + 16 * fb + 4 * g);
+    if constexpr (kTSched == 1) {
+        bf16x8 hp[2][3];
+        __builtin_amdgcn_sched_barrier(0);
+        split8(H1[0], H1[1], hp[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        split8(H1[2], H1[3], hp[1]);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            bf16x8 w[3];
+            ld_pieces(L, NX_W2F, (((0 * 4 + g) * 4 + fb) * 16 + j) * 8, w);
+            acc[fb] = mfma_split(w, hp[0], acc[fb]);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 3);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            if (fb < 3) __builtin_amdgcn_sched_group_barrier(0x100, 3, 3);
+#pragma unroll
+            for (int m = 0; m < 6; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 3);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 3);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+            bf16x8 w[3];
+            ld_pieces(L, NX_W2F, (((1 * 4 + g) * 4 + fb) * 16 + j) * 8, w);
+            acc[fb] = mfma_split(w, hp[1], acc[fb]);
+        }
+    } else
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         bf16x8 hp[3];
