@@ -237,6 +237,10 @@ constexpr int kConsSched = RD_CONS_SCHED;
 #define RD_TSCHED 1
 #endif
 constexpr int kTSched = RD_TSCHED;
+#ifndef RD_L1SCHED      // diagnostic builds: the pair's layer 1 + tanh with an interleave pattern (1)
+#define RD_L1SCHED 0
+#endif
+constexpr int kL1Sched = RD_L1SCHED;
 constexpr int kProdSched = RD_PROD_SCHED;
 #ifdef RD_MFMA_SRCC_FENCE
 constexpr bool kFenceAll = true;
@@ -847,6 +851,20 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
     for (int fb = 0; fb < 4; ++fb) {
         T1[fb] = tanh4<true>(at[fb]);
         H1[fb] = tanh4<true>(as[fb]);
+    }
+    if constexpr (kL1Sched == 1 && kL1Split) {   // both nets' piece loads, the teacher's input pieces, then
+        __builtin_amdgcn_sched_group_barrier(0x100, 24, 5);   // each MFMA with the next VALU (the student's
+        __builtin_amdgcn_sched_group_barrier(0x002, 30, 5);   // input pieces, then the teacher's tanh)
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 5);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 5);
+        }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 5);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 5);
+        }
     }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) {
