@@ -999,7 +999,7 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
         H1[fb] = tanh4(acc[fb]);
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NX_B2 + 16 * fb + 4 * g);
-    if constexpr (kTSched == 1) {
+    if constexpr (kTSched >= 1) {
         bf16x8 hp[2][3];
         __builtin_amdgcn_sched_barrier(0);
         split8(H1[0], H1[1], hp[0]);
@@ -1470,6 +1470,19 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     if constexpr (SPL) mlp_forward_split<CP>(LT, obt, j, g, mt0, mt1);
                     else mlp_forward<CP>(LT, obt, j, g, H1, H2, mt0, mt1);
                     mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
+                    if constexpr (SPL && kTSched == 2) {   // (diagnostic) the teacher's last K step and the
+                        __builtin_amdgcn_sched_group_barrier(0x100, 12, 6);   // student's MFMAs with VALU in
+#pragma unroll
+                        for (int i = 0; i < 24; ++i) {                        // their gaps
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 6);
+                            __builtin_amdgcn_sched_group_barrier(0x002, 2, 6);
+                        }
+#pragma unroll
+                        for (int i = 0; i < 12; ++i) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 6);
+                            __builtin_amdgcn_sched_group_barrier(0x002, 3, 6);
+                        }
+                    }
                 } else {
                     if constexpr (SPL) mlp_forward_pair_split(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
                     else mlp_forward_pair(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
