@@ -223,12 +223,15 @@ constexpr int kConsSched = RD_CONS_SCHED;
 #endif
 // The split pair forward's layer 2 (producer) in three scheduling regions: the first K step's
 // splits | its MFMAs with the second step's splits in their gaps (pattern: per output block its
-// six piece loads, then 12 x (one MFMA, two VALU)) | the second step's MFMAs: c4 80.9 -> 79.7 us
+// six piece loads, then 12 x (one MFMA, RD_PS_PER VALU)) | the second step's MFMAs: c4 80.9 -> 79.7 us
 // per step (profiles/r03y_sched_nt.txt).  Diagnostic builds: 0 = one region per K step behind a
 // sched_barrier (the previous schedule), 1 = one region for both steps with a pattern (slower:
 // its hoisted piece loads, profiles/r03v_cons_sched.txt).
 #ifndef RD_PROD_SCHED
 #define RD_PROD_SCHED 2
+#endif
+#ifndef RD_PS_PER       // VALU after each MFMA in that pattern (3: c4 -0.25 us vs 2, profiles/r03ze_ps_per.txt)
+#define RD_PS_PER 3
 #endif
 // The split teacher's layer 2 beside the bf16 student (c5) in the pair's three scheduling regions,
 // its second K step's splits in the first step's MFMA gaps: c5 37.2-37.6 -> 36.6 us per step
@@ -895,7 +898,7 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
 #pragma unroll
             for (int m = 0; m < 12; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 2);
+                __builtin_amdgcn_sched_group_barrier(0x002, RD_PS_PER, 2);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
