@@ -27,9 +27,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <stdlib.h>
-#include <string.h>
-
 #include <new>
 
 #include "../../include/reacher_distill.h"
@@ -132,10 +129,6 @@ struct ReduceArgs {
     const uint32_t* xerr;   // bound exchange's failure word (xGMI) or null: nonzero = skip Adam
 };
 
-#ifndef RDD_RED_COLS   // diagnostic builds may change the reduce blocking (A/B)
-#define RDD_RED_COLS 32
-#define RDD_RED_ROWS 16
-#endif
 // The partials workspace is column-chunked: chunk c (params 32c .. 32c+31) holds the rows of
 // every workgroup of the launch contiguously, [chunk][row][RED_COLS], one 128-B line per row,
 // so one reduce block per chunk reads one contiguous run and the reduce spreads over 159
@@ -143,8 +136,8 @@ struct ReduceArgs {
 // pulled c4's 5.2 MB of partials).  Bitwise the same sums (the row order per column depends
 // on RED_ROWS only).  16-column chunks (317 blocks) make the rollout's stores half lines and
 // cost it 5 us at c4 (profiles/r02_ws_chunked.txt).
-constexpr int RED_COLS = RDD_RED_COLS;              // params per reduce block = chunk width
-constexpr int RED_ROWS = RDD_RED_ROWS;              // partial rows summed in parallel
+constexpr int RED_COLS = 32;                        // params per reduce block = chunk width
+constexpr int RED_ROWS = 16;                        // partial rows summed in parallel
 constexpr int RED_BLOCK = RED_COLS * RED_ROWS;
 constexpr int RED_GRID = (P_PAD + RED_COLS - 1) / RED_COLS;
 constexpr int P_WS = RED_GRID * RED_COLS;           // workspace floats per partial row
@@ -194,57 +187,6 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // the MFMA still reads (found statically with scripts/isa/hazards.py, confirmed
 // by profiles/r03_srcc_probe_*.txt).  The consumer-side-env-step kernels (bf16 student) fence
 // their teacher's f32 MFMAs; -DRD_MFMA_SRCC_FENCE fences every group (diagnostic builds).
-#ifndef RDD_DW2_SPLIT   // f32_split: dW2 on split bf16 MFMAs (dw2_split; 0: f32 MFMAs, A/B builds)
-#define RDD_DW2_SPLIT 1
-#endif
-constexpr bool kDw2Split = RDD_DW2_SPLIT != 0;
-#ifndef RDD_L1_SPLIT    // f32_split teacher beside the bf16 student: layer 1 on split bf16 MFMAs
-#define RDD_L1_SPLIT 1      // (layer1_split; 0: f32 MFMAs, SrcC-fenced in the consumer-side-step kernels)
-#endif
-constexpr bool kL1Split = RDD_L1_SPLIT != 0;
-// The f32-split consumer's backward as one scheduling region: the dH1 operand split is issued
-// ahead of the dW2 MFMAs and an interleave pattern (sched_group_barrier: RD_CS_HEAD VALU, then
-// RD_CS_N x (one MFMA, RD_CS_PER VALU)) puts the splits' VALU in the bf16 MFMAs' issue gaps
-// instead of in runs between them: c4 82.5 -> 80.7 us per step, c3 -1.5 %, c2 -1.5 %
-// (profiles/r03v_cons_sched.txt).  Diagnostic builds: 0 = the previous schedule (the split per
-// K step behind a sched_barrier), 1 = the reordering without the pattern (no gain).
-#ifndef RD_CONS_SCHED
-#define RD_CONS_SCHED 2
-#endif
-constexpr int kConsSched = RD_CONS_SCHED;
-#ifndef RD_CS_HEAD      // kConsSched == 2's pattern: VALU ahead of the first MFMA, then RD_CS_N x (one MFMA,
-#define RD_CS_HEAD 40   // RD_CS_PER VALU)
-#endif
-#ifndef RD_CS_PER
-#define RD_CS_PER 3
-#endif
-#ifndef RD_CS_N
-#define RD_CS_N 80
-#endif
-// The split pair forward's layer 2 (producer) in three scheduling regions: the first K step's
-// splits | its MFMAs with the second step's splits in their gaps (pattern: per output block its
-// six piece loads, then 12 x (one MFMA, RD_PS_PER VALU)) | the second step's MFMAs: c4 80.9 -> 79.7 us
-// per step (profiles/r03y_sched_nt.txt).  Diagnostic builds: 0 = one region per K step behind a
-// sched_barrier (the previous schedule), 1 = one region for both steps with a pattern (slower:
-// its hoisted piece loads, profiles/r03v_cons_sched.txt).
-#ifndef RD_PROD_SCHED
-#define RD_PROD_SCHED 2
-#endif
-#ifndef RD_PS_PER       // VALU after each MFMA in that pattern (3: c4 -0.25 us vs 2, profiles/r03ze_ps_per.txt)
-#define RD_PS_PER 3
-#endif
-// The split teacher's layer 2 beside the bf16 student (c5) in the pair's three scheduling regions,
-// its second K step's splits in the first step's MFMA gaps: c5 37.2-37.6 -> 36.6 us per step
-// (profiles/r03za_tsched.txt).  Diagnostic builds: 0 = the compiler's own schedule.
-#ifndef RD_TSCHED
-#define RD_TSCHED 1
-#endif
-constexpr int kTSched = RD_TSCHED;
-#ifndef RD_L1SCHED      // diagnostic builds: the pair's layer 1 + tanh with an interleave pattern (1)
-#define RD_L1SCHED 0
-#endif
-constexpr int kL1Sched = RD_L1SCHED;
-constexpr int kProdSched = RD_PROD_SCHED;
 #ifdef RD_MFMA_SRCC_FENCE
 constexpr bool kFenceAll = true;
 #else
@@ -269,11 +211,7 @@ __device__ __forceinline__ void fence_end(f32x4 (&acc)[4]) {   // every MFMA of 
 // (The backward only needs tanh's output; W2^T for dH1 keeps the unscaled weights.)
 constexpr float kTanhScale = 2.8853900817779268f;
 __device__ __forceinline__ float tanh_pre(float y) {
-#ifdef RD_ABL_TANH   // ablation build: no transcendentals (timing only, wrong results)
-    return fminf(fmaxf(0.25f * y, -1.0f), 1.0f);
-#else
     return fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(y) + 1.0f), 1.0f);
-#endif
 }
 // tanh_pre on the four rows of an accumulator.  PK: the add and the fma as packed-f32 pairs
 // (v_pk_add_f32 / v_pk_fma_f32), bitwise the same results.  Measured per call site
@@ -282,7 +220,6 @@ __device__ __forceinline__ float tanh_pre(float y) {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool PK = false>
 __device__ __forceinline__ f32x4 tanh4(f32x4 y) {
-#ifndef RD_ABL_TANH
     if constexpr (!PK) {
         return f32x4{tanh_pre(y[0]), tanh_pre(y[1]), tanh_pre(y[2]), tanh_pre(y[3])};
     } else {
@@ -296,9 +233,6 @@ __device__ __forceinline__ f32x4 tanh4(f32x4 y) {
         const f32x2 t1 = __builtin_elementwise_fma(r1, (f32x2){-2.0f, -2.0f}, (f32x2){1.0f, 1.0f});
         return f32x4{t0[0], t0[1], t1[0], t1[1]};
     }
-#else
-    return f32x4{tanh_pre(y[0]), tanh_pre(y[1]), tanh_pre(y[2]), tanh_pre(y[3])};
-#endif
 }
 
 // The per-wave scratch is private to its wave: LDS instructions of one wave execute in
@@ -327,11 +261,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // state row k of env i: (state + k n)[i] -- uniform 64-bit row base, 32-bit lane offset
-#ifdef RD_NT_LDSTATE   // diagnostic build: the state read as a non-temporal stream
-__device__ __forceinline__ float ldst(const float* p) { return __builtin_nontemporal_load(p); }
-#else
 __device__ __forceinline__ float ldst(const float* p) { return *p; }
-#endif
 __device__ __forceinline__ void load_state(const float* s, int64_t n, uint32_t i, rd::State& st) {
     st.q0 = ldst(s + 0 * n + i); st.q1 = ldst(s + 1 * n + i); st.v0 = ldst(s + 2 * n + i); st.v1 = ldst(s + 3 * n + i);
     st.tx = ldst(s + 4 * n + i); st.ty = ldst(s + 5 * n + i); st.dx = ldst(s + 6 * n + i); st.dy = ldst(s + 7 * n + i);
@@ -369,30 +299,17 @@ __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4
 // for the end-of-kernel writeback, c5 -0.5 us per step; the f32-student kernels keep plain stores
 // (neutral at c4, -0.25 us at c3, +0.25 at c2's 64 workgroups; DESIGN.md §3,
 // profiles/r03k_nt_stores.txt, profiles/r03y_sched_nt.txt).  An inline-asm NT store that chose per
-// launch made the first rollout of a process differ in one lanes-48-63 gradient entry beside the
-// rescheduled consumer and is gone (profiles/r03x_nt_asm_rejected.txt).  Diagnostic builds:
-// -DRD_WS_NT (every kernel's row NT), -DRD_NT_RED (the reduce+Adam kernel's stores), -DRD_NT_STATE
-// (the rollout's state stores): no gain.
-#ifdef RD_NT_RED
-constexpr bool kNtRed = true;
-#else
-constexpr bool kNtRed = false;
-#endif
-#ifdef RD_NT_STATE
-constexpr bool kNtState = true;
-#else
-constexpr bool kNtState = false;
-#endif
-#ifdef RD_WS_NT
-constexpr bool kWsNt = true;
-#else
-constexpr bool kWsNt = false;
-#endif
+// launch made the first rollout of a process differ in one gradient entry and is gone
+// (profiles/r03x_nt_asm_rejected.txt; no wait-state pair explains it, profiles/r04_r03x_isa.txt).
+// NT state, reduce+Adam and all-kernel row stores measured no gain
+// (profiles/r04_removed_diagnostic_variants.diff).
 template <bool NT, class T>
 __device__ __forceinline__ void gst(T* p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
+template <class T>
+__device__ __forceinline__ void put(T* p, T v) { *p = v; }
 
 // global net = params[P] | mu[11] | sd[11]  ->  LDS image (+ W2^T if `transposed`); the
 // forward images of W1, b1, W2, b2 carry the tanh scale (kTanhScale)
@@ -756,10 +673,10 @@ __device__ __forceinline__ f32x4 mfma_split(const bf16x8 (&w)[3], const bf16x8 (
 // Split-mode image of a net (offsets in floats): the small vectors first, then the three
 // pieces of the scaled W2 in the bf16 student's permuted forward order
 // [q][s 2][g 4][fb 4][i 16][jj 8] = piece q of kTanhScale W2[kperm(s,g,jj)][16fb+i], then layer 1:
-// with kL1Split (the product) the A operands of layer1_split's two piece pairings
-// [v 2][g 4][fb 4][i 16][jj 8]: slot jj = 2s + c (s < 3) holds piece (v ? (0,1) : (0,2))[c] of
-// kTanhScale W1[4s + g][16fb + i] (row 11 = b1), slots 6, 7 zero; else W1 [12][16][4] f32 (as
-// N_W1, scaled).  The student adds the pieces of the unscaled W2 for dH1 in the NB_W2B order.
+// the A operands of layer1_split's two piece pairings [v 2][g 4][fb 4][i 16][jj 8]: slot
+// jj = 2s + c (s < 3) holds piece (v ? (0,1) : (0,2))[c] of kTanhScale W1[4s + g][16fb + i]
+// (row 11 = b1), slots 6, 7 zero.  The student adds the pieces of the unscaled W2 for dH1 in
+// the NB_W2B order.
 constexpr int SP_PIECE = 2 * 4 * 4 * 16 * 8;      // bf16 elements per piece
 constexpr int NX_B2 = 0;
 constexpr int NX_W3 = NX_B2 + HID;                // 64
@@ -768,12 +685,11 @@ constexpr int NX_LS = NX_B3 + ACD;
 constexpr int NX_MU = NX_LS + ACD;
 constexpr int NX_RS = NX_MU + 12;
 constexpr int NX_W2F = NX_RS + 12;                // 220
-constexpr int NX_W1S = NX_W2F + 3 * SP_PIECE / 2; // 6364 (kL1Split)
-constexpr int NX_W1 = NX_W1S;                     // (RDD_L1_SPLIT=0 builds)
-constexpr int NETX = NX_W1 + (kL1Split ? 2 * 4 * 4 * 16 * 8 / 2 : 12 * HID);   // 8412 (7132)
+constexpr int NX_W1S = NX_W2F + 3 * SP_PIECE / 2; // 6364
+constexpr int NETX = NX_W1S + 2 * 4 * 4 * 16 * 8 / 2;   // 8412
 constexpr int NX_W2B = NETX;                      // student only
-constexpr int NETX_S = NX_W2B + 3 * SP_PIECE / 2; // 14556 (13276)
-static_assert(NX_W3 % 4 == 0 && NX_B2 % 4 == 0 && NX_W2F % 4 == 0 && NX_W1 % 4 == 0 && NETX % 4 == 0 &&
+constexpr int NETX_S = NX_W2B + 3 * SP_PIECE / 2; // 14556
+static_assert(NX_W3 % 4 == 0 && NX_B2 % 4 == 0 && NX_W2F % 4 == 0 && NX_W1S % 4 == 0 && NETX % 4 == 0 &&
               NETX_S % 4 == 0, "16-B aligned split images");
 
 // the student image's W3 / filter offsets by kind: exact f32 (N_*), split (NX_*), bf16 (NB_*)
@@ -823,58 +739,31 @@ __device__ __forceinline__ void layer1_split(const float* L, const float* ob, in
 }
 
 // Teacher and student forwards of one tile with split images (both nets, interleaved):
-// layer 1 on split bf16 MFMAs (layer1_split; RDD_L1_SPLIT=0 builds: exact f32, K = 12, as
-// mlp_forward_pair), layer 2 on split bf16 MFMAs.
+// layer 1 (layer1_split) and layer 2 on split bf16 MFMAs.  Layer 2 runs in three scheduling
+// regions: the first K step's splits | its MFMAs with the second step's splits in their gaps
+// (per output block its six piece loads, then 12 x (one MFMA, three VALU)) | the second
+// step's MFMAs (c4 80.9 -> 79.7 us per step, profiles/r03y_sched_nt.txt; 3 VALU per MFMA
+// -0.25 us vs 2, profiles/r03ze_ps_per.txt).
 __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const float* LS, const float* ob, int j, int g,
                                                        f32x4 (&H1)[4], f32x4 (&H2)[4], float& mt0, float& mt1,
                                                        float& ms0, float& ms1) {
     f32x4 at[4], as[4];
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) at[fb] = as[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (kL1Split) {
-        layer1_split(LT, ob, j, g, at);
-        layer1_split(LS, ob, j, g, as);
-    } else
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        const int k = 4 * s + g;
-        const float x = ob[j * SOS + k];
-        const float zt = fminf(fmaxf((x - LT[NX_MU + k]) * LT[NX_RS + k], -5.0f), 5.0f);
-        const float zs = fminf(fmaxf((x - LS[NX_MU + k]) * LS[NX_RS + k], -5.0f), 5.0f);
-        const f32x4 wt = ld4(LT + NX_W1 + k * HID + 4 * j);
-        const f32x4 ws = ld4(LS + NX_W1 + k * HID + 4 * j);
-#pragma unroll
-        for (int fb = 0; fb < 4; ++fb) {
-            at[fb] = mfma(wt[fb], zt, at[fb]);
-            as[fb] = mfma(ws[fb], zs, as[fb]);
-        }
-    }
+    layer1_split(LT, ob, j, g, at);
+    layer1_split(LS, ob, j, g, as);
     f32x4 T1[4];
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) {
         T1[fb] = tanh4<true>(at[fb]);
         H1[fb] = tanh4<true>(as[fb]);
     }
-    if constexpr (kL1Sched == 1 && kL1Split) {   // both nets' piece loads, the teacher's input pieces, then
-        __builtin_amdgcn_sched_group_barrier(0x100, 24, 5);   // each MFMA with the next VALU (the student's
-        __builtin_amdgcn_sched_group_barrier(0x002, 30, 5);   // input pieces, then the teacher's tanh)
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 5);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 5);
-        }
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 5);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 5);
-        }
-    }
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) {
         at[fb] = ld4(LT + NX_B2 + 16 * fb + 4 * g);
         as[fb] = ld4(LS + NX_B2 + 16 * fb + 4 * g);
     }
-    if constexpr (kProdSched >= 2) {   // three regions: split s0 | s0 MFMAs + split s1 | s1 MFMAs + tanh
+    {   // three regions: split s0 | s0 MFMAs + split s1 | s1 MFMAs
         bf16x8 tp[2][3], sp[2][3];
         __builtin_amdgcn_sched_barrier(0);
         split8(T1[0], T1[1], tp[0]);
@@ -898,7 +787,7 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
 #pragma unroll
             for (int m = 0; m < 12; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-                __builtin_amdgcn_sched_group_barrier(0x002, RD_PS_PER, 2);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 2);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -910,46 +799,6 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
             ld_pieces(LS, NX_W2F, o, ws);
             at[fb] = mfma_split(wt, tp[1], at[fb]);
             as[fb] = mfma_split(ws, sp[1], as[fb]);
-        }
-        if constexpr (kProdSched == 3) {   // (diagnostic, slower: c4 +1.3 us) the last step's MFMAs with the tanh / W3 VALU in their gaps
-            __builtin_amdgcn_sched_group_barrier(0x100, 6, 4);
-#pragma unroll
-            for (int fb = 0; fb < 4; ++fb) {
-                if (fb < 3) __builtin_amdgcn_sched_group_barrier(0x100, 6, 4);
-#pragma unroll
-                for (int m = 0; m < 12; ++m) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 4);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 4);
-                }
-            }
-        }
-    } else
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        if constexpr (kProdSched == 0) __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
-        bf16x8 tp[3], sp[3];
-        split8(T1[2 * s], T1[2 * s + 1], tp);
-        split8(H1[2 * s], H1[2 * s + 1], sp);
-#pragma unroll
-        for (int fb = 0; fb < 4; ++fb) {
-            const int o = (((s * 4 + g) * 4 + fb) * 16 + j) * 8;
-            bf16x8 wt[3], ws[3];
-            ld_pieces(LT, NX_W2F, o, wt);
-            ld_pieces(LS, NX_W2F, o, ws);
-            at[fb] = mfma_split(wt, tp, at[fb]);
-            as[fb] = mfma_split(ws, sp, as[fb]);
-        }
-    }
-    if constexpr (kProdSched == 1) {   // the first K step's splits, then per net block: its pieces, each MFMA with 2 VALU
-        __builtin_amdgcn_sched_group_barrier(0x002, 88, 1);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 3, 1);
-#pragma unroll
-            for (int m = 0; m < 6; ++m) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 1);
-            }
         }
     }
     float pt0 = 0.0f, pt1 = 0.0f, ps0 = 0.0f, ps1 = 0.0f;
@@ -977,32 +826,19 @@ __device__ __forceinline__ void mlp_forward_pair_split(const float* LT, const fl
 
 // One net's forward with a split image (the teacher beside the bf16 student; HO: also
 // return the hidden activations).
-template <bool HO, bool FENCE = false>
+template <bool HO>
 __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float* ob, int j, int g, f32x4 (&H1)[4],
                                                     f32x4 (&H2)[4], float& m0, float& m1) {
     f32x4 acc[4];
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (kL1Split) {
-        layer1_split(L, ob, j, g, acc);
-    } else {
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        const int k = 4 * s + g;
-        const float z = fminf(fmaxf((ob[j * SOS + k] - L[NX_MU + k]) * L[NX_RS + k], -5.0f), 5.0f);
-        const f32x4 w = ld4(L + NX_W1 + k * HID + 4 * j);
-        fence_begin<FENCE>(acc);
-#pragma unroll
-        for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma(w[fb], z, acc[fb]);
-        fence_end<FENCE>(acc);
-    }
-    }
+    layer1_split(L, ob, j, g, acc);
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
         H1[fb] = tanh4(acc[fb]);
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NX_B2 + 16 * fb + 4 * g);
-    if constexpr (kTSched >= 1) {
+    {   // three regions, as the pair's layer 2 (c5 37.2-37.6 -> 36.6 us per step, profiles/r03za_tsched.txt)
         bf16x8 hp[2][3];
         __builtin_amdgcn_sched_barrier(0);
         split8(H1[0], H1[1], hp[0]);
@@ -1031,17 +867,6 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
             ld_pieces(L, NX_W2F, (((1 * 4 + g) * 4 + fb) * 16 + j) * 8, w);
             acc[fb] = mfma_split(w, hp[1], acc[fb]);
         }
-    } else
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        bf16x8 hp[3];
-        split8(H1[2 * s], H1[2 * s + 1], hp);
-#pragma unroll
-        for (int fb = 0; fb < 4; ++fb) {
-            bf16x8 w[3];
-            ld_pieces(L, NX_W2F, (((s * 4 + g) * 4 + fb) * 16 + j) * 8, w);
-            acc[fb] = mfma_split(w, hp, acc[fb]);
-        }
     }
     float p0 = 0.0f, p1 = 0.0f;
 #pragma unroll
@@ -1059,10 +884,9 @@ __device__ __forceinline__ void mlp_forward_split_t(const float* L, const float*
     m0 = xsum32(xsum16(p0)) + L[NX_B3];
     m1 = xsum32(xsum16(p1)) + L[NX_B3 + 1];
 }
-template <bool FENCE = false>
 __device__ __forceinline__ void mlp_forward_split(const float* L, const float* ob, int j, int g, float& m0, float& m1) {
     f32x4 h1[4], h2[4];
-    mlp_forward_split_t<false, FENCE>(L, ob, j, g, h1, h2, m0, m1);
+    mlp_forward_split_t<false>(L, ob, j, g, h1, h2, m0, m1);
 }
 
 
@@ -1081,88 +905,85 @@ __device__ __forceinline__ void pack_param(float* img, int p, float v, bool stud
         unsigned short q[3];
         if (p < P_W2) {   // W1 rows 0..10, b1 as row 11
             const int k = p < P_B1 ? p >> 6 : OBD, f = p < P_B1 ? p & 63 : p - P_B1;
-            if constexpr (kL1Split) {   // layer1_split's A operands: slots 2s, 2s + 1 of lane group k & 3
-                split1(kTanhScale * v, q);
-                const int o = 2 * NX_W1S + (((k & 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + 2 * (k >> 2);
-                constexpr int V1 = 4 * 4 * 16 * 8;   // the (0,1) pairing follows the (0,2) one
-                gst<kNtRed>(h + (o), q[0]); gst<kNtRed>(h + (o + 1), q[2]);
-                gst<kNtRed>(h + (o + V1), q[0]); gst<kNtRed>(h + (o + V1 + 1), q[1]);
-            } else {
-                gst<kNtRed>(img + (NX_W1 + k * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
-            }
+            // layer1_split's A operands: slots 2s, 2s + 1 of lane group k & 3
+            split1(kTanhScale * v, q);
+            const int o = 2 * NX_W1S + (((k & 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + 2 * (k >> 2);
+            constexpr int V1 = 4 * 4 * 16 * 8;   // the (0,1) pairing follows the (0,2) one
+            put(h + (o), q[0]); put(h + (o + 1), q[2]);
+            put(h + (o + V1), q[0]); put(h + (o + V1 + 1), q[1]);
         } else if (p < P_B2) {
             const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
             {   // forward: k is the permuted K index (as NB_W2F), pieces of the scaled weight
                 const int s = k >> 5, r = k & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
                 const int o = 2 * NX_W2F + (((s * 4 + gg) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + jj;
                 split1(kTanhScale * v, q);
-                gst<kNtRed>(h + (o), q[0]); gst<kNtRed>(h + (o + SP_PIECE), q[1]); gst<kNtRed>(h + (o + 2 * SP_PIECE), q[2]);
+                put(h + (o), q[0]); put(h + (o + SP_PIECE), q[1]); put(h + (o + 2 * SP_PIECE), q[2]);
             }
             if (student) {   // dH1: f is the permuted K index (as NB_W2B), unscaled
                 const int s = f >> 5, r = f & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
                 const int o = 2 * NX_W2B + (((s * 4 + gg) * 4 + (k >> 4)) * 16 + (k & 15)) * 8 + jj;
                 split1(v, q);
-                gst<kNtRed>(h + (o), q[0]); gst<kNtRed>(h + (o + SP_PIECE), q[1]); gst<kNtRed>(h + (o + 2 * SP_PIECE), q[2]);
+                put(h + (o), q[0]); put(h + (o + SP_PIECE), q[1]); put(h + (o + 2 * SP_PIECE), q[2]);
             }
         } else if (p < P_W3) {
-            gst<kNtRed>(img + (NX_B2 + (p - P_B2)), kTanhScale * v);
+            put(img + (NX_B2 + (p - P_B2)), kTanhScale * v);
         } else if (p < P_B3) {
-            gst<kNtRed>(img + (NX_W3 + (p - P_W3)), v);
+            put(img + (NX_W3 + (p - P_W3)), v);
         } else if (p < P_LS) {
-            gst<kNtRed>(img + (NX_B3 + (p - P_B3)), v);
+            put(img + (NX_B3 + (p - P_B3)), v);
         } else if (p < P_TOT) {
-            gst<kNtRed>(img + (NX_LS + (p - P_LS)), v);
+            put(img + (NX_LS + (p - P_LS)), v);
         }
         return;
     }
     if (kind == IMG_F32) {
         if (p < P_B1) {
             const int k = p >> 6, f = p & 63;
-            gst<kNtRed>(img + (N_W1 + k * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
+            put(img + (N_W1 + k * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
         } else if (p < P_W2) {
             const int f = p - P_B1;
-            gst<kNtRed>(img + (N_W1 + OBD * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
+            put(img + (N_W1 + OBD * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
         } else if (p < P_B2) {
             const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
-            gst<kNtRed>(img + (N_W2 + k * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
-            if (student) gst<kNtRed>(img + (N_W2T + f * HID + (k & 15) * 4 + (k >> 4)), v);
+            put(img + (N_W2 + k * HID + (f & 15) * 4 + (f >> 4)), kTanhScale * v);
+            if (student) put(img + (N_W2T + f * HID + (k & 15) * 4 + (k >> 4)), v);
         } else if (p < P_W3) {
-            gst<kNtRed>(img + (N_B2 + (p - P_B2)), kTanhScale * v);
+            put(img + (N_B2 + (p - P_B2)), kTanhScale * v);
         } else if (p < P_B3) {
-            gst<kNtRed>(img + (N_W3 + (p - P_W3)), v);
+            put(img + (N_W3 + (p - P_W3)), v);
         } else if (p < P_LS) {
-            gst<kNtRed>(img + (N_B3 + (p - P_B3)), v);
+            put(img + (N_B3 + (p - P_B3)), v);
         } else if (p < P_TOT) {
-            gst<kNtRed>(img + (N_LS + (p - P_LS)), v);
+            put(img + (N_LS + (p - P_LS)), v);
         }
         return;
     }
     unsigned short* h = reinterpret_cast<unsigned short*>(img);
     if (p < P_B1) {
         const int k = p >> 6, f = p & 63;   // k = 8gg + jj
-        gst<kNtRed>(h + (2 * NB_W1 + (((k >> 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + (k & 7)), bf16_bits(v));
+        put(h + (2 * NB_W1 + (((k >> 3) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + (k & 7)), bf16_bits(v));
     } else if (p < P_W2) {
-        gst<kNtRed>(img + (NB_B1 + (p - P_B1)), v);
+        put(img + (NB_B1 + (p - P_B1)), v);
     } else if (p < P_B2) {
         const int k = (p - P_W2) >> 6, f = (p - P_W2) & 63;
         // forward image: k (H1 feature) is the permuted K index, f the output row
         {
             const int s = k >> 5, r = k & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
-            gst<kNtRed>(h + (2 * NB_W2F + (((s * 4 + gg) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + jj), bf16_bits(v));
+            put(h + (2 * NB_W2F + (((s * 4 + gg) * 4 + (f >> 4)) * 16 + (f & 15)) * 8 + jj), bf16_bits(v));
         }
         // dH1 image: f (dZ2 feature) is the permuted K index, k the output row
         {
             const int s = f >> 5, r = f & 31, gg = (r & 15) >> 2, jj = (r & 3) + 4 * (r >> 4);
-            gst<kNtRed>(h + (2 * NB_W2B + (((s * 4 + gg) * 4 + (k >> 4)) * 16 + (k & 15)) * 8 + jj), bf16_bits(v));
+            put(h + (2 * NB_W2B + (((s * 4 + gg) * 4 + (k >> 4)) * 16 + (k & 15)) * 8 + jj), bf16_bits(v));
         }
     } else if (p < P_W3) {
-        gst<kNtRed>(img + (NB_B2 + (p - P_B2)), v);
+        put(img + (NB_B2 + (p - P_B2)), v);
     } else if (p < P_B3) {
-        gst<kNtRed>(img + (NB_W3 + (p - P_W3)), bf16_round(v));
+        put(img + (NB_W3 + (p - P_W3)), bf16_round(v));
     } else if (p < P_LS) {
-        gst<kNtRed>(img + (NB_B3 + (p - P_B3)), v);
+        put(img + (NB_B3 + (p - P_B3)), v);
     } else if (p < P_TOT) {
-        gst<kNtRed>(img + (NB_LS + (p - P_LS)), v);
+        put(img + (NB_LS + (p - P_LS)), v);
     }
 }
 
@@ -1273,12 +1094,7 @@ __device__ __forceinline__ void publish(uint32_t* f, uint32_t v) {
 __device__ __forceinline__ float env_step_group(const RolloutArgs& a, uint32_t C, int64_t i, bool valid, float act0,
                                                 float act1, rd::State& st, float& met_n) {
     const uint32_t iu = (uint32_t)i;
-#ifdef RD_ABL_PHYSICS   // ablation build: no dynamics (timing only)
-    const float rew = act0 + act1;
-    st.q0 += 0.01f * act0;
-#else
     const float rew = rd::env_step<false>(st, act0, act1);
-#endif
     // episode clock of this env (RDD_STAGGER_GROUP envs share an offset)
     const int64_t gid = a.env_base + i;
     const uint32_t u = C + (a.stagger ? (uint32_t)((gid / RDD_STAGGER_GROUP) % rd::kEpisodeSteps) : 0u);
@@ -1291,10 +1107,10 @@ __device__ __forceinline__ float env_step_group(const RolloutArgs& a, uint32_t C
     if (!valid) return 0.0f;
     float* s = a.state;
     const int64_t n = a.n;
-    gst<kNtState>(s + 0 * n + iu, st.q0); gst<kNtState>(s + 1 * n + iu, st.q1);
-    gst<kNtState>(s + 2 * n + iu, st.v0); gst<kNtState>(s + 3 * n + iu, st.v1);
-    if (done_step) { gst<kNtState>(s + 4 * n + iu, st.tx); gst<kNtState>(s + 5 * n + iu, st.ty); }
-    gst<kNtState>(s + 6 * n + iu, st.dx); gst<kNtState>(s + 7 * n + iu, st.dy);
+    put(s + 0 * n + iu, st.q0); put(s + 1 * n + iu, st.q1);
+    put(s + 2 * n + iu, st.v0); put(s + 3 * n + iu, st.v1);
+    if (done_step) { put(s + 4 * n + iu, st.tx); put(s + 5 * n + iu, st.ty); }
+    put(s + 6 * n + iu, st.dx); put(s + 7 * n + iu, st.dy);
     met_n += 1.0f;
     return rew;
 }
@@ -1329,10 +1145,10 @@ __device__ __forceinline__ void col_finish(const ReduceArgs& a, int p, const flo
         g = (q[0] + q[1]) + (q[2] + q[3]);
         if (p < P_TOT) {
             if (a.accum) g += a.grad[p];
-            gst<kNtRed>(a.grad + p, g);
+            put(a.grad + p, g);
         } else {
             float* h = a.hist + (int64_t)(S % (uint32_t)a.hist_len) * N_MET + (p - P_TOT);
-            gst<kNtRed>(h, a.accum ? *h + g : g);
+            put(h, a.accum ? *h + g : g);
         }
     } else {
         g = p < P_TOT ? a.grad[p] : 0.f;
@@ -1342,10 +1158,10 @@ __device__ __forceinline__ void col_finish(const ReduceArgs& a, int p, const flo
         float m = m_p, v = v_p;
         m += (g - m) * (1.0f - a.b1);
         v += (g * g - v) * (1.0f - a.b2);
-        gst<kNtRed>(a.m + p, m);
-        gst<kNtRed>(a.v + p, v);
+        put(a.m + p, m);
+        put(a.v + p, v);
         const float w = w_p - (m * alpha) / (sqrtf(v) + a.eps);
-        gst<kNtRed>(a.params + p, w);
+        put(a.params + p, w);
         pack_param(a.simg, p, w, true, a.img_kind);
     }
 }
@@ -1469,23 +1285,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 STAMP(10);
                 if constexpr (BS) {
                     // CP: in this kernel's schedule the compiler issues loads into the SrcC
-                    // registers of the teacher's f32 layer-1 MFMAs: fenced (see mfma())
-                    if constexpr (SPL) mlp_forward_split<CP>(LT, obt, j, g, mt0, mt1);
+                    // registers of the exact teacher's f32 MFMAs: fenced (see mfma())
+                    if constexpr (SPL) mlp_forward_split(LT, obt, j, g, mt0, mt1);
                     else mlp_forward<CP>(LT, obt, j, g, H1, H2, mt0, mt1);
                     mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
-                    if constexpr (SPL && kTSched == 2) {   // (diagnostic) the teacher's last K step and the
-                        __builtin_amdgcn_sched_group_barrier(0x100, 12, 6);   // student's MFMAs with VALU in
-#pragma unroll
-                        for (int i = 0; i < 24; ++i) {                        // their gaps
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 6);
-                            __builtin_amdgcn_sched_group_barrier(0x002, 2, 6);
-                        }
-#pragma unroll
-                        for (int i = 0; i < 12; ++i) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 6);
-                            __builtin_amdgcn_sched_group_barrier(0x002, 3, 6);
-                        }
-                    }
                 } else {
                     if constexpr (SPL) mlp_forward_pair_split(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
                     else mlp_forward_pair(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
@@ -1672,9 +1475,9 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                         acc[mb] = mfma_k32(ldbf8(LS + NB_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8), db, acc[mb]);
                 }
             } else {
-                // S2: dW2 on split bf16 MFMAs, x[b][e] / y[b][e] over envs 4g+e (dw2_split);
-                // else f32 MFMAs, x[s][b] / y[s][b] over env 4s+g (k-step s)
-                constexpr bool S2 = SPL && kDw2Split;
+                // split: dW2 on split bf16 MFMAs, x[b][e] / y[b][e] over envs 4g+e (dw2_split);
+                // exact: f32 MFMAs, x[s][b] / y[s][b] over env 4s+g (k-step s)
+                constexpr bool S2 = SPL;
                 float x[4][4], y[4][4];
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
@@ -1700,14 +1503,12 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 publish(flags + 1, ++tiles);
                 STAMP(13);
                 // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
-                bf16x8 dpre[2][3];   // kConsSched: the dH1 operand pieces, made before the dW2 MFMAs
+                bf16x8 dpre[2][3];   // split: the dH1 operand pieces, made before the dW2 MFMAs
                 if constexpr (S2) {
 #pragma unroll
                     for (int b = 0; b < 4; ++b) gb2[b] += (y[b][0] + y[b][1]) + (y[b][2] + y[b][3]);
-                    if constexpr (kConsSched > 0) {
-                        split8(dZ[0], dZ[1], dpre[0]);
-                        split8(dZ[2], dZ[3], dpre[1]);
-                    }
+                    split8(dZ[0], dZ[1], dpre[0]);
+                    split8(dZ[2], dZ[3], dpre[1]);
                     dw2_split(x, y, gW2);
                 } else {
 #pragma unroll
@@ -1723,7 +1524,10 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 // dH1 = W2 . dZ2 (A = W2^T image)
 #pragma unroll
                 for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if constexpr (SPL && S2 && kConsSched > 0) {
+                if constexpr (S2) {
+                    // one scheduling region with the dW2 MFMAs: the splits first, then 80 x (one
+                    // MFMA, three VALU), so the dH1 splits issue in the bf16 MFMAs' gaps (c4 82.5 ->
+                    // 80.7 us per step, c3/c2 -1.5 %; profiles/r03v_cons_sched.txt)
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
 #pragma unroll
@@ -1733,26 +1537,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                             acc[mb] = mfma_split(w, dpre[s], acc[mb]);
                         }
                     }
-                    if constexpr (kConsSched == 2) {   // splits first, then each MFMA with up to three VALU
-                        __builtin_amdgcn_sched_group_barrier(0x002, RD_CS_HEAD, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
 #pragma unroll
-                        for (int i = 0; i < RD_CS_N; ++i) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                            __builtin_amdgcn_sched_group_barrier(0x002, RD_CS_PER, 0);
-                        }
-                    }
-                } else if constexpr (SPL) {   // two K = 32 steps on split pieces (dZ2 in accumulator layout = B)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted piece loads (VGPRs)
-                        bf16x8 dp[3];
-                        split8(dZ[2 * s], dZ[2 * s + 1], dp);
-#pragma unroll
-                        for (int mb = 0; mb < 4; ++mb) {
-                            bf16x8 w[3];
-                            ld_pieces(LS, NX_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8, w);
-                            acc[mb] = mfma_split(w, dp, acc[mb]);
-                        }
+                    for (int i = 0; i < 80; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
                     }
                 } else {
                 // exact f32, k-step (fb, r) = W2^T row 16fb + 4g + r.  Each fb group of 16 MFMAs is
@@ -1877,7 +1666,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         const int p4 = threadIdx.x + u * BLOCK;
         if (p4 < P_PAD / 4) {
             const int q = ridx(4 * p4);   // 4 | 64: the four entries stay contiguous
-            gst<kWsNt || BS>(reinterpret_cast<f32x4*>(a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x)),
+            gst<BS>(reinterpret_cast<f32x4*>(a.ws + ws_index(4 * p4, blockIdx.x, gridDim.x)),
                        (ld4(lds + q) + ld4(lds + RPAD + q)) + (ld4(lds + 2 * RPAD + q) + ld4(lds + 3 * RPAD + q)));
         }
     }
@@ -1963,7 +1752,9 @@ __global__ __launch_bounds__(FBLOCK) void forward_kernel(const float* tnet, cons
                 mlp_forward_bf16(L, ob, j, g, H1, H2, m0, m1);
                 ls0 = L[NB_LS]; ls1 = L[NB_LS + 1];
             } else {
-                mlp_forward(L, ob, j, g, H1, H2, m0, m1);
+                // BS: beside the bf16 student's forward hipcc issues an LDS load into the SrcC of
+                // one of the teacher's in-flight f32 MFMAs (hazards.py LDSRC): fenced (see mfma())
+                mlp_forward<BS>(L, ob, j, g, H1, H2, m0, m1);
             }
             if (i < n && g == 0) {
                 out[i * 4 + 0] = m0;
@@ -2018,14 +1809,8 @@ namespace {
 // that a pair's tiles run serially while most CUs idle, so small batches use 32- or 16-env
 // groups over more pairs (c2, 4,096 envs: 19.1 us per launch vs 35.4 with 64-env groups).
 // rdd_config.group_envs = 16|32|64 fixes it (tests: the group size changes only the
-// summation order); diagnostic builds (RD_DIAG_KNOBS) also read RDD_GROUP_ENVS.
+// summation order).
 int group_envs(int64_t n, int pairs_total, int fixed) {
-#ifdef RD_DIAG_KNOBS
-    if (const char* e = getenv("RDD_GROUP_ENVS")) {
-        const int v = atoi(e);
-        if (v == 16 || v == 32 || v == 64) return v;
-    }
-#endif
     if (fixed) return fixed;
     if (n >= (int64_t)GROUP * pairs_total) return 64;
     if (n >= (int64_t)32 * pairs_total) return 32;
@@ -2047,17 +1832,9 @@ int image_floats(int kind, bool student) {
 // the consumer, after its last tile of a group (the actions travel with each tile's slot):
 // this balances the roles, since the producer's forward (f32 teacher + bf16 student) is the
 // longer one.  Its MFMAs are all bf16 (XDL: the compiler protects their SrcC) except the
-// teacher's f32 layer 1, which is SrcC-fenced (mfma<true>).  The f32 student: the producer
-// steps the envs it computed the actions for; a consumer-side step there would need the
-// consumer's 80 f32 MFMAs per tile fenced (diagnostic builds: -DRD_CP_VARIANT selects it with
-// RDD_PHYS=consumer, -DRD_MFMA_SRCC_FENCE fences every f32 MFMA).
-#ifdef RD_CP_VARIANT
-bool consumer_physics() {
-    const char* e = getenv("RDD_PHYS");
-    return e && !strcmp(e, "consumer");
-}
-#endif
-
+// exact teacher's f32 ones, which are SrcC-fenced.  The f32 student: the producer steps the
+// envs it computed the actions for (a consumer-side step there measured c4 -0.8 %, c3 +2.7 %,
+// c2 +3.7 % and would need the consumer's f32 MFMAs fenced; profiles/r03h_cp_f32_and_nopack.txt).
 int grid_for(int64_t n, int gs, int cap) {
     const int64_t want = ((n + gs - 1) / gs + PAIRS - 1) / PAIRS;   // one group per pair at least
     return (int)(want < cap ? want : cap);
@@ -2118,9 +1895,6 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     const bool bs = t->cfg.student_dtype == RDD_DTYPE_BF16, spl = t->cfg.f32_split != 0;
     void (*k)(RolloutArgs) = bs ? (spl ? rollout_kernel<true, true, true> : rollout_kernel<true, false, true>)
                                 : (spl ? rollout_kernel<false, true, false> : rollout_kernel<false, false, false>);
-#ifdef RD_CP_VARIANT
-    if (!bs && consumer_physics()) k = spl ? rollout_kernel<false, true, true> : rollout_kernel<false, false, true>;
-#endif
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
     return RD_OK;

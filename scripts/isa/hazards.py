@@ -1,37 +1,86 @@
 #!/usr/bin/env python3
-"""Static MFMA -> VALU hazard listing for one kernel's ISA (settle the
-consumer-side env step's run-to-run differences statically).
+"""Static hazard scan of gfx950 ISA (hipcc -S output): register-sharing instruction pairs whose
+distance in wait states is below the requirement of their hazard class.
 
-For every MFMA, every later vector instruction within WINDOW issue slots that touches one of
-its registers is listed with the number of wait states between them (each instruction = 1,
-`s_nop N` = N + 1), by kind:
-  RAW  VALU/VMEM/DS reads the MFMA's destination
-  WAW  VALU/VMEM/DS writes the MFMA's destination
-  WARc VALU writes the MFMA's SrcC (read over the MFMA's passes)
-  WARab VALU writes SrcA/SrcB
-  MRAW a later MFMA reads this MFMA's destination as SrcA/SrcB (SrcC chaining is exempt)
-The scan follows the text order (fall-through), which is conservative at branch targets.
-Pass counts (4 cycles each), measured on gfx950 (scripts/micro/mfma_mix.hip): 16x16x4 f32 8,
-16x16x32 bf16 4, 16x16x16 bf16 4.  The requirement quoted beside each hit is the CDNA3/CDNA4
-ISA rule for XDL ops, NumPasses + 2 wait states for RAW/WAW/MRAW and NumPasses for a SrcC
-WAR (conservative reading); anything below it would be a missed hazard.
-usage: hazards.py FILE.s SYMBOL_SUBSTRING [WINDOW]
-build: hipcc -O3 --offload-arch=gfx950 --cuda-device-only -S [-DRD_CP_VARIANT] distill.hip"""
+Round 3 used it to settle the consumer-side env step's run-to-run differences (loads issued into
+the SrcC of in-flight f32 MFMAs); round 4 widened it
+from four rollout kernels and one class to EVERY function of every .hip source and these classes
+(requirement in wait states: each instruction = 1, `s_nop N` = N + 1; NP = the MFMA's passes):
+
+  LDSRC  a DS / VMEM load writes the SrcC of an in-flight MFMA                 NP + 2 (completion)
+         (ROCm 7.2 protects this WAR for the XDL/bf16 MFMAs but not for the 8-pass f32 form; a
+         value loaded there is lost for lanes 48-63 -- profiles/r03_srcc_probe_*.txt)
+         (XDL: NP - 1, which hipcc keeps itself)
+  WARc   a VALU writes the SrcC of an in-flight MFMA                           XDL NP - 1, f32 0
+  WARab  a VALU / load writes SrcA/SrcB of an in-flight MFMA                   0 (informational)
+  RAW    a VALU / VMEM / DS reads an MFMA's destination                        NP + 2 (XDL NP + 4)
+  WAW    a VALU / load writes an MFMA's destination                            NP + 2 (XDL NP + 4)
+  MRAW   an MFMA reads an earlier MFMA's destination as SrcA/SrcB              NP + 2
+         (SrcC chaining of the same accumulator is exempt)
+  VMFMA  a VALU writes a VGPR that a later MFMA reads (A/B/C)                  2
+         (cdna_hip_programming.md §5.7 item 2: `s_nop 1` after a VALU-written MFMA operand)
+  STDATA a VALU / MFMA / load overwrites the data VGPRs of an earlier VMEM     2
+         store with more than 64 bits of data (dwordx3/x4): the store reads them after issue
+         (cdna_hip_programming.md §5.7 item 1: an asm dwordx3/x4 store ends with `s_nop 1`)
+  PERM   a VALU writes a VGPR that v_permlane16/32_swap reads                  2
+         (cdna_hip_programming.md T21, LLVM gfx950 "VALU write vdst -> v_permlane read")
+  TRANS  a VALU reads the result of a transcendental (v_exp/log/rcp/rsq/sqrt/sin/cos) 1
+  SGPRV  a VALU-written SGPR (v_readfirstlane/readlane/cmp) read by a VMEM     5
+         instruction as address / descriptor / offset (§5.7 item 2: `s_nop 4`)
+
+The VALU-side requirements are calibrated against hipcc's own output (the smallest distance it
+emits for that class in any product kernel: e.g. it writes an in-flight f32 MFMA's SrcC with a
+VALU at 0 wait states, and the f32 parity tests hold there), so a hit marks a pair the compiler
+did not model.  The scan follows the control flow (fall-through and branch targets, loop back-edges
+included) for WINDOW instructions after each producer, and no further than a few wait states
+past the largest requirement that producer can have.  `;;#ASMSTART` .. `;;#ASMEND` blocks are scanned like compiler
+code: that is where the compiler's hazard recognizer does NOT look (§5.7), so a hit there is the
+interesting kind.
+
+usage: hazards.py FILE.s [SYMBOL_SUBSTRING] [WINDOW]     (no symbol: every function)
+build: hipcc -O3 --offload-arch=gfx950 --cuda-device-only -S -o FILE.s SOURCE.hip"""
 import re
 import sys
 
-PASSES = {"v_mfma_f32_16x16x4_f32": 8, "v_mfma_f32_16x16x4f32": 8, "v_mfma_f32_16x16x32_bf16": 4,
-          "v_mfma_f32_16x16x16_bf16": 4, "v_mfma_f32_16x16x16bf16_1k": 4}
+PASSES = {"v_mfma_f32_16x16x4_f32": 8, "v_mfma_f32_16x16x4f32": 8, "v_mfma_f32_32x32x2_f32": 16,
+          "v_mfma_f32_32x32x2f32": 16, "v_mfma_f32_16x16x32_bf16": 4, "v_mfma_f32_16x16x16_bf16": 4,
+          "v_mfma_f32_16x16x16bf16_1k": 4, "v_mfma_f32_32x32x16_bf16": 8, "v_mfma_f32_32x32x8_bf16": 8}
+TRANS = ("v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_", "v_sin_", "v_cos_")
+LOAD = ("ds_read", "ds_load", "global_load", "buffer_load", "flat_load", "scratch_load")
+STORE = ("global_store", "buffer_store", "flat_store", "scratch_store")
+VMEM = ("global_", "buffer_", "flat_", "scratch_")
+XDL = ("_bf16", "_f16", "_i8", "_fp8", "_bf8", "xf32")   # the XDL (low-precision) MFMA forms
+
+
+def xdl(op):
+    return any(t in op for t in XDL)
+
+
+# requirement of each class (wait states) given the MFMA op and its pass count.  Where the
+# compiler's own hazard recognizer models the pair (VALU-side classes) the requirement is the
+# smallest distance hipcc (ROCm 7.2) itself emits across every product kernel, so a hit marks a
+# pair it did not model (inline asm, a load); where it does not (LDSRC of the f32 form), the
+# measured rule (profiles/r03_srcc_probe_*.txt): the load issues after the MFMA completed.
+REQ = {"LDSRC": lambda op, np: np - 1 if xdl(op) else np + 2,
+       "WARc": lambda op, np: np - 1 if xdl(op) else 0,     # VALU writes of an f32 MFMA's SrcC: interlocked
+       "WARab": lambda op, np: 0,                           # hipcc emits them at 0 (informational)
+       "RAW": lambda op, np: np + 4 if xdl(op) else np + 2,
+       "WAW": lambda op, np: np + 4 if xdl(op) else np + 2,
+       "MRAW": lambda op, np: np + 2,
+       "VMFMA": lambda op, np: 2, "STDATA": lambda op, np: 2, "PERM": lambda op, np: 2,
+       "TRANS": lambda op, np: 1, "SGPRV": lambda op, np: 5}
 
 
 def regs(tok):
-    """VGPR/AGPR numbers of one operand token ('v7', 'v[4:7]', 'a[0:3]') as a set of ('v', n)."""
-    m = re.fullmatch(r"([va])\[(\d+):(\d+)\]", tok)
+    """Register numbers of one operand token ('v7', 'v[4:7]', 'a[0:3]', 's[4:7]', 'vcc') as a set."""
+    m = re.fullmatch(r"([vas])\[(\d+):(\d+)\]", tok)
     if m:
         return {(m.group(1), k) for k in range(int(m.group(2)), int(m.group(3)) + 1)}
-    m = re.fullmatch(r"([va])(\d+)", tok)
+    m = re.fullmatch(r"([vas])(\d+)", tok)
     if m:
         return {(m.group(1), int(m.group(2)))}
+    if tok in ("vcc", "vcc_lo", "vcc_hi"):
+        return {("s", "vcc")}
     return set()
 
 
@@ -43,70 +92,212 @@ def operands(line):
     return [o.split()[0] if o else o for o in ops]
 
 
-def scan(path, sym, window=24):
-    """[(kind, wait states, requirement, MFMA line, MFMA op, line, instruction)] of one kernel."""
+def vset(rs):
+    return {r for r in rs if r[0] in "va"}
+
+
+def classify(l):
+    """(op, written registers, read registers, store-data registers) of one instruction."""
+    op = l.split()[0]
+    o = operands(l)
+    R = [regs(x) for x in o]
+    allr = set().union(*R) if R else set()
+    if op.startswith("v_mfma") or op.startswith("v_smfmac"):
+        return op, (R[0] if R else set()), set().union(*R[1:]) if len(R) > 1 else set(), set()
+    if op.startswith(STORE):
+        data = R[0] if op.startswith("buffer_") else (R[1] if len(R) > 1 else set())
+        return op, set(), allr, data
+    if op.startswith(("ds_write", "ds_store")) or op.startswith("ds_") and not op.startswith(LOAD):
+        # LDS stores / atomics without return: reads only (ds_*_rtn returns into o[0])
+        if "_rtn" in op:
+            return op, R[0], set().union(*R[1:]) if len(R) > 1 else set(), set()
+        return op, set(), allr, set()
+    if op.startswith(LOAD) or (op.startswith(VMEM) and "atomic" in op):
+        if op.startswith(LOAD) and "_lds" in op:   # LDS-DMA: no VGPR destination
+            return op, set(), allr, set()
+        return op, (R[0] if R else set()), set().union(*R[1:]) if len(R) > 1 else set(), set()
+    if op.startswith("v_permlane") and "swap" in op:
+        return op, allr, allr, set()
+    if op.startswith("v_cmpx"):
+        return op, {("s", "exec")}, allr, set()
+    if op.startswith("v_"):
+        w = R[0] if R else set()
+        if op.startswith(("v_cmp_",)) and len(R) == 2:   # e32 form writes vcc implicitly
+            w = {("s", "vcc")}
+        return op, w, set().union(*R[1:]) if len(R) > 1 else set(), set()
+    return op, set(), allr, set()
+
+
+def functions(path):
+    """{symbol: [(line number, instruction or 'label:')]} of every function in an ISA file."""
     lines = open(path).read().split("\n")
-    start = next(i for i, l in enumerate(lines) if l.startswith("_Z") and sym in l and l.split(";")[0].rstrip().endswith(":"))
-    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
-    code = []
-    for i in range(start, end + 1):
-        l = lines[i].strip()
-        if not l or l.startswith((";", ".")) or l.endswith(":"):
+    names = [m.group(1) for m in (re.match(r"\s*\.type\s+([\w.$]+),@function", l) for l in lines) if m]
+    out = {}
+    for name in names:
+        try:
+            start = next(i for i, l in enumerate(lines) if l.split(";")[0].rstrip() == name + ":")
+        except StopIteration:
             continue
-        code.append((i + 1, l))
-    hits = []
-    for idx, (ln, l) in enumerate(code):
+        code = []
+        for i in range(start + 1, len(lines)):
+            l = lines[i].split(";")[0].strip() if not lines[i].strip().startswith(";") else ""
+            if l.startswith(".Lfunc_end") or l.startswith(".size"):
+                break
+            if not l or (l.startswith(".") and not l.endswith(":")):
+                continue
+            code.append((i + 1, l))
+        out[name] = code
+    return out
+
+
+def _cfg(code):
+    """Instructions (labels dropped) and each one's successor indices (fall-through, branch target)."""
+    insts, pos, pending = [], {}, []
+    for ln, l in code:
+        if l.endswith(":"):
+            pending.append(l[:-1])
+            continue
+        for lab in pending:
+            pos[lab] = len(insts)
+        pending = []
+        insts.append((ln, l))
+    for lab in pending:
+        pos[lab] = len(insts)
+    succ = []
+    for k, (ln, l) in enumerate(insts):
         op = l.split()[0]
-        if not op.startswith("v_mfma"):
+        tgt = l.split()[1] if len(l.split()) > 1 else ""
+        if op.startswith(("s_endpgm", "s_setpc_b64")):
+            succ.append([])
+        elif op == "s_branch":
+            succ.append([pos[tgt]] if tgt in pos else [])
+        elif op.startswith("s_cbranch"):
+            succ.append([k + 1] + ([pos[tgt]] if tgt in pos else []))
+        else:
+            succ.append([k + 1])
+    return insts, succ
+
+
+def scan_code(code, window=24):
+    """[(kind, wait states, requirement, line, op, line2, instruction2)] of one function's code.
+    Successors are followed along the control flow (fall-through and branch targets, so loop
+    back-edges too) for up to `window` instructions; a pair reached on several paths is reported
+    once, at its smallest distance."""
+    insts, succ = _cfg(code)
+    parsed = [(ln, l, *classify(l)) for ln, l in insts]
+    best = {}
+    for idx, (ln, l, op, w, r, sd) in enumerate(parsed):
+        is_mfma = op.startswith(("v_mfma", "v_smfmac"))
+        src_trans = op.startswith(TRANS)
+        wide_store = op.startswith(STORE) and re.search(r"(dwordx[34]|_b96|_b128)", op)
+        valu_w = op.startswith("v_") and not is_mfma
+        sgpr_w = {x for x in w if x[0] == "s"} if valu_w else set()
+        vw = vset(w) if (valu_w and not op.startswith("v_cmp")) else set()
+        if not (is_mfma or src_trans or wide_store or vw or sgpr_w):
             continue
-        o = operands(l)
-        dst, a, b, c = (regs(x) for x in (o + ["", "", "", ""])[:4])
-        npass = PASSES.get(op, 8)
-        ws = 0
-        for ln2, l2 in code[idx + 1: idx + 1 + window]:
-            op2 = l2.split()[0]
+        if is_mfma:
+            o = operands(l)
+            dst, a, b, c = (regs(x) for x in (o + ["", "", "", ""])[:4])
+            npass = PASSES.get(op, 8)
+
+        # wait states beyond which no class of this producer can be below its requirement
+        horizon = max(npass + 6, 12) if is_mfma else (6 if sgpr_w else 3)
+
+        def hit(kind, ws, req, k2):
+            key = (kind, idx, k2)
+            if key not in best or ws < best[key][1]:
+                best[key] = (kind, ws, req, ln, op, parsed[k2][0], parsed[k2][1])
+
+        seen = {}
+        stack = [(k, 0, 1) for k in succ[idx]]
+        while stack:
+            k2, ws, steps = stack.pop()
+            if k2 >= len(parsed) or steps > window or ws >= horizon or seen.get(k2, 1 << 30) <= ws:
+                continue
+            seen[k2] = ws
+            ln2, l2, op2, w2, r2, sd2 = parsed[k2]
             if op2 == "s_nop":
-                ws += int(l2.split()[1], 0) + 1
+                nxt = ws + int(l2.split()[1], 0) + 1
+                stack.extend((k3, nxt, steps + 1) for k3 in succ[k2])
                 continue
-            o2 = operands(l2)
-            if op2.startswith("v_mfma"):
-                d2, a2, b2, c2 = (regs(x) for x in (o2 + ["", "", "", ""])[:4])
-                if (a2 | b2) & dst:
-                    hits.append(("MRAW", ws, npass + 2, ln, op, ln2, l2))
-                ws += 1
-                continue
-            if not (op2.startswith("v_") or op2.startswith("ds_") or op2.startswith(("global_", "buffer_"))):
-                ws += 1
-                continue
-            w = regs(o2[0]) if o2 and not op2.startswith(("ds_write", "global_store", "buffer_store")) else set()
-            r = set().union(*(regs(x) for x in (o2[1:] if w else o2))) if o2 else set()
-            if r & dst:
-                hits.append(("RAW", ws, npass + 2, ln, op, ln2, l2))
-            if w & dst:
-                hits.append(("WAW", ws, npass + 2, ln, op, ln2, l2))
-            if w & (c - dst):
-                hits.append(("WARc", ws, npass, ln, op, ln2, l2))
-            if w & (a | b):
-                hits.append(("WARab", ws, 1, ln, op, ln2, l2))
-            ws += 1
-    return hits, code
+            v2w, v2r = vset(w2), vset(r2)
+            m2 = op2.startswith(("v_mfma", "v_smfmac"))
+            ld2 = op2.startswith(LOAD) or (op2.startswith(VMEM) and "atomic" in op2) or "_rtn" in op2
+            killed = False   # the hazard's registers were overwritten on this path: later readers see the new value
+            if is_mfma:
+                if m2:
+                    o2 = operands(l2)
+                    d2, a2, b2, c2 = (regs(x) for x in (o2 + ["", "", "", ""])[:4])
+                    if (a2 | b2) & dst:
+                        hit("MRAW", ws, REQ["MRAW"](op, npass), k2)
+                elif v2r & dst and not op2.startswith("s_"):
+                    hit("RAW", ws, REQ["RAW"](op, npass), k2)
+                if not m2:
+                    if v2w & dst:
+                        hit("WAW", ws, REQ["WAW"](op, npass), k2)
+                    if v2w & (c - dst):
+                        kk = "LDSRC" if ld2 else "WARc"
+                        hit(kk, ws, REQ[kk](op, npass), k2)
+                    if v2w & (a | b):
+                        hit("WARab", ws, REQ["WARab"](op, npass), k2)
+            if wide_store and (v2w & vset(sd)):
+                hit("STDATA", ws, REQ["STDATA"](op, 0), k2)
+            if vw:
+                if m2 and (v2r & vw):
+                    hit("VMFMA", ws, REQ["VMFMA"](op, 0), k2)
+                if op2.startswith("v_permlane") and (v2r & vw):
+                    hit("PERM", ws, REQ["PERM"](op, 0), k2)
+                killed = bool(v2w >= vw) and not m2
+            if src_trans and op2.startswith("v_") and not m2 and (v2r & vset(w)):
+                hit("TRANS", ws, REQ["TRANS"](op, 0), k2)
+            if sgpr_w and op2.startswith(VMEM) and ({x for x in r2 if x[0] == "s"} & sgpr_w):
+                hit("SGPRV", ws, REQ["SGPRV"](op, 0), k2)
+            if not killed:
+                stack.extend((k3, ws + 1, steps + 1) for k3 in succ[k2])
+    return sorted(best.values(), key=lambda h: (h[3], h[5], h[0]))
+
+
+def scan(path, sym, window=24):
+    """Hits of the first function whose name contains `sym` (round-3 interface), and its code."""
+    fns = functions(path)
+    name = next(n for n in fns if sym in n)
+    return scan_code(fns[name], window), fns[name]
+
+
+def scan_all(path, window=24):
+    """{function: hits} for every function of the file."""
+    return {name: scan_code(code, window) for name, code in functions(path).items()}
+
+
+def violations(hits):
+    return [h for h in hits if h[1] < h[2]]
+
+
+def summary(name, hits, code, window):
+    out = [f"{name}: {sum(1 for _, l in code if l.startswith(('v_mfma', 'v_smfmac')))} MFMAs, "
+           f"{len(hits)} register-sharing pairs within {window} slots"]
+    kinds = {}
+    for h in hits:
+        kinds.setdefault((h[0], h[4] if h[0] in ("LDSRC", "WARc", "WARab", "RAW", "WAW", "MRAW") else "-"), []).append(h)
+    for (k, op), hs in sorted(kinds.items()):
+        ws = [h[1] for h in hs]
+        out.append(f"  {k:6s} after {op:28s} n={len(ws):5d} min wait states {min(ws):3d} (requirement {hs[0][2]})")
+    short = violations(hits)
+    out.append(f"  below the requirement: {len(short)}")
+    for h in short[:40]:
+        out.append(f"    {h[0]:6s} ws {h[1]:2d} < {h[2]:2d}: line {h[3]} {h[4]} -> line {h[5]}: {h[6][:90]}")
+    return "\n".join(out)
 
 
 def main():
-    path, sym = sys.argv[1], sys.argv[2]
-    window = int(sys.argv[3]) if len(sys.argv) > 3 else 24
-    hits, code = scan(path, sym, window)
-    short = [h for h in hits if h[1] < h[2]]
-    kinds = {}
-    for h in hits:
-        kinds.setdefault((h[0], h[4]), []).append(h[1])
-    print(f"{sym}: {sum(1 for _, l in code if l.startswith('v_mfma'))} MFMAs, {len(hits)} register-sharing "
-          f"instructions within {window} slots")
-    for (k, op), ws in sorted(kinds.items()):
-        print(f"  {k:5s} after {op:28s} n={len(ws):4d} min wait states {min(ws):3d}")
-    print(f"below the conservative requirement: {len(short)}")
-    for h in short[:40]:
-        print(f"  {h[0]:5s} ws {h[1]:2d} < {h[2]:2d}: line {h[3]} {h[4]} -> line {h[5]}: {h[6][:90]}")
+    path = sys.argv[1]
+    sym = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].isdigit() else None
+    window = int(sys.argv[-1]) if sys.argv[-1].isdigit() else 24
+    fns = functions(path)
+    for name, code in fns.items():
+        if sym and sym not in name:
+            continue
+        print(summary(name, scan_code(code, window), code, window))
 
 
 if __name__ == "__main__":
