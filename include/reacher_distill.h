@@ -125,6 +125,15 @@ int rdd_step(rdd_trainer* tr);
  * optimiser-step counter only; the envs' episode clocks advance with env rollouts. */
 int rdd_rollout_obs(rdd_trainer* tr, const float* obs, int64_t n, int64_t n_global);
 int rdd_step_obs(rdd_trainer* tr, const float* obs, int64_t n);
+/* Rows mode: the same student forward/backward + loss + Adam on caller-given rows whose
+ * teacher output is already recorded -- obs [n][11] and t_pdflat [n][4] = the teacher's
+ * mean[2] | logstd[2] per row (device, t_pdflat 16-byte aligned); no teacher network runs.
+ * The reference's training step on its dataset: sess.run([loss, minimize_adam],
+ * {..., t_pdflat_batch_ph: t_pdflat_batch_array}) (mlp_train.py:146-161, the t_pdflat of
+ * dataset.py:179-194 training_batches).  rdd_rollout_rows fills rdd_grad_buffer() (MSE
+ * normalised by n_global); rdd_step_rows = rollout_rows + apply on one rank. */
+int rdd_rollout_rows(rdd_trainer* tr, const float* obs, const float* t_pdflat, int64_t n, int64_t n_global);
+int rdd_step_rows(rdd_trainer* tr, const float* obs, const float* t_pdflat, int64_t n);
 
 /* The same work as individual launches (for per-kernel timing with events in between, and
  * for accumulating several rollouts into one optimiser step):

@@ -149,7 +149,8 @@ struct RolloutArgs {
     int64_t n, env_base;
     uint64_t seed;
     float* state;                          // [8][n]
-    const float* tnet;                     // teacher: params[P], mu[11], sd[11] (contiguous)
+    const float* tnet;                     // teacher: params[P], mu[11], sd[11] (contiguous); in
+                                           // distill_rows_kernel the rows' recorded teacher pdflat [n][4]
     const float* snet;                     // student
     uint32_t* ctl;                         // [0] completed steps, [4..7] snapshot
     float* ws;                             // [RED_GRID][gridDim.x][RED_COLS] (ws_index)
@@ -1183,10 +1184,12 @@ static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NETB_S
               "LDS budget (split images)");
 
 // BS: bf16 student (RDD_DTYPE_BF16); SPL: split-bf16 f32 hidden layers; CP: the consumer wave
-// steps the envs (else the producer does, from the state it loaded for the observations)
-template <bool BS, bool SPL, bool CP>
+// steps the envs (else the producer does, from the state it loaded for the observations);
+// TGT: observation rows with their recorded teacher pdflat (a.tflat_in), no teacher network
+// (no teacher image in LDS), no env step -- distill_rows_kernel
+template <bool BS, bool SPL, bool CP, bool TGT>
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
-    constexpr int TN = img_t(SPL), SN = img_s(BS, SPL);
+    constexpr int TN = TGT ? 0 : img_t(SPL), SN = img_s(BS, SPL);
     __shared__ __attribute__((aligned(16))) float lds[TN + SN + PAIRS * PSCR];
     float* LT = lds;
     float* LS = lds + TN;
@@ -1253,7 +1256,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
 #pragma unroll
         for (int x = 0; x < 4; ++x) gw3a[x] = gw3b[x] = f32x4{0.f, 0.f, 0.f, 0.f};
         float gb3a = 0, gb3b = 0, gls0 = 0, gls1 = 0, met_l = 0, met_m = 0, met_r = 0, met_n = 0;
-        const float tl0 = a.tnet[P_LS], tl1 = a.tnet[P_LS + 1];
+        // teacher log-std (TGT: per row, from the recorded pdflat, below)
+        const float tl0 = TGT ? 0.0f : a.tnet[P_LS], tl1 = TGT ? 0.0f : a.tnet[P_LS + 1];
         const float sl0 = a.snet[P_LS], sl1 = a.snet[P_LS + 1];
         const float sv0 = __expf(2.0f * sl0), sv1 = __expf(2.0f * sl1);
         const float rtv0 = 1.0f / __expf(2.0f * tl0), rtv1 = 1.0f / __expf(2.0f * tl1);
@@ -1282,8 +1286,23 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 const float* obt = obs + TILE * t * SOS;
                 f32x4 H1[4], H2[4];
                 float mt0, mt1, ms0, ms1;
+                float rl0 = tl0, rl1 = tl1, rr0 = rtv0, rr1 = rtv1;   // this row's teacher log-std, 1/var
                 STAMP(10);
-                if constexpr (BS) {
+                if constexpr (TGT) {
+                    // the reference's t_pdflat feed (mlp_train.py:146-161): this env's recorded
+                    // teacher mean and log-std instead of a teacher query; the student alone runs
+                    const uint32_t row = base + TILE * t + j;
+                    const f32x4 tq = tvalid ? ld4(a.tnet + (size_t)row * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+                    if constexpr (BS) mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
+                    else if constexpr (SPL) mlp_forward_split_t<true>(LS, obt, j, g, H1, H2, ms0, ms1);
+                    else mlp_forward(LS, obt, j, g, H1, H2, ms0, ms1);
+                    mt0 = tq[0];
+                    mt1 = tq[1];
+                    rl0 = tq[2];
+                    rl1 = tq[3];
+                    rr0 = 1.0f / __expf(2.0f * rl0);
+                    rr1 = 1.0f / __expf(2.0f * rl1);
+                } else if constexpr (BS) {
                     // CP: in this kernel's schedule the compiler issues loads into the SrcC
                     // registers of the exact teacher's f32 MFMAs: fenced (see mfma())
                     if constexpr (SPL) mlp_forward_split(LT, obt, j, g, mt0, mt1);
@@ -1302,12 +1321,12 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     dm1 = d1 * a.inv_n_global;
                     lossv = (d0 * d0 + d1 * d1) * (0.5f * a.inv_n_global);
                 } else {
-                    dm0 = d0 * rtv0;
-                    dm1 = d1 * rtv1;
-                    dl0 = sv0 * rtv0 - 1.0f;
-                    dl1 = sv1 * rtv1 - 1.0f;
-                    lossv = (tl0 - sl0 + (sv0 + d0 * d0) * (0.5f * rtv0) - 0.5f) +
-                            (tl1 - sl1 + (sv1 + d1 * d1) * (0.5f * rtv1) - 0.5f);
+                    dm0 = d0 * rr0;
+                    dm1 = d1 * rr1;
+                    dl0 = sv0 * rr0 - 1.0f;
+                    dl1 = sv1 * rr1 - 1.0f;
+                    lossv = (rl0 - sl0 + (sv0 + d0 * d0) * (0.5f * rr0) - 0.5f) +
+                            (rl1 - sl1 + (sv1 + d1 * d1) * (0.5f * rr1) - 0.5f);
                 }
                 if (!tvalid) { dm0 = dm1 = dl0 = dl1 = 0.0f; }
                 if (g == 0 && tvalid) {
@@ -1674,6 +1693,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     RTSTAMP(17);
 }
 
+
 // Sum the rollout's per-workgroup partials (fixed order: deterministic), then TF1 Adam.
 __global__ __launch_bounds__(RED_BLOCK) void reduce_adam_kernel(ReduceArgs a) {
     __shared__ float part[RED_ROWS][RED_COLS];
@@ -1866,7 +1886,8 @@ ReduceArgs reduce_args(const rdd_trainer* t, int reduce, int adam, int accum) {
     return a;
 }
 
-int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs = 0, int64_t n_obs_global = 0) {
+int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs = 0, int64_t n_obs_global = 0,
+                   const float* tflat_in = nullptr) {
     RolloutArgs a;
     a.n = obs_in ? n_obs : t->cfg.n_envs;
     a.obs_in = obs_in;
@@ -1875,7 +1896,7 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     a.env_base = t->cfg.env_base;
     a.seed = t->cfg.seed;
     a.state = t->state;
-    a.tnet = t->tnet;
+    a.tnet = tflat_in ? tflat_in : t->tnet;   // rows mode: the recorded teacher outputs
     a.snet = t->snet;
     a.ctl = t->ctl;
     a.ws = t->ws;
@@ -1893,8 +1914,10 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     }
     t->last_grid = grid;
     const bool bs = t->cfg.student_dtype == RDD_DTYPE_BF16, spl = t->cfg.f32_split != 0;
-    void (*k)(RolloutArgs) = bs ? (spl ? rollout_kernel<true, true, true> : rollout_kernel<true, false, true>)
-                                : (spl ? rollout_kernel<false, true, false> : rollout_kernel<false, false, false>);
+    void (*k)(RolloutArgs) = bs ? (spl ? rollout_kernel<true, true, true, false> : rollout_kernel<true, false, true, false>)
+                                : (spl ? rollout_kernel<false, true, false, false> : rollout_kernel<false, false, false, false>);
+    if (tflat_in)   // the teacher is not run: the bf16 student's kernel does not depend on the teacher's mode
+        k = bs ? rollout_kernel<true, false, false, true> : (spl ? rollout_kernel<false, true, false, true> : rollout_kernel<false, false, false, true>);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
     return RD_OK;
@@ -2093,6 +2116,30 @@ int rdd_step_obs(rdd_trainer* t, const float* obs, int64_t n) {
     rd::DeviceGuard g(t->device);
     RD_HIP(g.err, "rdd_step_obs: hipSetDevice");
     if (int rc = launch_rollout(t, obs, n, n)) return rc;
+    return launch_reduce(t, 1, 1);
+}
+
+static int rows_args(rdd_trainer* t, const float* obs, const float* t_pdflat, int64_t n, int64_t n_global,
+                     const char* what) {
+    if (!t || !obs || !t_pdflat || n <= 0 || n > ((int64_t)1 << 31) || n_global < n)
+        return rd::set_error(RD_EINVAL, "%s: bad argument", what);
+    if (((uintptr_t)t_pdflat & 15) != 0) return rd::set_error(RD_EINVAL, "%s: t_pdflat must be 16-byte aligned", what);
+    return RD_OK;
+}
+
+int rdd_rollout_rows(rdd_trainer* t, const float* obs, const float* t_pdflat, int64_t n, int64_t n_global) {
+    if (int rc = rows_args(t, obs, t_pdflat, n, n_global, "rdd_rollout_rows")) return rc;
+    rd::DeviceGuard g(t->device);
+    RD_HIP(g.err, "rdd_rollout_rows: hipSetDevice");
+    if (int rc = launch_rollout(t, obs, n, n_global, t_pdflat)) return rc;
+    return launch_reduce(t, 1, 0);
+}
+
+int rdd_step_rows(rdd_trainer* t, const float* obs, const float* t_pdflat, int64_t n) {
+    if (int rc = rows_args(t, obs, t_pdflat, n, n, "rdd_step_rows")) return rc;
+    rd::DeviceGuard g(t->device);
+    RD_HIP(g.err, "rdd_step_rows: hipSetDevice");
+    if (int rc = launch_rollout(t, obs, n, n, t_pdflat)) return rc;
     return launch_reduce(t, 1, 1);
 }
 

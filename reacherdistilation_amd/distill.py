@@ -60,6 +60,8 @@ nat.register({
     "rdd_get_counters": (INT, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
     "rdd_rollout_obs": (INT, [P, P, I64, I64]),
     "rdd_step_obs": (INT, [P, P, I64]),
+    "rdd_rollout_rows": (INT, [P, P, P, I64, I64]),
+    "rdd_step_rows": (INT, [P, P, P, I64]),
     "rdd_read_metrics": (INT, [P, I64, P]),
     "rdd_bind_comm": (INT, [P, P]),
     "rdd_allreduce_grad": (INT, [P]),
@@ -212,6 +214,35 @@ class DistillTrainer:
         nat.check(self._lib.rdd_rollout_obs(self._h, nat.ptr(obs), obs.shape[0], n_global or obs.shape[0]),
                   "rdd_rollout_obs")
         self._keep = obs
+
+    # -- rows mode: observations with their recorded teacher pdflat (the reference's dataset) --
+    def step_rows(self, obs: torch.Tensor, t_pdflat: torch.Tensor):
+        """One distillation step on dataset rows: observations [n, 11] and the teacher's recorded
+        pdflat [n, 4] (mean | logstd), the reference's sess.run([loss, minimize_adam],
+        {..., t_pdflat_batch_ph: t_pdflat_batch_array}) (mlp_train.py:146-161).  No teacher
+        network runs; student forward/backward, loss, (all-reduce), TF1 Adam."""
+        obs, tp = self._obs_arg(obs), self._tflat_arg(t_pdflat, obs.shape[0])
+        n = obs.shape[0]
+        if self.world == 1:
+            nat.check(self._lib.rdd_step_rows(self._h, nat.ptr(obs), nat.ptr(tp), n), "rdd_step_rows")
+        else:
+            nat.check(self._lib.rdd_rollout_rows(self._h, nat.ptr(obs), nat.ptr(tp), n, n * self.world),
+                      "rdd_rollout_rows")
+            self.allreduce_grad()
+            nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
+        self._keep = (obs, tp)
+
+    def rollout_rows(self, obs: torch.Tensor, t_pdflat: torch.Tensor, n_global: int | None = None):
+        obs, tp = self._obs_arg(obs), self._tflat_arg(t_pdflat, obs.shape[0])
+        nat.check(self._lib.rdd_rollout_rows(self._h, nat.ptr(obs), nat.ptr(tp), obs.shape[0],
+                                             n_global or obs.shape[0]), "rdd_rollout_rows")
+        self._keep = (obs, tp)
+
+    def _tflat_arg(self, t, n):
+        t = torch.as_tensor(t).to(self.device, torch.float32).contiguous()
+        if t.dim() != 2 or t.shape != (n, 4):
+            raise ValueError("t_pdflat must be [n, 4] (teacher mean | logstd per row)")
+        return t
 
     def _obs_arg(self, obs):
         obs = torch.as_tensor(obs).to(self.device, torch.float32).contiguous()

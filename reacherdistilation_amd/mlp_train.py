@@ -26,7 +26,8 @@ from __future__ import annotations
 
 import torch
 
-from .config import MLP_BATCH_SIZE, MLP_EPISODE_BUDGET, OBSPACE_SHAPE
+from . import _native as nat
+from .config import EPISODE_STEPS, LSTM_BATCH_SIZE, MLP_BATCH_SIZE, MLP_EPISODE_BUDGET, OBSPACE_SHAPE, STEPS_UNROLLED
 from .dataset import DeviceDataset
 from .pages import PageStore
 from .distill import DistillConfig, DistillTrainer
@@ -84,8 +85,8 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
         for ob_batch, t_batch, prev_batch, prew_batch in dataset.training_batches():
             if sm is not None:   # mlp_train.py:145-160 on the reference graph
                 sm.step(rows(ob_batch, prev_batch, prew_batch), t_batch.reshape(-1, 4))
-            else:
-                tr.step_obs(ob_batch.reshape(-1, OBSPACE_SHAPE))
+            else:           # the same feed: the window's recorded teacher pdflat (rows mode)
+                tr.step_rows(ob_batch.reshape(-1, OBSPACE_SHAPE), t_batch.reshape(-1, 4))
             opt_steps += 1
         t_pdflat, s_pdflat = query(ob)
         dataset.write(ob=ob, reward=reward, t_pdflat=t_pdflat, s_pdflat=s_pdflat, stepped_with="s")
@@ -104,3 +105,106 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
             if dataset.num_episodes() >= episodes or done:
                 break
     return (sm or tr), dataset, losses
+
+
+# -- phase 2 on recorded teacher data (no env) ------------------------------------------------
+def _windows(gen, n_eps, lens_ok, count, B=LSTM_BATCH_SIZE, T=STEPS_UNROLLED, device="cuda:0"):
+    """[count, T * B] flat record indices of `count` training batches drawn as the reference's
+    training_batches (dataset.py:179-194): B episodes with replacement and ONE start per batch,
+    T consecutive steps from it."""
+    eps = torch.randint(0, n_eps, (count, B), generator=gen)
+    start = torch.randint(0, EPISODE_STEPS - T + 1, (count, 1, 1), generator=gen)
+    idx = eps[:, None, :] * EPISODE_STEPS + start + torch.arange(T)[None, :, None]   # [count, T, B]
+    return idx.reshape(count, T * B).to(device)
+
+
+def fit_records(ob, t_pdflat, rew=None, *, student: str = "policy", steps: int = 250_000, loss: str = "mse",
+                lr: float = 1e-4, seed: int = 0, device="cuda:0", graph_steps: int = 100, log_every: int = 0,
+                trainer=None):
+    """The reference's phase-2 optimiser steps (mlp_train.py:143-161) on RECORDED teacher data:
+    episodes ob [E, 50, 11] with the teacher's pdflat t_pdflat [E, 50, 4] (and rewards [E, 50]
+    for the reference student's prev_rew), e.g. the fixture's teacher-stepped episodes.  Each
+    step is one Adam step on one training batch of 20 windows x 10 steps (200 rows, drawn as
+    dataset.py:179-194 draws them, from a seeded host generator), with the recorded t_pdflat
+    as the target (rows mode: no teacher network runs).  student="policy": the 2x64 MlpPolicy
+    (DistillTrainer.step_rows), captured `graph_steps` steps per HIP graph with the batch
+    indices drawn ahead into a device buffer; student="mlp": the reference graph
+    (StudentMlpTrainer.step on rows ob | prev_pdflat | prev_rew).  Returns (trainer, history)
+    with history = [(step, mean training action-MSE of the last steps)] every `log_every`."""
+    ob = torch.as_tensor(ob, dtype=torch.float32)
+    tp = torch.as_tensor(t_pdflat, dtype=torch.float32)
+    E = ob.shape[0]
+    dev = torch.device(device)
+    ob_all = ob.reshape(-1, OBSPACE_SHAPE).to(dev).contiguous()
+    t_all = tp.reshape(-1, 4).to(dev).contiguous()
+    gen = torch.Generator().manual_seed(int(seed))
+    history = []
+    if student == "policy":
+        tr = trainer or DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr, metrics_len=graph_steps),
+                                       device=device)
+        rows_per = LSTM_BATCH_SIZE * STEPS_UNROLLED
+        idx_buf = torch.zeros(graph_steps, rows_per, dtype=torch.long, device=dev)
+        ob_buf = torch.zeros(graph_steps, rows_per, OBSPACE_SHAPE, device=dev)
+        t_buf = torch.zeros(graph_steps, rows_per, 4, device=dev)
+        g = torch.cuda.CUDAGraph()
+        prev = torch.cuda.current_stream(dev)
+        torch.cuda.synchronize(dev)
+        with torch.cuda.graph(g):
+            tr.set_stream(torch.cuda.current_stream(dev))
+            torch.index_select(ob_all, 0, idx_buf.reshape(-1), out=ob_buf.reshape(-1, OBSPACE_SHAPE))
+            torch.index_select(t_all, 0, idx_buf.reshape(-1), out=t_buf.reshape(-1, 4))
+            for k in range(graph_steps):
+                nat.check(tr._lib.rdd_step_rows(tr._h, nat.ptr(ob_buf[k]), nat.ptr(t_buf[k]), rows_per),
+                          "rdd_step_rows")
+        tr.set_stream(prev)
+        done = 0
+        while done < steps:
+            idx_buf.copy_(_windows(gen, E, None, graph_steps, device=dev))
+            g.replay()
+            done += graph_steps
+            tr.steps += graph_steps
+            if log_every and done % log_every < graph_steps:
+                m = tr.metrics(graph_steps)
+                history.append((done, float((m[:, 2] / (2 * m[:, 3])).mean())))
+        torch.cuda.synchronize(dev)
+        return tr, history
+    if student != "mlp":
+        raise ValueError(f"unknown student {student!r}")
+    r = torch.zeros(E, EPISODE_STEPS) if rew is None else torch.as_tensor(rew, dtype=torch.float32)
+    prev_t = torch.zeros_like(tp)
+    prev_t[:, 1:] = tp[:, :-1]
+    prev_r = torch.zeros(E, EPISODE_STEPS, 1)
+    prev_r[:, 1:, 0] = r[:, :-1]
+    x_all = rows(ob, prev_t, prev_r).to(dev)
+    sm = trainer or StudentMlpTrainer(StudentMlpConfig(loss=loss, lr=lr, seed=seed), device=device)
+    done = 0
+    while done < steps:
+        for i in _windows(gen, E, None, min(graph_steps, steps - done), device=dev):
+            sm.step(x_all[i], t_all[i])
+        done += min(graph_steps, steps - done)
+        if log_every and done % log_every < graph_steps:
+            m = sm.metrics(min(graph_steps, done))
+            history.append((done, float((m[:, 1] / (2 * m[:, 2])).mean())))
+    torch.cuda.synchronize(dev)
+    return sm, history
+
+
+def action_mse(trainer, ob, t_pdflat, rew=None) -> float:
+    """mean over records and both action dims of (mu_student - mu_teacher)^2 on recorded
+    episodes ob [E, 50, 11] / t_pdflat [E, 50, 4] (the reference LSTM student's
+    0.0212 on the fixture's episodes 21-24 is this quantity)."""
+    ob = torch.as_tensor(ob, dtype=torch.float32)
+    tp = torch.as_tensor(t_pdflat, dtype=torch.float32)
+    dev = trainer.device
+    if isinstance(trainer, DistillTrainer):
+        _, s = trainer.forward(ob.reshape(-1, OBSPACE_SHAPE).to(dev), teacher=False)
+    else:
+        E = ob.shape[0]
+        r = torch.zeros(E, EPISODE_STEPS) if rew is None else torch.as_tensor(rew, dtype=torch.float32)
+        prev_t = torch.zeros_like(tp)
+        prev_t[:, 1:] = tp[:, :-1]
+        prev_r = torch.zeros(E, EPISODE_STEPS, 1)
+        prev_r[:, 1:, 0] = r[:, :-1]
+        s = trainer.forward(rows(ob, prev_t, prev_r).to(dev))
+    d = s[:, :2].double().cpu() - tp.reshape(-1, 4)[:, :2].double()
+    return float((d ** 2).mean())

@@ -1,0 +1,19 @@
+#!/bin/bash
+# r04a: tightened parity suite (per-entry gradient bounds, per-env isolation, per-component state), smoke,
+# and the reference student's fenced weight gradient vs the unfenced build (libreacher_prevmlp.so)
+set -o pipefail
+OUT=gpurun_out/r04a; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -60 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+cat $OUT/smoke.log
+for lib in libreacher_prevmlp.so libreacher.so libreacher_prevmlp.so libreacher.so; do
+  echo "== $lib" >> $OUT/student_mlp_ab.jsonl
+  RD_LIB=$lib timeout -k 10 120 python3 scripts/bench_student_mlp.py 4096 65536 262144 1048576 >> $OUT/student_mlp_ab.jsonl 2>&1 || exit 1
+done
+grep -v cpu $OUT/student_mlp_ab.jsonl | python3 -c "
+import sys, json
+lib = None
+for l in sys.stdin:
+    if l.startswith('=='): lib = l.split()[1]; continue
+    d = json.loads(l); print(lib, d['rows'], 'step_us %.1f' % d['step_us'])"

@@ -1,0 +1,193 @@
+"""Rows mode (rdd_rollout_rows / rdd_step_rows): distillation on observations with their
+RECORDED teacher pdflat, the reference's feed of t_pdflat_batch_ph from its dataset
+(mlp_train.py:146-161) -- and the reference's own teacher data: the fixture's 21
+teacher-stepped episodes (src/distilation/tests/data/dataset.json -> tests/golden/
+reacher_fixture.npz; the real baselines teacher's outputs, no checkpoint needed).
+
+Tolerances: gradients per entry 2e-5 x M_e and 1e-5 x max|g| (tests/parity.py; the teacher
+log-std per row in KL); training trajectories against the oracle (policy_np / refnet_np
+forward + backward in f64, TF1 Adam in f32) on the same batches: per-step loss rtol 2e-3 and
+parameters as tests/test_distill_gpu.py::test_multistep_matches_c_oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import policy_np as pn
+from tests import parity
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _trainer(n=64, **kw):
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    return DistillTrainer(DistillConfig(n_envs=n, seed=3, **kw), device=DEV)
+
+
+def _rows(n, seed):
+    rs = np.random.RandomState(seed)
+    q0, q1 = rs.uniform(-3, 3, n), rs.uniform(-3, 3, n)
+    ob = np.stack([np.cos(q0), np.cos(q1), np.sin(q0), np.sin(q1), rs.uniform(-.2, .2, n), rs.uniform(-.2, .2, n),
+                   rs.uniform(-5, 5, n), rs.uniform(-5, 5, n), rs.uniform(-.3, .3, n), rs.uniform(-.3, .3, n),
+                   np.zeros(n)], 1).astype(np.float32)
+    t = np.concatenate([rs.uniform(-.5, .5, (n, 2)), rs.uniform(-3.5, -0.5, (n, 2))], 1).astype(np.float32)
+    return ob, t
+
+
+@pytest.mark.parametrize("n", [17, 200, 4096])
+@pytest.mark.parametrize("loss", ["mse", "kl"])
+@pytest.mark.parametrize("split", [False, True])
+def test_rows_gradient_matches_oracle(n, loss, split):
+    tr = _trainer(loss=loss, f32_split=split)
+    ob, t = _rows(n, n)
+    sp = tr.student_params().cpu().numpy()
+    tr.rollout_rows(torch.from_numpy(ob), torch.from_numpy(t))
+    g = tr.grad().cpu().numpy()
+    g64, M, L, sq = parity.oracle_grad_rows(sp, tr.student, ob.astype(np.float64), t, loss, n)
+    ok, rep = parity.grad_ok(g, g64, M)
+    print(f"rows n={n} {loss} split={split}: {rep}")
+    assert ok, rep
+
+
+@pytest.mark.parametrize("loss", ["mse", "kl"])
+def test_rows_bf16_student_gradient(loss):
+    n = 4096
+    tr = _trainer(loss=loss, student_dtype="bf16")
+    ob, t = _rows(n, 5)
+    sp = tr.student_params().cpu().numpy()
+    tr.rollout_rows(torch.from_numpy(ob), torch.from_numpy(t))
+    g = tr.grad().cpu().numpy()
+    gb, M, L, sq = parity.oracle_grad_rows(sp, tr.student, ob.astype(np.float64), t, loss, n, bf16=True)
+    rep = parity.grad_report(g, gb, M)
+    print(f"rows bf16 {loss}: {rep}")
+    assert rep["entry"] <= parity.TOL_ENTRY_BF16 and rep["global"] < 1e-2, rep
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_rows_with_the_teacher_outputs_equal_the_teacher_relabel(split):
+    """Rows fed with the teacher network's own pdflat (rdd_forward) give the obs mode's gradient
+    (rdd_rollout_obs relabels with the same teacher) to f32 rounding."""
+    n = 3000
+    tr = _trainer(loss="kl", f32_split=split)
+    ob, _ = _rows(n, 9)
+    obt = torch.from_numpy(ob).to(DEV)
+    t, _ = tr.forward(obt, student=False)
+    tr.rollout_obs(obt)
+    g_obs = tr.grad().clone()
+    tr.rollout_rows(obt, t)
+    g_rows = tr.grad()
+    assert (g_rows - g_obs).abs().max() <= 2e-5 * g_obs.abs().max()
+
+
+def test_rows_argument_errors():
+    from reacherdistilation_amd import _native as nat
+    tr = _trainer()
+    ob, t = _rows(8, 1)
+    with pytest.raises(ValueError):
+        tr.step_rows(torch.from_numpy(ob), torch.from_numpy(t[:7]))
+    tb = torch.zeros(8 * 4 + 1, device=DEV)[1:].view(8, 4)      # 4-byte aligned only
+    tb.copy_(torch.from_numpy(t))
+    with pytest.raises(nat.NativeError):
+        nat.check(tr._lib.rdd_step_rows(tr._h, nat.ptr(torch.from_numpy(ob).to(DEV)), nat.ptr(tb), 8), "x")
+
+
+def _fixture(golden):
+    ob, t, rew, stu = golden["ob"], golden["t"], golden["rew"], golden["student"]
+    teacher_eps = np.flatnonzero(~stu.any(1))
+    assert list(teacher_eps) == list(range(21))
+    return ob, t, rew
+
+
+def _batches(seed, count, E):
+    from reacherdistilation_amd.mlp_train import _windows
+    return _windows(torch.Generator().manual_seed(seed), E, None, count, device="cpu").numpy()
+
+
+@pytest.mark.parametrize("loss", ["mse", "kl"])
+def test_fixture_training_trajectory_matches_oracle(golden, loss):
+    """100 Adam steps of the 2x64 student on the fixture's teacher episodes
+    0-19 (the real teacher's recorded pdflat as targets, 200-row windows as dataset.py:179-194
+    draws them), GPU step_rows vs the oracle on the same rows."""
+    ob, t, rew = _fixture(golden)
+    E, steps, lr = 20, 100, 1e-3
+    ob_all = ob[:E].reshape(-1, 11).astype(np.float32)
+    t_all = t[:E].reshape(-1, 4).astype(np.float32)
+    tr = _trainer(loss=loss, lr=lr)
+    sp = tr.student_params().cpu().numpy().astype(np.float32)
+    opt = pn.AdamTF1(pn.P_TOT, lr=lr)
+    ref_loss = []
+    for idx in _batches(4, steps, E):
+        tr.step_rows(torch.from_numpy(ob_all[idx]), torch.from_numpy(t_all[idx]))
+        g64, _, L, _ = parity.oracle_grad_rows(sp, tr.student, ob_all[idx].astype(np.float64), t_all[idx], loss,
+                                              len(idx))
+        opt.step(sp, g64.astype(np.float32))
+        ref_loss.append(L)
+    got = tr.metrics(steps)[:, 1]
+    print(f"fixture {loss}: loss {ref_loss[0]:.4g} -> {ref_loss[-1]:.4g}, max rel dev "
+          f"{np.max(np.abs(got - ref_loss) / np.abs(ref_loss)):.2e}")
+    np.testing.assert_allclose(got, ref_loss, rtol=2e-3)
+    p = tr.student_params().cpu().numpy()
+    assert np.abs(p - sp).max() < 2e-3 * max(1.0, np.abs(sp).max())
+    assert ref_loss[-1] < 0.5 * ref_loss[0]
+
+
+def test_fit_records_graph_equals_eager_steps(golden):
+    """mlp_train.fit_records (HIP-graph replays of 100 steps) takes exactly the eager
+    step_rows trajectory on the same batches: parameters bitwise equal."""
+    from reacherdistilation_amd.mlp_train import fit_records
+    ob, t, rew = _fixture(golden)
+    E = 20
+    a, _ = fit_records(ob[:E], t[:E], student="policy", steps=200, lr=1e-3, seed=6, device=DEV)
+    b = _trainer(loss="mse", lr=1e-3)
+    ob_all = torch.from_numpy(ob[:E].reshape(-1, 11).astype(np.float32)).to(DEV)
+    t_all = torch.from_numpy(t[:E].reshape(-1, 4).astype(np.float32)).to(DEV)
+    for idx in _batches(6, 200, E):
+        i = torch.from_numpy(idx).to(DEV)
+        b.step_rows(ob_all[i], t_all[i])
+    assert torch.equal(a.student_params(), b.student_params())
+    assert a.counters()[1] == b.counters()[1] == 200
+
+
+def test_fixture_reference_student_trajectory_matches_oracle(golden):
+    """The reference graph student (student_nn.py:51-57, rows ob | prev_pdflat | prev_rew) on the
+    same fixture batches: 30 Adam steps (KL, the reference's loss) vs refnet_np + TF1 Adam."""
+    from oracle import refnet_np as rn
+    from reacherdistilation_amd.student_mlp import StudentMlpConfig, StudentMlpTrainer, rows
+    ob, t, rew = _fixture(golden)
+    E, steps, lr = 20, 30, 1e-3
+    obt, tt = torch.from_numpy(ob[:E].astype(np.float32)), torch.from_numpy(t[:E].astype(np.float32))
+    prev_t = torch.zeros_like(tt)
+    prev_t[:, 1:] = tt[:, :-1]
+    prev_r = torch.zeros(E, 50, 1)
+    prev_r[:, 1:, 0] = torch.from_numpy(rew[:E, :-1].astype(np.float32))
+    x_all = rows(obt, prev_t, prev_r).numpy()
+    t_all = tt.reshape(-1, 4).numpy()
+    sm = StudentMlpTrainer(StudentMlpConfig(loss="kl", lr=lr, seed=0, keep_prob=1.0), device=DEV)
+    p = sm.params().cpu().numpy().astype(np.float32)
+    opt = pn.AdamTF1(rn.P_REF, lr=lr)
+    ref_loss = []
+    for idx in _batches(8, steps, E):
+        sm.step(torch.from_numpy(x_all[idx]), torch.from_numpy(t_all[idx]))
+        fw = rn.forward(p.astype(np.float64), x_all[idx].astype(np.float64))
+        L, d, _ = rn.loss_and_dout(fw["pdflat"], t_all[idx].astype(np.float64), "kl", len(idx))
+        opt.step(p, rn.backward(p.astype(np.float64), fw, d).astype(np.float32))
+        ref_loss.append(L)
+    got = sm.metrics(steps)[:, 0]
+    print(f"fixture reference student: loss {ref_loss[0]:.4g} -> {ref_loss[-1]:.4g}")
+    np.testing.assert_allclose(got, ref_loss, rtol=2e-3)
+
+
+def test_fixture_heldout_mse_falls(golden):
+    """fit_records on episodes 0-19 (5,000 steps, lr 1e-3): the held-out teacher episode 20's
+    action-MSE and that of the reference LSTM student's own episodes 21-24 (labelled by the
+    teacher) fall well below their initial values."""
+    from reacherdistilation_amd.mlp_train import action_mse, fit_records
+    ob, t, rew = _fixture(golden)
+    tr0 = _trainer(loss="mse", lr=1e-3)
+    h0 = action_mse(tr0, ob[20:21], t[20:21])
+    tr, hist = fit_records(ob[:20], t[:20], student="policy", steps=5000, lr=1e-3, seed=1, device=DEV,
+                           log_every=1000)
+    h20, h21 = action_mse(tr, ob[20:21], t[20:21]), action_mse(tr, ob[21:25], t[21:25])
+    print(f"fixture held-out: ep20 {h0:.4g} -> {h20:.4g}; eps 21-24 {h21:.4g}; train {hist}")
+    assert h20 < 0.2 * h0 and h21 < 0.2 * action_mse(tr0, ob[21:25], t[21:25])
