@@ -66,14 +66,21 @@ int rd_comm_destroy(rd_comm* c);
  * Failure: a wait that does not see a peer within timeout_s (wall clock) FAILS the
  * communicator on every rank: the kernel leaves the buffer unsummed, raises this rank's error
  * word and poisons every peer's buffer, so a peer that arrives later fails its exchange too
- * instead of completing it alone.  A trainer with the communicator bound skips the Adam update
- * of a failed exchange (no replica applies a partial sum) and its next rdd_step /
- * rdd_allreduce_grad / counter read returns RD_ECOMM; rd_comm_check() returns RD_ECOMM without
- * synchronising.  A failed communicator fails every later exchange: destroy it.  (A peer that
- * completes within the last poll of the deadline can still have summed while this rank gave
- * up: with the default 60 s limit that window is a poll interval; the replica checksum,
- * DistillTrainer.replicas_identical, detects it.)  The reference's exchange it replaces:
- * MpiAdam's Allreduce(SUM) (backup/student_rollout.py:658-659,709). */
+ * instead of completing it alone.  The blocks of one exchange agree on one outcome per rank
+ * (each posts its verdict on a device counter; the decision is taken once all are in), so a
+ * rank's gradient is either fully summed or untouched.  A trainer with the communicator bound
+ * skips the Adam update of a failed exchange (no replica applies a partial sum) and its next
+ * rdd_step / rdd_allreduce_grad / counter read returns RD_ECOMM; rd_comm_check() returns
+ * RD_ECOMM without synchronising.  A failed communicator fails every later exchange: destroy
+ * it.  Across ranks the outcome is not atomic: a peer whose last flag lands within the final
+ * poll before this rank's deadline can have summed and stepped while this rank skipped, so
+ * after RD_ECOMM the student parameters AND the Adam state must be re-broadcast from one rank
+ * before training resumes on a new communicator (the replica checksum,
+ * DistillTrainer.replicas_identical, detects a divergence).  timeout_s bounds rank-local host
+ * work between two exchanges too: a rank held longer than that (checkpoint I/O, evaluation on
+ * rank 0 only) fails the communicator for good, so size it above any such pause (dist.XgmiComm
+ * defaults to 600 s; torch/RCCL collectives default to 30 min).  The reference's exchange it
+ * replaces: MpiAdam's Allreduce(SUM) (backup/student_rollout.py:658-659,709). */
 #define RD_XCOMM_HANDLE_BYTES 64
 int rd_xcomm_create(rd_comm** out, int nranks, int rank, int device, int64_t cap, double timeout_s, uint8_t* handle);
 int rd_xcomm_connect(rd_comm* c, const uint8_t* handles);

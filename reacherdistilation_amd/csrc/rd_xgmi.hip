@@ -18,9 +18,16 @@
 // does not see a peer before its deadline (rd_xcomm_create's timeout_s, wall clock) FAILS
 // the communicator: it raises the error words (device + host-visible), POISONS every rank's
 // buffer (so a peer that arrives late fails its exchange too instead of completing it alone),
-// and leaves the gradient as it was.  The trainer's Adam kernel reads the device word and
-// skips its update, so no replica applies a partial sum; rdd_step / rd_comm_check report it.
-// A poisoned communicator fails every later exchange at once (destroy it, make a new one).
+// and leaves the gradient as it was.  The blocks of one exchange kernel agree on ONE outcome
+// before any in-place sum: each posts its verdict on a device counter after
+// raising the failure word if it failed, and every block reads the failure word only once all
+// verdicts are in, so the gradient is either fully summed or untouched.  The trainer's Adam
+// kernel reads the device word and skips its update; rdd_step / rd_comm_check report it.
+// Across ranks the outcome can still differ (a peer whose last flag lands just before this
+// rank's deadline sums and steps while this rank skips): after RD_ECOMM the replicas must be
+// re-synchronised from one rank before training goes on (reacher_comm.h;
+// DistillTrainer.step checks and reports it).  A poisoned communicator fails every later
+// exchange at once (destroy it, make a new one).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -49,7 +56,8 @@ struct XgArgs {
     int vec;                  // n >= 4 and grad 16-B aligned: the float4 push
     uint32_t epoch;
     uint64_t deadline_ticks;  // wall-clock limit of each wait, in s_memrealtime ticks (100 MHz)
-    uint32_t* err;            // [0] this communicator failed, [1] blocks that finished pushing (all epochs)
+    uint32_t* err;            // [0] this communicator failed, [1] blocks that finished pushing, [2] blocks
+                              // that posted their verdict (both counted over all epochs)
     volatile uint32_t* herr;  // host-visible copy of err[0]
 };
 
@@ -81,7 +89,10 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
     if (threadIdx.x == 0) bad = poisoned(a) || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (bad) {   // a peer (or this rank) failed an earlier exchange: fail this one, touch nothing
-        if (threadIdx.x == 0) fail(a);
+        if (threadIdx.x == 0) {
+            fail(a);
+            __hip_atomic_fetch_add(a.err + 2, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);   // verdict
+        }
         return;
     }
     // 1. push: this rank's gradient -> slot[rank] of rank dst's buffer
@@ -144,12 +155,25 @@ __global__ __launch_bounds__(XG_BLOCK) void xgmi_allreduce_kernel(XgArgs a) {
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0 && !bad) bad = poisoned(a);   // a peer gave up on this exchange meanwhile
-    __syncthreads();
-    if (bad) {   // the gradient keeps its input; the Adam kernel sees err[0] and skips
-        if (threadIdx.x == 0) fail(a);
-        return;
+    if (threadIdx.x == 0) {
+        // this block's verdict: its waits, or a peer that gave up on this exchange meanwhile;
+        // a failing block raises the failure word BEFORE posting, then every block waits for
+        // all verdicts and decides on the failure word alone -- one outcome per rank
+        if (bad || poisoned(a)) fail(a);
+        __hip_atomic_fetch_add(a.err + 2, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t want = a.epoch * (uint32_t)gridDim.x;
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        while ((int32_t)(__hip_atomic_load(a.err + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+            if (__builtin_amdgcn_s_memrealtime() - t1 > a.deadline_ticks) {   // (cannot happen: every
+                fail(a);                                                      // block posts; bounded anyway)
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        bad = __hip_atomic_load(a.err, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     }
+    __syncthreads();
+    if (bad) return;   // the gradient keeps its input; the Adam kernel sees err[0] and skips
     __threadfence_system();
     // 4. this block's share of the columns: the sum over ranks in rank order
     const int64_t per = (a.n + gridDim.x - 1) / gridDim.x;
@@ -227,8 +251,8 @@ int rd_xcomm_create(rd_comm** out, int nranks, int rank, int device, int64_t cap
     static_assert((XG_POISON + 1) * sizeof(uint32_t) <= XG_FLAGS_BYTES, "flag words");
     hipError_t e = hipExtMallocWithFlags((void**)&c->mine, bytes, hipDeviceMallocUncached);
     if (e == hipSuccess) e = hipMemset(c->mine, 0, bytes);
-    if (e == hipSuccess) e = hipMalloc((void**)&c->err, 2 * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemset(c->err, 0, 2 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->err, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(c->err, 0, 4 * sizeof(uint32_t));
     void* hp = nullptr;   // pinned, coherent host word the kernel raises on failure
     if (e == hipSuccess) e = hipHostMalloc(&hp, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess) {

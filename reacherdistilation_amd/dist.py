@@ -161,9 +161,13 @@ class XgmiComm(RcclComm):
     IPC, a buffer that cannot be mapped) raises on every rank.  `cap` = floats per exchange;
     `timeout` = seconds an exchange waits for a peer before the communicator fails on every
     rank (the bound trainer then skips that optimiser step and raises NativeError on its next
-    call; include/reacher_comm.h)."""
+    call; include/reacher_comm.h).  It also bounds rank-local host work between two exchanges:
+    a rank held longer (checkpoint I/O, evaluation on rank 0 only) fails the communicator for
+    good, hence the 10-minute default.  After such a failure re-broadcast the student and its
+    Adam state from one rank before training on a new communicator: the outcome of the failed
+    exchange is atomic per rank, not across ranks."""
 
-    def __init__(self, device, group=None, cap: int = 8192, timeout: float = 60.0):
+    def __init__(self, device, group=None, cap: int = 8192, timeout: float = 600.0):
         import ctypes
 
         import torch

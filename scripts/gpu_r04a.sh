@@ -2,7 +2,7 @@
 # r04a: tightened parity suite (per-entry gradient bounds, per-env isolation, per-component state), smoke,
 # and the reference student's fenced weight gradient vs the unfenced build (libreacher_prevmlp.so)
 set -o pipefail
-OUT=gpurun_out/r04a; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r04a}; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -60 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }

@@ -13,18 +13,20 @@ one wrong lane group (the lanes-48-63 class passed a green suite in r03w).  Thes
   gradient of a batch minus the gradient of the same batch with env e replaced is env e's
   contribution minus the replacement's, compared per entry at small N where every lane of a
   64-env group owns one env;
-* env state per component: angles and fingertip offsets atol 1e-5, velocities atol 1e-5 +
-  rtol 1e-5, targets bitwise, for envs whose joint limit is inactive; the limit-active envs keep
-  the round-3 bound (the clamp's branch can flip between f32 and f64 near |q1| = 3).
+* env state per component: angles atol 2e-6, fingertip offsets 1e-6, velocities 5e-6 + 1e-6
+  rel, targets bitwise, for envs whose joint limit is inactive; the limit-active envs keep the
+  round-3 bound (the clamp's branch can flip between f32 and f64 near |q1| = 3).
 tests/test_parity_mutation.py shows on CPU that each check rejects one wrong env in lanes 48-63.
 """
 import numpy as np
 
 from oracle import policy_np as pn
 
-TOL_GLOBAL = 1e-5          # x max|g64|      (measured on MI355X: see tests/test_distill_gpu.py)
+# measured on MI355X (r04a, profiles/r04a_parity_errors.txt): global <= 3.8e-7, per entry <= 1.5e-6
+# (f32 / split, N = 17 .. 262,144); bf16 student vs its bf16 definition: per entry <= 1.5e-5
+TOL_GLOBAL = 1e-5          # x max|g64|
 TOL_ENTRY = 2e-5           # x M_e, f32 / split modes
-TOL_ENTRY_BF16 = 2e-2      # x M_e, bf16 student (bf16 rounding flips of single operands)
+TOL_ENTRY_BF16 = 1e-4      # x M_e, bf16 student (a rare bf16 rounding flip of one operand)
 BLOCKS = (("W1", pn.P_W1, pn.P_B1), ("b1", pn.P_B1, pn.P_W2), ("W2", pn.P_W2, pn.P_B2),
           ("b2", pn.P_B2, pn.P_W3), ("W3", pn.P_W3, pn.P_B3), ("b3", pn.P_B3, pn.P_LS), ("ls", pn.P_LS, pn.P_TOT))
 
@@ -82,16 +84,19 @@ def per_env_contributions(sp, fs, dmean, dls_per_env, bf16=False):
     return out
 
 
-def state_ok(st1, ref, active):
+def state_ok(st1, ref, active, vtol=(5e-6, 1e-6)):
     """Per-component env-state bounds after one step (rows q0 q1 v0 v1 tx ty dx dy); `active`:
-    envs whose joint-1 limit is (or may be) engaged, held to the round-3 bound."""
+    envs whose joint-1 limit is (or may be) engaged, held to the round-3 bound; `vtol`: the
+    velocity bound (atol, rtol) -- wider where the actions themselves carry the bf16 student's
+    rounding (DAgger with the bf16 student: measured 7.5e-6)."""
     st1 = np.asarray(st1, np.float64)
     ref = np.asarray(ref, np.float64)
     inact = ~active
     worst = {}
     ok = True
-    for rows, atol, rtol, name in (((0, 1), 1e-5, 0.0, "q"), ((2, 3), 1e-5, 1e-5, "v"), ((4, 5), 0.0, 0.0, "target"),
-                                   ((6, 7), 1e-5, 0.0, "offset")):
+    # measured (r04a): |dq| <= 2.4e-7, |dv| <= 1.7e-6 (|v| <= 9), |doffset| <= 5.4e-8
+    for rows, atol, rtol, name in (((0, 1), 2e-6, 0.0, "q"), ((2, 3), vtol[0], vtol[1], "v"), ((4, 5), 0.0, 0.0, "target"),
+                                   ((6, 7), 1e-6, 0.0, "offset")):
         a, b = st1[list(rows)][:, inact], ref[list(rows)][:, inact]
         excess = np.abs(a - b) - (atol + rtol * np.abs(b))
         worst[name] = float(np.abs(a - b).max()) if a.size else 0.0

@@ -268,7 +268,7 @@ def test_bf16_rollout_gradient_matches_bf16_oracle(loss):
     from tests import parity
     rep = parity.grad_report(g, gb, parity.abs_scale(sp, fs, dmean, dls, bf16=True))
     print(f"bf16 grad {loss}: global {err_b:.2e} vs f32 {err_f:.2e}; {rep}")
-    assert err_b < 1e-2, err_b
+    assert err_b < 1e-4, err_b
     assert rep["entry"] <= parity.TOL_ENTRY_BF16, rep
     assert err_f > 2 * err_b, (err_f, err_b)
 
@@ -381,7 +381,8 @@ def test_fused_step_joint_limit_and_resets_match_oracle(oracle_c, split, act, sd
     assert np.all(np.abs(ref[1][active & ~reset]) > 2.9)
     keep = ~reset
     from tests import parity
-    sok, worst = parity.state_ok(st1[:, keep], ref[:, keep], active[keep])
+    sok, worst = parity.state_ok(st1[:, keep], ref[:, keep], active[keep],
+                                 vtol=(3e-5, 1e-5) if sdt == "bf16" and act == "student" else (5e-6, 1e-6))
     print(f"fused step split={split} act={act} {sdt}: {worst}")
     assert sok, worst
     draws = oracle_c.philox_draws(seed, np.flatnonzero(reset), 1)
@@ -407,8 +408,9 @@ def test_each_env_contribution_isolated(n, gs, split, loss):
     """Every env of a small batch, i.e. every lane 0..63 of a 64-env group (and of 16- / 32-env
     groups), owns one env; its contribution to every gradient entry is isolated as
     g(batch) - g(batch with env e replaced by a fixed env z) = c(x_e) - c(z) and compared with
-    the oracle's per entry: |error| <= 1e-4 x (M(x_e) + M(z)) + 2e-5 x M(batch) (the second term:
-    the f32 round-off of the two batch sums).  One env's wrong lane -- a lost load in lanes
+    the oracle's per entry: |error| <= 1e-5 x (M(x_e) + M(z)) + 5e-6 x M(batch) (the second term:
+    the f32 round-off of the two batch sums; measured r04a: worst error 0.014 of the round's first,
+    4x looser, bound).  One env's wrong lane -- a lost load in lanes
     48-63 -- moves c(x_e) by O(1) in the entries it touches, far past this bound
     (tests/test_parity_mutation.py)."""
     from tests import parity
@@ -441,7 +443,7 @@ def test_each_env_contribution_isolated(n, gs, split, loss):
         d64 = g64_all - g64_e
         _, Mx, _ = parity.oracle_grad(sp, tr.teacher, tr.student, ob[e:e + 1], loss, n)
         _, Mz, _ = parity.oracle_grad(sp, tr.teacher, tr.student, obz, loss, n)
-        bound = 1e-4 * (Mx + Mz) + 2e-5 * np.maximum(M_all, M_e)
+        bound = 1e-5 * (Mx + Mz) + 5e-6 * np.maximum(M_all, M_e)
         r = np.abs(d_gpu - d64) / np.where(bound > 0, bound, 1.0)
         r[(bound == 0) & (np.abs(d_gpu - d64) > 0)] = np.inf
         worst = max(worst, float(r.max()))
@@ -453,7 +455,7 @@ def test_each_env_contribution_isolated(n, gs, split, loss):
 @pytest.mark.parametrize("loss", ["mse", "kl"])
 def test_each_env_contribution_isolated_bf16(loss):
     """The same isolation for the bf16 student (DAgger, config 5's arithmetic) at 64 envs, with
-    its rounding-flip tolerance: |error| <= 2e-2 x (M(x_e) + M(z)) + 2e-3 x M(batch)."""
+    its rounding-flip tolerance: |error| <= 1e-4 x (M(x_e) + M(z)) + 2e-5 x M(batch)."""
     from tests import parity
     n = 64
     rs = np.random.RandomState(11)
@@ -482,7 +484,7 @@ def test_each_env_contribution_isolated_bf16(loss):
         obe[e] = obz[0]
         g64_e, M_e, _ = parity.oracle_grad(sp, tr.teacher, tr.student, obe, loss, n, bf16=True)
         _, Mx, _ = parity.oracle_grad(sp, tr.teacher, tr.student, ob[e:e + 1], loss, n, bf16=True)
-        bound = 2e-2 * (Mx + Mz) + 2e-3 * np.maximum(M_all, M_e)
+        bound = 1e-4 * (Mx + Mz) + 2e-5 * np.maximum(M_all, M_e)
         err = np.abs(d_gpu - (g64_all - g64_e))
         r = err / np.where(bound > 0, bound, 1.0)
         r[(bound == 0) & (err > 0)] = np.inf

@@ -88,7 +88,7 @@ def test_env_isolation_rejects_a_wrong_lane(loss):
         obe[e] = z
         g_e, M_e, _ = parity.oracle_grad(s.flat, t, s, obe, loss, n)
         _, Mx, _ = parity.oracle_grad(s.flat, t, s, ob[e:e + 1], loss, n)
-        bound = 1e-4 * (Mx + Mz) + 2e-5 * np.maximum(M_all, M_e)
+        bound = 1e-5 * (Mx + Mz) + 5e-6 * np.maximum(M_all, M_e)
         d64 = g_all - g_e
         d_f32 = g_all.astype(np.float32).astype(np.float64) - g_e.astype(np.float32).astype(np.float64)
         assert (np.abs(d_f32 - d64) <= bound).all()

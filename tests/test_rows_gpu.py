@@ -61,7 +61,7 @@ def test_rows_bf16_student_gradient(loss):
     gb, M, L, sq = parity.oracle_grad_rows(sp, tr.student, ob.astype(np.float64), t, loss, n, bf16=True)
     rep = parity.grad_report(g, gb, M)
     print(f"rows bf16 {loss}: {rep}")
-    assert rep["entry"] <= parity.TOL_ENTRY_BF16 and rep["global"] < 1e-2, rep
+    assert rep["entry"] <= parity.TOL_ENTRY_BF16 and rep["global"] < 1e-4, rep
 
 
 @pytest.mark.parametrize("split", [False, True])
@@ -129,7 +129,7 @@ def test_fixture_training_trajectory_matches_oracle(golden, loss):
     np.testing.assert_allclose(got, ref_loss, rtol=2e-3)
     p = tr.student_params().cpu().numpy()
     assert np.abs(p - sp).max() < 2e-3 * max(1.0, np.abs(sp).max())
-    assert ref_loss[-1] < 0.5 * ref_loss[0]
+    assert ref_loss[-1] < (0.5 if loss == "mse" else 0.9) * ref_loss[0]
 
 
 def test_fit_records_graph_equals_eager_steps(golden):
