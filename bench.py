@@ -58,6 +58,10 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 FLOP_SPLIT_PER_NET_L2 = 2 * 64 * 64
 FLOP_L1 = 2 * 11 * 64
 PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
+# reference numbers quoted beside the fixture leg (derived from the fixture)
+REF_LSTM_STUDENT_MSE = 0.0212
+# the round-3 mixed peaks (mixed_peak() of the round-3 FLOP mix), frozen for a round-stable frac
+FIXED_PEAK = {("f32", True): 376.9, ("f32", False): 157.3, ("bf16", True): 1058.0}      # the reference LSTM student vs the teacher on the fixture's episodes 21-24
 
 
 def default_f32_mode():
@@ -94,6 +98,13 @@ def parse():
     ap.add_argument("--conv-small-envs", type=int, default=64,
                     help="env count of the second convergence run (the env-step reading of the budget: "
                          "scripts/conv_sweep.py measured 16/32/64/128 envs within it at lr 1e-4, 256 not)")
+    ap.add_argument("--fixture-steps", type=int, default=250_000,
+                    help="convergence_fixture leg: Adam steps of the 2x64 student on the fixture's teacher episodes "
+                         "0-19 (the reference's budget: 5000 episodes x 50 steps); 0 = skip")
+    ap.add_argument("--fixture-ref-steps", type=int, default=25_000,
+                    help="the same leg's steps for the reference graph student (student_nn.py:51-57)")
+    ap.add_argument("--no-strong-projection", action="store_true",
+                    help="at N = 1 skip timing c4's 2/4/8-GPU strong shards (strong_projection)")
     return ap.parse_args()
 
 
@@ -182,6 +193,29 @@ def env_roofline(dev, n=1 << 24, iters=100, warmup=20):
     gbs = 113 * n / sec / 1e9
     return {"kernel": "rd_step_kernel", "bound": "hbm", "envs": n, "env_steps_per_s": n / sec,
             "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
+
+
+def copy_ceiling(gib=1.0, reps=20):
+    """The float4 copy ceiling measured in this run (scripts/micro/copy_bw.hip built as
+    scripts/micro/libcopybw.so: grid-stride 16 B and one-shot float4 x4 / x8, plain and
+    non-temporal; read + write bytes / s), the practical HBM ceiling the env kernel is quoted
+    against (MI355X_MICROARCH.md: 6.29 TB/s measured for a float4 copy).  None if not built."""
+    import ctypes
+    path = os.path.join(ROOT, "scripts", "micro", "libcopybw.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.copy_bw_tbs.restype = ctypes.c_double
+    lib.copy_bw_tbs.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.copy_bw_name.restype = ctypes.c_char_p
+    lib.copy_bw_name.argtypes = [ctypes.c_int]
+    nbytes = int(gib * (1 << 30))
+    res = {}
+    for v, blocks in ((1, 65536), (2, 65536), (3, 0), (4, 0), (5, 0), (6, 0)):
+        res[lib.copy_bw_name(v).decode()] = 1e3 * lib.copy_bw_tbs(nbytes, v, blocks, reps)   # GB/s
+    best = max(res, key=res.get)
+    return {"best_gbs": res[best], "best": best, "variants_gbs": res, "bytes": nbytes,
+            "source": "scripts/micro/copy_bw.hip (libcopybw.so), this run"}
 
 
 def copy_bandwidth(dev, gib=1.0, iters=40):
@@ -386,6 +420,100 @@ def strong_leg(wl, total, sdt, split, dev, lr, steps, warmup, rank, world, comm,
     return out
 
 
+def strong_projection(wl, sdt, split, dev, lr, steps, settle_ms):
+    """the compute side of c4's strong-scaling curve measured on one GPU --
+    one-process steps at the 2/4/8-GPU shards of the 262,144-env global batch (131,072 /
+    65,536 / 32,768 envs), the sharded step's extra launch (rollout, reduce, [exchange], Adam:
+    three launches instead of rdd_step's two) measured at each shard -- and a MODEL of the
+    exchange: `exchange_us_model` low = the one-kernel xGMI push measured with two ranks on one
+    GPU (profiles/r03a_n2_rehearsal.json), high = 25 us, an assumed small-message RCCL
+    all-reduce over xGMI at 8 GPUs (never measured here: no multi-GPU box).  projected
+    speedup = N x t(262,144 on 1 GPU) / (t(shard) + t(split) + exchange)."""
+    import torch
+
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    total = wl["envs"]
+    xlo, xhi = 9.2, 25.0
+    out = {"global_envs": total, "target_speedup_8": 6.0, "exchange_us_model": {"low": xlo, "high": xhi},
+           "model": "N t1 / (t_shard + t_split + exchange); t_* measured here, exchange modelled", "shards": {}}
+    t1 = None
+    for N in (1, 2, 4, 8):
+        n = total // N
+        tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
+                                          student_dtype=sdt, f32_split=split), device=dev)
+        settle(tr.step, dev, settle_ms)
+
+        def timeit(fn):
+            for _ in range(20):
+                fn()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                fn()
+            torch.cuda.synchronize(dev)
+            return (time.perf_counter() - t0) * 1e6 / steps
+
+        def three():   # the sharded step's launches with a zero-cost exchange
+            tr.launch(tr.STAGE_ROLLOUT)
+            tr.launch(tr.STAGE_REDUCE)
+            tr.launch(tr.STAGE_APPLY)
+        us = timeit(tr.step)
+        us3 = timeit(three)
+        tr.close()
+        if N == 1:
+            t1 = us
+            out["t1_us"] = us
+            continue
+        split_us = max(0.0, us3 - us)
+        lo = N * t1 / (us + split_us + xhi)
+        hi = N * t1 / (us + split_us + xlo)
+        out["shards"][str(N)] = {"envs_per_gpu": n, "step_us": us, "sharded_step_launches_us": us3,
+                                 "split_overhead_us": split_us,
+                                 "projected_speedup": {"with_exchange_high": lo, "with_exchange_low": hi},
+                                 "projected_env_steps_per_s": {"with_exchange_high": total / (us + split_us + xhi) * 1e6,
+                                                               "with_exchange_low": total / (us + split_us + xlo) * 1e6}}
+    s8 = out["shards"]["8"]["projected_speedup"]
+    out["meets_6x_at_8"] = {"with_exchange_low": s8["with_exchange_low"] >= 6.0,
+                            "with_exchange_high": s8["with_exchange_high"] >= 6.0}
+    return out
+
+
+def convergence_fixture(dev, lr, steps, ref_steps):
+    """distillation from the reference's REAL teacher data -- the fixture's
+    teacher-stepped episodes (src/distilation/tests/data/dataset.json via
+    tests/golden/reacher_fixture.npz: observations with the baselines teacher's recorded pdflat).
+    Train on episodes 0-19 (rows mode: recorded t_pdflat as the target, 200-row windows as
+    dataset.py:179-194 draws them, one Adam step each, lr as the reference) and report the
+    held-out action-MSE on teacher episode 20 and on episodes 21-24 (the reference LSTM
+    student's own trajectories, labelled by the teacher) beside that student's 0.0212 on them."""
+    import numpy as np
+
+    from reacherdistilation_amd import mlp_train
+    path = os.path.join(ROOT, "tests", "golden", "reacher_fixture.npz")
+    if not os.path.exists(path):
+        return None
+    d = np.load(path)
+    ob, t, rew = d["ob"], d["t"], d["rew"]
+    out = {"data": "reference fixture (dataset.json): 21 teacher-stepped episodes, 4 stepped by the reference LSTM "
+                   "student; train = teacher episodes 0-19 (1,000 records), held out = episode 20 and episodes 21-24",
+           "reference_lstm_student_mse_eps21_24": REF_LSTM_STUDENT_MSE, "lr": lr, "loss": "mse",
+           "target_mse": 1e-3, "reference_budget_opt_steps": 5000 * 50}
+    for student, k in (("policy", steps), ("mlp", ref_steps)):
+        if k <= 0:
+            continue
+        t0 = time.perf_counter()
+        tr, hist = mlp_train.fit_records(ob[:20], t[:20], rew[:20], student=student, steps=k, loss="mse", lr=lr,
+                                         seed=0, device=dev, log_every=max(k // 10, 100))
+        el = time.perf_counter() - t0
+        out["student_2x64" if student == "policy" else "student_reference_graph"] = {
+            "opt_steps": k, "seconds": el, "train_mse_curve": hist,
+            "heldout_mse_ep20": mlp_train.action_mse(tr, ob[20:21], t[20:21], rew[20:21]),
+            "heldout_mse_eps21_24": mlp_train.action_mse(tr, ob[21:25], t[21:25], rew[21:25]),
+            "train_mse_eps0_19": mlp_train.action_mse(tr, ob[:20], t[:20], rew[:20])}
+        tr.close()
+    return out
+
+
 def cpu_baseline(workload, seconds, threads, n):
     """Time the oracle's C f32 rollout+distill step (OpenMP) at the workload's own env count
     (the same per-GPU batch as the timed GPU step), for a bounded number of steps."""
@@ -451,6 +579,9 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
     budget = 5000 * 50   # mlp_train.py:143-204: 5000 episodes x 50 steps, one Adam step per env step
     return {"target_mse": target, "lr": lr, "loss": wl["loss"], "envs_total": n * world,
             "steps_checked_every": chunk, "opt_steps_to_target": hit, "env_steps_to_target": env_steps,
+            "env_count_choice": ("the small-batch env count is a sweep's pick (scripts/conv_sweep.py, "
+                                 "profiles/r03_conv_sweep.jsonl, lr 1e-4): 16/32/64/128 envs per step reach < 1e-3 "
+                                 "within 250,000 env steps, 256 do not") if n * world <= 256 else None,
             "reference_budget_opt_steps": budget, "reference_budget_env_steps": budget,
             "within_opt_step_budget": hit is not None and hit <= budget,
             "within_env_step_budget": env_steps is not None and env_steps <= budget,
@@ -698,6 +829,10 @@ def main():
                          "peak_basis": ("MFMA-time-weighted peak of the FLOP mix: f32 MFMA 157.3 TF; split-emulated "
                                         "f32 (six bf16 products) 2500/6 TF; bf16 2500 TF"),
                          "frac_of_f32_mfma_peak": achieved / PEAK_F32_TFLOPS,
+                         # round-stable reading: the same FLOP mix's peak as in round
+                         # 3 (c4 split 376.9 TF, c5 1,058 TF), held fixed while the mix is unchanged
+                         "frac_fixed_basis": achieved / FIXED_PEAK.get((sdt, split), peak),
+                         "fixed_peak": FIXED_PEAK.get((sdt, split), peak),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "flop_per_env_step": FLOP_PER_ENV_STEP, "launch_us": kern_ms * 1e3,
                          "launch_timing": f"HIP events around each of {npass} rollout launches, a pass after "
@@ -722,7 +857,17 @@ def main():
             if world == 1:
                 out["convergence_reference_driver"] = convergence_driver(dev, args.lr)
         out["roofline_env"] = env_roofline(dev)
-        out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / copy_gbs
+        ceil = copy_ceiling()
+        if ceil is not None:   # the float4 copy measured in this run
+            out["roofline_env"]["copy_ceiling"] = ceil
+            out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / ceil["best_gbs"]
+        else:
+            out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / copy_gbs
+            out["roofline_env"]["copy_ceiling"] = "torch copy_ (scripts/micro/libcopybw.so not built)"
+        if world == 1 and args.workload == "c4" and not args.no_strong_projection and not args.envs_per_gpu:
+            out["strong_projection"] = strong_projection(wl, sdt, split, dev, args.lr, 200, min(args.settle_ms, 100.0))
+        if world == 1 and args.fixture_steps > 0:
+            out["convergence_fixture"] = convergence_fixture(dev, args.lr, args.fixture_steps, args.fixture_ref_steps)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads, n)
             out["cpu_baseline"]["ref_loop"] = cpu_ref_loop(min(4.0, args.cpu_seconds))

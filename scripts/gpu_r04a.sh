@@ -17,3 +17,12 @@ lib = None
 for l in sys.stdin:
     if l.startswith('=='): lib = l.split()[1]; continue
     d = json.loads(l); print(lib, d['rows'], 'step_us %.1f' % d['step_us'])"
+timeout -k 10 900 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { tail -20 $OUT/bench_default.err; exit 1; }
+python3 - $OUT/bench_default.json <<'P'
+import json, sys
+d = json.load(open(sys.argv[1]))
+print("value %.4g ms/step %.4f frac %.3f fixed %.3f" % (d["value"], d["ms_per_step"], d["roofline"]["frac"], d["roofline"]["frac_fixed_basis"]))
+print("env", {k: d["roofline_env"][k] for k in ("achieved", "frac", "frac_of_measured_copy")}, d["roofline_env"].get("copy_ceiling"))
+print("strong", json.dumps(d.get("strong_projection")))
+print("fixture", json.dumps(d.get("convergence_fixture")))
+P
