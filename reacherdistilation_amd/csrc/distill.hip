@@ -1004,26 +1004,24 @@ __global__ __launch_bounds__(256) void pack_net_kernel(const float* net, float* 
     for (int p = x; p < P_TOT; p += gridDim.x * 256) pack_param(img, p, net[p], student != 0, kind);
 }
 
-// Both rollout images (contiguous in LDS: teacher then student) with every 16-B load of a
-// thread issued before its first LDS store, so a workgroup keeps ~3.7k loads in flight
-// instead of one round trip per loop iteration.
-// `between` runs while the loads are in flight (the producers' first observations).
+// Both rollout images (contiguous in LDS: teacher then student) by LDS-DMA: every 16-B piece is
+// one global_load_lds_dwordx4 (wave-uniform LDS base + lane x 16 B, per-lane global address), so
+// the copy needs no staging VGPRs and no ds_write pass.  `between` runs while they are in flight
+// (the producers' first observations; hipcc waits vmcnt(0) before it uses the state loads, so the
+// image has landed by then) and the caller's __syncthreads publishes the image.  Measured against
+// the register-staged copy it replaces (profiles/r04c_imgdma_ab.txt): c2 -0.3 us per step, c3
+// -0.3, c5 -0.2, c4 -0.2; that form is in profiles/r04_removed_diagnostic_variants.diff.
 template <int V4A, int V4B, int NT, class F>
 __device__ __forceinline__ void copy_images(float* L, const float* ta, const float* sb, F&& between) {
     constexpr int TOT = V4A + V4B, PER = (TOT + NT - 1) / NT;
-    f32x4 r[PER];
+    const int wbase = threadIdx.x & ~63;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const int x = threadIdx.x + u * NT;
-        if (x < V4A) r[u] = reinterpret_cast<const f32x4*>(ta)[x];
-        else if (x < TOT) r[u] = reinterpret_cast<const f32x4*>(sb)[x - V4A];
+        if (x < TOT)
+            __builtin_amdgcn_global_load_lds(x < V4A ? ta + 4 * x : sb + 4 * (x - V4A), L + 4 * (wbase + u * NT), 16, 0, 0);
     }
     between();
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int x = threadIdx.x + u * NT;
-        if (x < TOT) reinterpret_cast<f32x4*>(L)[x] = r[u];
-    }
 }
 
 // bf16-student forward of a 16-env tile (same outputs/layouts as mlp_forward).

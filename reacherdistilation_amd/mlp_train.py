@@ -112,10 +112,12 @@ def _windows(gen, n_eps, lens_ok, count, B=LSTM_BATCH_SIZE, T=STEPS_UNROLLED, de
     """[count, T * B] flat record indices of `count` training batches drawn as the reference's
     training_batches (dataset.py:179-194): B episodes with replacement and ONE start per batch,
     T consecutive steps from it."""
-    eps = torch.randint(0, n_eps, (count, B), generator=gen)
-    start = torch.randint(0, EPISODE_STEPS - T + 1, (count, 1, 1), generator=gen)
-    idx = eps[:, None, :] * EPISODE_STEPS + start + torch.arange(T)[None, :, None]   # [count, T, B]
-    return idx.reshape(count, T * B).to(device)
+    out = torch.empty(count, T, B, dtype=torch.long)
+    for k in range(count):   # batch by batch, so the sequence does not depend on how it is chunked
+        eps = torch.randint(0, n_eps, (B,), generator=gen)
+        start = int(torch.randint(0, EPISODE_STEPS - T + 1, (1,), generator=gen))
+        out[k] = eps[None, :] * EPISODE_STEPS + start + torch.arange(T)[:, None]
+    return out.reshape(count, T * B).to(device)
 
 
 def fit_records(ob, t_pdflat, rew=None, *, student: str = "policy", steps: int = 250_000, loss: str = "mse",

@@ -90,7 +90,7 @@ def _random_states(n, seed=0):
     return np.stack([q0, q1, v0, v1, tx, ty, fx - tx, fy - ty])
 
 
-@pytest.mark.parametrize("n", [1, 255, 4096, 65537])
+@pytest.mark.parametrize("n", [1, 255, 4096, 4100, 65537])
 def test_step_matches_oracle_random(oracle_c, n):
     """One step from random states (limits active, |a| > 1 clamped) vs the C oracle."""
     from reacherdistilation_amd.env import BatchedReacher
@@ -205,3 +205,4 @@ def test_errors_are_loud():
         env.step(torch.zeros(8, 2, device=DEV))
     with pytest.raises(ValueError):
         env.step(torch.zeros(8, 3, device=DEV))
+

