@@ -30,6 +30,8 @@ draws use a seeded torch generator, not Python's ``random`` (page choice does us
 """
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import torch
 
 from .config import (EPISODE_STEPS, LSTM_BATCH_SIZE, OBSPACE_SHAPE, PDFLAT_SHAPE, STEPS_UNROLLED,
@@ -63,7 +65,9 @@ class DeviceDataset:
         self.pool_mode = pool
         self._pool = None                  # training pool [P, 50, REC] (reference training_data)
         self._pool_lens = None
-        self._page_cache = {}              # page path -> (records on the device, lengths)
+        self._page_cache = OrderedDict()   # page path -> (records on the device, lengths); LRU of PAGE_CACHE
+        self._bptt_pages = None            # the BPTT pool's borrowed pages (drawn once per emptied data_in_memory)
+        self._bptt_stale = True
         self._zeros = torch.zeros(PDFLAT_SHAPE, dtype=torch.float32, device=self.device)
         self._with = torch.tensor([[0.0], [1.0]], dtype=torch.float32, device=self.device)   # stepped with t / s
 
@@ -117,6 +121,7 @@ class DeviceDataset:
             if slots else []
         if not store.store(eps):
             self._mem_slots = []
+            self._bptt_stale = True   # the reference's data_in_memory (and the BPTT pool aliasing it) emptied
 
     def load_page(self, path: str) -> int:
         """Append a page's episodes (incomplete ones with their length) to the ring and to
@@ -136,11 +141,17 @@ class DeviceDataset:
         return min(self.num_total_episodes, self.capacity)
 
     # -- the training pool (reference training_data, dataset.py:164-182) -----------------
+    PAGE_CACHE = 15   # pages kept on the device: max(POOL_PAGES, BPTT_POOL_PAGES), least recently used evicted
+
     def _page_records(self, page):
-        if page not in self._page_cache:
+        if page in self._page_cache:
+            self._page_cache.move_to_end(page)
+        else:
             from .pages import episodes_to_records
             rec, lens = episodes_to_records(self.store.load(page), with_lengths=True)
             self._page_cache[page] = (torch.as_tensor(rec, dtype=torch.float32).to(self.device), list(map(int, lens)))
+            while len(self._page_cache) > self.PAGE_CACHE:
+                self._page_cache.popitem(last=False)
         return self._page_cache[page]
 
     def reset_training_data(self):
@@ -212,15 +223,17 @@ class DeviceDataset:
         driver carries the LSTM state from one window to the next (backup/lstm_bbpt.py:
         141-158).  Same tuple layout as training_batches().  Pool (dataset_bbpt.py:164-181):
         training_data IS data_in_memory there (the same list), so episodes flushed since are
-        drawn at once; the episodes of up to 15 random stored pages join it whenever
-        data_in_memory is empty (or no pool was built yet).  (The reference's alias also makes
-        those borrowed page episodes part of data_in_memory, so its next dump writes them into
-        the current page again; that duplication is not reproduced.)"""
+        drawn at once; the episodes of up to 15 random stored pages join it on the first call and
+        after every dump that emptied data_in_memory, and stay until the next such dump (the
+        borrowed episodes are then part of data_in_memory, so it is no longer empty).  (The
+        alias also makes its next dump write the borrowed episodes into the current page again;
+        that duplication is not reproduced.)"""
         if self.pool_mode == "ring":
             n = self.stored()
             src, lens = self.ring[:n], list(self.lens[:n])
         else:
-            if not self._mem_slots or getattr(self, "_bptt_pages", None) is None:
+            if self._bptt_pages is None or (self._bptt_stale and not self._mem_slots):
+                self._bptt_stale = False
                 self._bptt_pages = []
                 if self.store is not None and self.store.pages:
                     self._bptt_pages = [p for p in self.store.rand_pages(self.BPTT_POOL_PAGES)

@@ -129,3 +129,42 @@ def test_incomplete_episode_in_a_page_round_trips_with_its_length(tmp_path, gold
     back = DeviceDataset(capacity=8, device="cpu")
     assert back.load_page(store.curr_page) == 2 and back.lens[:2] == [50, 13]
     np.testing.assert_array_equal(back.ring[1, :13, :11].numpy(), ds.ring[1, :13, :11].numpy())
+
+
+def test_bptt_pool_pages_fixed_until_a_dump_empties_data_in_memory(tmp_path, golden):
+    """the BPTT variant's pool aliases data_in_memory (backup/dataset_bbpt.py:164-181),
+    so the pages it borrows stay until a dump empties data_in_memory -- not re-drawn per call."""
+    store = _store_with_pages(tmp_path, golden, 20, 1000)
+    ds = DeviceDataset(capacity=64, device="cpu", seed=5, store=pages.PageStore(str(tmp_path)))
+    list(ds.bptt_batches())
+    first = list(ds._bptt_pages)
+    assert 0 < len(first) <= DeviceDataset.BPTT_POOL_PAGES
+    for _ in range(5):                       # data_in_memory empty: the borrowed pages stay
+        list(ds.bptt_batches())
+        assert ds._bptt_pages == first
+    for i in range(MAX_CAPACITY):            # a full page -> the dump empties data_in_memory
+        _write(ds, _episode(golden, i, 1 + i))
+        ds.flush()
+        list(ds.bptt_batches())
+        assert ds._bptt_pages == first       # flushed episodes join; the pages do not change
+    ds.dump()
+    assert not ds._mem_slots
+    draws = []
+    for _ in range(3):
+        list(ds.bptt_batches())
+        draws.append(list(ds._bptt_pages))
+    assert draws[0] == draws[1] == draws[2]  # one new draw after the emptying dump
+    assert len(store.pages) == 20
+
+
+def test_page_cache_is_bounded(tmp_path, golden):
+    """The device page cache keeps the PAGE_CACHE most recently used pages."""
+    _store_with_pages(tmp_path, golden, 20, 1000)
+    st = pages.PageStore(str(tmp_path))
+    ds = DeviceDataset(capacity=64, device="cpu", store=st)
+    for page in st.pages:
+        ds._page_records(page)
+    assert len(ds._page_cache) == DeviceDataset.PAGE_CACHE
+    assert list(ds._page_cache) == list(st.pages)[-DeviceDataset.PAGE_CACHE:]
+    ds._page_records(list(st.pages)[-DeviceDataset.PAGE_CACHE])     # a hit moves it to the end
+    assert list(ds._page_cache)[-1] == list(st.pages)[-DeviceDataset.PAGE_CACHE]
