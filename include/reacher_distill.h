@@ -65,7 +65,10 @@ typedef struct {
     int32_t group_envs;      /* envs per producer/consumer group of the rollout: 0 = auto
                                 (64, or 32/16 when the batch cannot give every wave pair a
                                 64-env group); 16, 32 or 64 fixes it.  Changes only the
-                                order of the gradient's summation                         */
+                                order of the gradient's summation.  Auto also picks the
+                                helper-pair layout for a batch of at most two 16-env groups
+                                per CU (pairs 2, 3 of a workgroup run the teacher forwards
+                                of pairs 0, 1); a fixed size never does      */
 } rdd_config;
 
 /* Student precision.  RDD_DTYPE_F32: every product exact f32 (v_mfma_f32_16x16x4_f32).

@@ -406,6 +406,7 @@ __device__ __forceinline__ void mlp_forward(const float* L, const float* ob, int
 // Teacher and student forwards of one tile, interleaved layer by layer: 8 independent
 // accumulator chains per layer, and one net's tanh can issue behind the other's MFMAs.
 // Returns the student's hidden activations (needed by the backward) and both means.
+template <bool FENCE = false>
 __device__ __forceinline__ void mlp_forward_pair(const float* LT, const float* LS, const float* ob, int j, int g,
                                                  f32x4 (&H1)[4], f32x4 (&H2)[4], float& mt0, float& mt1,
                                                  float& ms0, float& ms1) {
@@ -420,11 +421,15 @@ __device__ __forceinline__ void mlp_forward_pair(const float* LT, const float* L
         const float zs = fminf(fmaxf((x - LS[N_MU + k]) * LS[N_RS + k], -5.0f), 5.0f);
         const f32x4 wt = ld4(LT + N_W1 + k * HID + 4 * j);
         const f32x4 ws = ld4(LS + N_W1 + k * HID + 4 * j);
+        fence_begin<FENCE>(at);
+        fence_begin<FENCE>(as);
 #pragma unroll
         for (int fb = 0; fb < 4; ++fb) {
             at[fb] = mfma(wt[fb], zt, at[fb]);
             as[fb] = mfma(ws[fb], zs, as[fb]);
         }
+        fence_end<FENCE>(at);
+        fence_end<FENCE>(as);
     }
     f32x4 T1[4];
 #pragma unroll
@@ -449,11 +454,15 @@ __device__ __forceinline__ void mlp_forward_pair(const float* LT, const float* L
                 wtn = ld4(LT + N_W2 + kn * HID + 4 * j);
                 wsn = ld4(LS + N_W2 + kn * HID + 4 * j);
             }
+            fence_begin<FENCE>(at);
+            fence_begin<FENCE>(as);
 #pragma unroll
             for (int fb = 0; fb < 4; ++fb) {
                 at[fb] = mfma(wt[fb], T1[kb][r], at[fb]);
                 as[fb] = mfma(ws[fb], H1[kb][r], as[fb]);
             }
+            fence_end<FENCE>(at);
+            fence_end<FENCE>(as);
         }
     float pt0 = 0.0f, pt1 = 0.0f, ps0 = 0.0f, ps1 = 0.0f;
 #pragma unroll
@@ -1004,24 +1013,30 @@ __global__ __launch_bounds__(256) void pack_net_kernel(const float* net, float* 
     for (int p = x; p < P_TOT; p += gridDim.x * 256) pack_param(img, p, net[p], student != 0, kind);
 }
 
-// Both rollout images (contiguous in LDS: teacher then student) by LDS-DMA: every 16-B piece is
-// one global_load_lds_dwordx4 (wave-uniform LDS base + lane x 16 B, per-lane global address), so
-// the copy needs no staging VGPRs and no ds_write pass.  `between` runs while they are in flight
-// (the producers' first observations; hipcc waits vmcnt(0) before it uses the state loads, so the
-// image has landed by then) and the caller's __syncthreads publishes the image.  Measured against
-// the register-staged copy it replaces (profiles/r04c_imgdma_ab.txt): c2 -0.3 us per step, c3
-// -0.3, c5 -0.2, c4 -0.2; that form is in profiles/r04_removed_diagnostic_variants.diff.
+// Both rollout images (contiguous in LDS: teacher then student) with every 16-B load of a
+// thread issued before its first LDS store, so a workgroup keeps ~3.7k loads in flight
+// instead of one round trip per loop iteration.
+// `between` runs while the loads are in flight (the producers' first observations).
+// An LDS-DMA fill (global_load_lds_dwordx4, no staging VGPRs) measured 0.2-0.3 us per step
+// faster but its build's c4 and grid-300 rollouts were not reproducible: the first rollout of a
+// process differed from the later ones in 1-3 dW3 entries owned by lanes 48-63 (6 of 18
+// repeats identical vs 18 of 18 with this copy; profiles/r04i_imgdma_nondeterminism.txt).
 template <int V4A, int V4B, int NT, class F>
 __device__ __forceinline__ void copy_images(float* L, const float* ta, const float* sb, F&& between) {
     constexpr int TOT = V4A + V4B, PER = (TOT + NT - 1) / NT;
-    const int wbase = threadIdx.x & ~63;
+    f32x4 r[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const int x = threadIdx.x + u * NT;
-        if (x < TOT)
-            __builtin_amdgcn_global_load_lds(x < V4A ? ta + 4 * x : sb + 4 * (x - V4A), L + 4 * (wbase + u * NT), 16, 0, 0);
+        if (x < V4A) r[u] = reinterpret_cast<const f32x4*>(ta)[x];
+        else if (x < TOT) r[u] = reinterpret_cast<const f32x4*>(sb)[x - V4A];
     }
     between();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int x = threadIdx.x + u * NT;
+        if (x < TOT) reinterpret_cast<f32x4*>(L)[x] = r[u];
+    }
 }
 
 // bf16-student forward of a 16-env tile (same outputs/layouts as mlp_forward).
@@ -1183,10 +1198,15 @@ static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NETB_S
 
 // BS: bf16 student (RDD_DTYPE_BF16); SPL: split-bf16 f32 hidden layers; CP: the consumer wave
 // steps the envs (else the producer does, from the state it loaded for the observations);
-// TGT: observation rows with their recorded teacher pdflat (a.tflat_in), no teacher network
-// (no teacher image in LDS), no env step -- distill_rows_kernel
-template <bool BS, bool SPL, bool CP, bool TGT>
+// MD: MD_TEACHER the teacher network is queried; MD_ROWS observation rows with their recorded
+// teacher pdflat (a.tnet), no teacher network (no teacher image in LDS); MD_HELPER (f32
+// student, one 16-env tile per pair's group, launch_rollout): pairs 0, 1 own the groups and
+// pairs 2, 3 run their tiles' teacher forwards on the other two SIMDs
+constexpr int MD_TEACHER = 0, MD_ROWS = 1, MD_HELPER = 2;
+template <bool BS, bool SPL, bool CP, int MD>
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
+    constexpr bool TGT = MD == MD_ROWS, HLP = MD == MD_HELPER;
+    static_assert(!HLP || !BS, "helper pairs: f32 student kernels only");
     constexpr int TN = TGT ? 0 : img_t(SPL), SN = img_s(BS, SPL);
     __shared__ __attribute__((aligned(16))) float lds[TN + SN + PAIRS * PSCR];
     float* LT = lds;
@@ -1204,8 +1224,18 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     // 32-bit group / env indices (n <= 2^31, rdd_create): fewer SGPRs live across the loops
     const uint32_t n32 = (uint32_t)a.n;
     const uint32_t ngroups = (n32 + (uint32_t)gs - 1) / (uint32_t)gs;
-    const uint32_t gstride = gridDim.x * PAIRS;
-    const uint32_t gfirst = blockIdx.x * PAIRS + pair;
+    // HLP: the owner pairs 0, 1 take the groups (one each), pairs 2, 3 none (they help).  The
+    // layout holds at most one group per owner (launch_rollout): a launch that breaks this ends
+    // at once with the hand-off error raised (rdd_counter reports it)
+    if constexpr (HLP) {
+        if (ngroups > 2u * gridDim.x) {
+            if (threadIdx.x == 0) __hip_atomic_store(a.ctl + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    const bool helper = HLP && pair >= 2;
+    const uint32_t gstride = gridDim.x * (HLP ? 2 : PAIRS);
+    const uint32_t gfirst = helper ? ngroups : blockIdx.x * (HLP ? 2 : PAIRS) + pair;
     // a producer's first group of envs: its state loads are issued before the image copy so
     // that their HBM latency overlaps the prologue
     rd::State st0{};
@@ -1262,6 +1292,28 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         uint32_t tiles = 0;
         uint32_t k = 0;
         bool ok = true;
+        // HLP helper (pair 2 + o): the teacher forward of owner o's first tile (its observations
+        // were formed in the prologue, before the barrier), means into this pair's P_ACT, flag [0]
+        if constexpr (HLP) {
+            const uint32_t og = blockIdx.x * 2 + (pair & 1);
+            if (helper && og < ngroups) {
+                STAMP(18);
+                const float* oobs = lds + TN + SN + (pair & 1) * PSCR + P_SO;
+                float m0, m1;
+                if constexpr (SPL) {
+                    mlp_forward_split(LT, oobs, j, g, m0, m1);
+                } else {
+                    f32x4 h1[4], h2[4];
+                    mlp_forward<true>(LT, oobs, j, g, h1, h2, m0, m1);
+                }
+                if (g == 0) {
+                    PS[P_ACT + 2 * j] = m0;
+                    PS[P_ACT + 2 * j + 1] = m1;
+                }
+                publish(flags, 1u);
+                STAMP(19);
+            }
+        }
         for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
             STAMP(8);
             const uint32_t base = grp * (uint32_t)gs;
@@ -1300,6 +1352,20 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     rl1 = tq[3];
                     rr0 = 1.0f / __expf(2.0f * rl0);
                     rr1 = 1.0f / __expf(2.0f * rl1);
+                } else if constexpr (HLP) {
+                    if (k == 0) {
+                        // owner: the student's forward of its tile; the teacher's comes from the
+                        // helper pair on another SIMD (gs = 16: one tile, t = 0)
+                        if constexpr (SPL) mlp_forward_split_t<true>(LS, obt, j, g, H1, H2, ms0, ms1);
+                        else mlp_forward<true>(LS, obt, j, g, H1, H2, ms0, ms1);
+                        const float* hp = lds + TN + SN + (pair + 2) * PSCR;
+                        if (!(ok = wait_ge(reinterpret_cast<const uint32_t*>(hp + P_FLAGS), 1u, err))) break;
+                        mt0 = hp[P_ACT + 2 * j];
+                        mt1 = hp[P_ACT + 2 * j + 1];
+                    } else {   // later groups (not launched in this layout): both forwards here
+                        if constexpr (SPL) mlp_forward_pair_split(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                        else mlp_forward_pair<true>(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                    }
                 } else if constexpr (BS) {
                     // CP: in this kernel's schedule the compiler issues loads into the SrcC
                     // registers of the exact teacher's f32 MFMAs: fenced (see mfma())
@@ -1522,12 +1588,14 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 // db2 partials and dW2 += H1^T dZ2 over the tile's 16 envs (K = env)
                 bf16x8 dpre[2][3];   // split: the dH1 operand pieces, made before the dW2 MFMAs
                 if constexpr (S2) {
+                    if constexpr (!HLP) {   // HLP: the helper pair's consumer takes dW2 and db2
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) gb2[b] += (y[b][0] + y[b][1]) + (y[b][2] + y[b][3]);
+                        for (int b = 0; b < 4; ++b) gb2[b] += (y[b][0] + y[b][1]) + (y[b][2] + y[b][3]);
+                    }
                     split8(dZ[0], dZ[1], dpre[0]);
                     split8(dZ[2], dZ[3], dpre[1]);
-                    dw2_split(x, y, gW2);
-                } else {
+                    if constexpr (!HLP) dw2_split(x, y, gW2);
+                } else if constexpr (!HLP) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
 #pragma unroll
@@ -1637,6 +1705,54 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 STAMP(5);
             }
         };
+        if constexpr (HLP) {
+            // helper pair 2 + o: dW2 = H1^T dZ2 and db2 of owner o's tile, read from the owner's
+            // slot beside the owner consumer's dH1 / dW1 (the owner's producer never rewrites the
+            // slot: one tile per owner in this layout)
+            const uint32_t og = blockIdx.x * 2 + (pair & 1);
+            if (helper && og < ngroups) {
+                const float* OP = lds + TN + SN + (pair & 1) * PSCR;
+                STAMP(20);
+                ok = wait_ge(reinterpret_cast<const uint32_t*>(OP + P_FLAGS), 1u, err);
+                STAMP(21);
+                if (ok) {
+                    const float* h1t = OP + P_H1T;
+                    const float* dzt = OP + P_DZT;
+                    float x[4][4], y[4][4];
+#pragma unroll
+                    for (int s = 0; s < 4; ++s)
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            if constexpr (SPL) {
+                                x[b][s] = h1t[(4 * g + s) * SAS + 16 * b + j];
+                                y[b][s] = dzt[(4 * g + s) * SAS + 16 * b + j];
+                            } else {
+                                x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];
+                                y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];
+                            }
+                        }
+                    if constexpr (SPL) {
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) gb2[b] += (y[b][0] + y[b][1]) + (y[b][2] + y[b][3]);
+                        dw2_split(x, y, gW2);
+                    } else {
+#pragma unroll
+                        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) gb2[b] += y[s][b];
+#pragma unroll
+                            for (int mb = 0; mb < 4; ++mb) {
+                                fence_begin<true>(gW2[mb]);
+#pragma unroll
+                                for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma(x[s][mb], y[s][nb], gW2[mb][nb]);
+                                fence_end<true>(gW2[mb]);
+                            }
+                        }
+                    }
+                }
+                STAMP(22);
+            }
+        }
         for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride) {
             const uint32_t base = grp * (uint32_t)gs;
             const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
@@ -1910,12 +2026,22 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
         a.gs = group_envs(n_obs, t->ws_rows * PAIRS, t->cfg.group_envs);
         grid = grid_for(n_obs, a.gs, t->ws_rows);
     }
-    t->last_grid = grid;
     const bool bs = t->cfg.student_dtype == RDD_DTYPE_BF16, spl = t->cfg.f32_split != 0;
-    void (*k)(RolloutArgs) = bs ? (spl ? rollout_kernel<true, true, true, false> : rollout_kernel<true, false, true, false>)
-                                : (spl ? rollout_kernel<false, true, false, false> : rollout_kernel<false, false, false, false>);
+    // helper pairs (f32 student): every group one 16-env tile and at most two groups per
+    // workgroup -- the batch would leave half the pairs idle or hold one tile each, so pairs 2,
+    // 3 run the owners' teacher forwards on the other SIMDs instead (c2: DESIGN.md §3)
+    const int64_t ngroups = (a.n + a.gs - 1) / a.gs;
+    const bool hlp = !bs && !tflat_in && a.gs == TILE && ngroups <= 2 * (int64_t)t->ws_rows &&
+                     t->cfg.group_envs == 0;   // a fixed group size keeps the plain layout
+    if (hlp) grid = (int)((ngroups + 1) / 2);
+    t->last_grid = grid;
+    void (*k)(RolloutArgs) =
+        bs ? (spl ? rollout_kernel<true, true, true, MD_TEACHER> : rollout_kernel<true, false, true, MD_TEACHER>)
+           : hlp ? (spl ? rollout_kernel<false, true, false, MD_HELPER> : rollout_kernel<false, false, false, MD_HELPER>)
+                 : (spl ? rollout_kernel<false, true, false, MD_TEACHER> : rollout_kernel<false, false, false, MD_TEACHER>);
     if (tflat_in)   // the teacher is not run: the bf16 student's kernel does not depend on the teacher's mode
-        k = bs ? rollout_kernel<true, false, false, true> : (spl ? rollout_kernel<false, true, false, true> : rollout_kernel<false, false, false, true>);
+        k = bs ? rollout_kernel<true, false, false, MD_ROWS>
+               : (spl ? rollout_kernel<false, true, false, MD_ROWS> : rollout_kernel<false, false, false, MD_ROWS>);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rollout_kernel launch");
     return RD_OK;

@@ -10,6 +10,9 @@ import numpy as np
 
 CASES = {   # name: DistillConfig overrides
     "c2": dict(n_envs=4096),
+    "c2_g16": dict(n_envs=4096, group_envs=16),   # the plain layout at c2 (auto picks helper pairs)
+    "c2_exact": dict(n_envs=4096, f32_split=False),
+    "small_777": dict(n_envs=777, loss="kl"),
     "c4": dict(n_envs=262144),
     "c5": dict(n_envs=131072, act_with="student", student_dtype="bf16"),
     "ragged_5003": dict(n_envs=5003, loss="kl"),

@@ -24,7 +24,8 @@ CASES = {"c4s": dict(n_envs=262144, f32_split=True), "c4e": dict(n_envs=262144, 
          "c5": dict(n_envs=131072, act_with="student", student_dtype="bf16", f32_split=True),
          "c5e": dict(n_envs=131072, act_with="student", student_dtype="bf16", f32_split=False),
          "c2s": dict(n_envs=4096, f32_split=True), "c2e": dict(n_envs=4096, f32_split=False),
-         "c3s": dict(n_envs=65536, loss="kl", f32_split=True)}
+         "c3s": dict(n_envs=65536, loss="kl", f32_split=True),
+         "grid300": dict(n_envs=300 * 4 * 64, grid=300, f32_split=True)}
 for name in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["c4s", "c4e"]):
     kw = CASES[name]
     ref = roll(**kw)

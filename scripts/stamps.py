@@ -48,6 +48,14 @@ def main():
     widx = np.flatnonzero(active) % 8
     st = st[active]
     prod = widx < 4
+    # RD_OWNERS=1 (the helper-pair layout of a small batch): the role statistics over
+    # the owner pairs 0, 1; the helper producers' teacher forwards are stamps 18 -> 19 (waves 2, 3),
+    # the helper consumers' dW2 wait / dW2 are 20 -> 21 -> 22 (waves 6, 7)
+    owners = os.environ.get("RD_OWNERS") == "1"
+    hp, hc = (widx == 2) | (widx == 3), (widx == 6) | (widx == 7)
+    if owners:
+        prod = (widx == 0) | (widx == 1)
+    cons = ((widx == 4) | (widx == 5)) if owners else ~prod
 
     def d(a, b, sel=None):
         v = (st[:, b] - st[:, a]) / iters
@@ -65,11 +73,15 @@ def main():
         "producer_fwd_tiles": d(10, 12, prod),
         "producer_wait": d(2, 3, prod),
         "producer_physics": d(4, 5, prod),
-        "consumer_physics": d(4, 5, ~prod),
-        "consumer_wait": d(2, 3, ~prod),
-        "consumer_slot_read": d(3, 13, ~prod),
-        "consumer_dw2_dh1": d(13, 14, ~prod),
-        "consumer_dz1_dw1": d(14, 15, ~prod),
+        "consumer_physics": d(4, 5, cons),
+        "consumer_wait": d(2, 3, cons),
+        "consumer_slot_read": d(3, 13, cons),
+        "consumer_dw2_dh1": d(13, 14, cons),
+        "consumer_dz1_dw1": d(14, 15, cons),
+        "helper_teacher_start": d(0, 18, hp) if owners else None,
+        "helper_teacher_fwd": d(18, 19, hp) if owners else None,
+        "helper_dw2_wait": d(20, 21, hc) if owners else None,
+        "helper_dw2": d(21, 22, hc) if owners else None,
         "epilogue_barrier_wait": d(6, 9),
         "epilogue_reduce": d(9, 7),
         # per wave slot (0-3 dispatched first; w and w+4 share a SIMD): time to reach the epilogue

@@ -41,14 +41,16 @@ def test_product_library_reads_no_environment(libpath):
 
 def test_consumer_side_step_only_for_the_bf16_student(libpath):
     blob = open(libpath, "rb").read()
-    names = set(re.findall(rb"rollout_kernelILb[01]ELb[01]ELb[01]ELb[01]E", blob))
+    names = set(re.findall(rb"rollout_kernelILb[01]ELb[01]ELb[01]ELi[0-9]E", blob))
     assert names, "rollout_kernel instantiations not found in the offload bundle"
-    # <bf16 student, f32 mode, consumer-side step, rows mode>: f32 student -> producer-side,
-    # bf16 -> consumer-side; rows mode (no env step) -> no consumer-side step, no teacher
-    assert names == {b"rollout_kernelILb0ELb0ELb0ELb0E", b"rollout_kernelILb0ELb1ELb0ELb0E",
-                     b"rollout_kernelILb1ELb0ELb1ELb0E", b"rollout_kernelILb1ELb1ELb1ELb0E",
-                     b"rollout_kernelILb0ELb0ELb0ELb1E", b"rollout_kernelILb0ELb1ELb0ELb1E",
-                     b"rollout_kernelILb1ELb0ELb0ELb1E"}, sorted(names)
+    # <bf16 student, f32 mode, consumer-side step, MD>: f32 student -> producer-side, bf16 ->
+    # consumer-side; MD 1 (rows: no env step) -> no consumer-side step, no teacher; MD 2 (helper
+    # pairs of a small batch) -> f32 student only
+    assert names == {b"rollout_kernelILb0ELb0ELb0ELi0E", b"rollout_kernelILb0ELb1ELb0ELi0E",
+                     b"rollout_kernelILb1ELb0ELb1ELi0E", b"rollout_kernelILb1ELb1ELb1ELi0E",
+                     b"rollout_kernelILb0ELb0ELb0ELi1E", b"rollout_kernelILb0ELb1ELb0ELi1E",
+                     b"rollout_kernelILb1ELb0ELb0ELi1E",
+                     b"rollout_kernelILb0ELb0ELb0ELi2E", b"rollout_kernelILb0ELb1ELb0ELi2E"}, sorted(names)
 
 
 def _hz():
@@ -87,8 +89,9 @@ def test_no_load_into_an_inflight_f32_mfma_srcc(product_isa):
     within the scan at all (their f32 MFMAs are dW1 only)."""
     hz = _hz()
     out = product_isa["distill.hip"]
-    for sym, split in (("rollout_kernelILb0ELb0ELb0ELb0E", False), ("rollout_kernelILb0ELb1ELb0ELb0E", True),
-                       ("rollout_kernelILb1ELb0ELb1ELb0E", False), ("rollout_kernelILb1ELb1ELb1ELb0E", True)):
+    for sym, split in (("rollout_kernelILb0ELb0ELb0ELi0E", False), ("rollout_kernelILb0ELb1ELb0ELi0E", True),
+                       ("rollout_kernelILb1ELb0ELb1ELi0E", False), ("rollout_kernelILb1ELb1ELb1ELi0E", True),
+                       ("rollout_kernelILb0ELb0ELb0ELi2E", False), ("rollout_kernelILb0ELb1ELb0ELi2E", True)):
         hits = [h for h in hz.scan(out, sym, 40)[0] if h[0] == "LDSRC" and "16x16x4" in h[4]]
         assert all(h[1] >= 10 for h in hits), (sym, [h[:6] for h in hits if h[1] < 10][:5])
         if split:
