@@ -1241,6 +1241,14 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     rd::State st0{};
     if (producer && !a.obs_in && gfirst < ngroups && lane < gs && gfirst * gs + lane < a.n)
         load_state(a.state, a.n, (uint32_t)(gfirst * gs + lane), st0);
+    // HLP with the teacher acting: the helper producer steps its owner's envs (below), so it loads
+    // their state here instead of the owner
+    const uint32_t og = blockIdx.x * 2 + (pair & 1);   // HLP: the owner group a helper serves
+    const bool hstep = helper && producer && !a.obs_in && !a.act_student;
+    if constexpr (HLP) {
+        if (hstep && og < ngroups && lane < gs && og * gs + lane < a.n)
+            load_state(a.state, a.n, (uint32_t)(og * gs + lane), st0);
+    }
     static_assert(NET % 4 == 0 && NET_S % 4 == 0, "16-B images");
     // ... and its observations are formed (into obs buffer 0) while the image loads are in flight
     float* PS = lds + TN + SN + pair * PSCR;
@@ -1295,7 +1303,6 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         // HLP helper (pair 2 + o): the teacher forward of owner o's first tile (its observations
         // were formed in the prologue, before the barrier), means into this pair's P_ACT, flag [0]
         if constexpr (HLP) {
-            const uint32_t og = blockIdx.x * 2 + (pair & 1);
             if (helper && og < ngroups) {
                 STAMP(18);
                 const float* oobs = lds + TN + SN + (pair & 1) * PSCR + P_SO;
@@ -1312,6 +1319,13 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 }
                 publish(flags, 1u);
                 STAMP(19);
+                // ... and, with the teacher acting, steps the owner's envs with these means (lane
+                // j < 16 holds env j's): the owner's producer skips its env step
+                if (hstep && lane < gs) {
+                    const uint32_t i = og * (uint32_t)gs + (uint32_t)lane;
+                    met_r += env_step_group(a, C, i, i < n32, m0, m1, st0, met_n);
+                }
+                STAMP(23);
             }
         }
         for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
@@ -1445,6 +1459,8 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             if constexpr (!CP) {
                 if (a.obs_in) {   // observation-batch mode: no env to step
                     if (lvalid) met_n += 1.0f;
+                } else if (HLP && k == 0 && !a.act_student) {
+                    // the helper pair steps these envs (above)
                 } else {
                     wave_sync();   // act[] rows were written by the g = 0 lanes of each tile
                     if (lane < gs) met_r += env_step_group(a, C, i, lvalid, act[lane * 2], act[lane * 2 + 1], st, met_n);
@@ -1709,7 +1725,6 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             // helper pair 2 + o: dW2 = H1^T dZ2 and db2 of owner o's tile, read from the owner's
             // slot beside the owner consumer's dH1 / dW1 (the owner's producer never rewrites the
             // slot: one tile per owner in this layout)
-            const uint32_t og = blockIdx.x * 2 + (pair & 1);
             if (helper && og < ngroups) {
                 const float* OP = lds + TN + SN + (pair & 1) * PSCR;
                 STAMP(20);

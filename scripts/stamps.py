@@ -80,6 +80,7 @@ def main():
         "consumer_dz1_dw1": d(14, 15, cons),
         "helper_teacher_start": d(0, 18, hp) if owners else None,
         "helper_teacher_fwd": d(18, 19, hp) if owners else None,
+        "helper_env_step": d(19, 23, hp) if owners else None,
         "helper_dw2_wait": d(20, 21, hc) if owners else None,
         "helper_dw2": d(21, 22, hc) if owners else None,
         "epilogue_barrier_wait": d(6, 9),

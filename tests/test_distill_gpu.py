@@ -332,6 +332,39 @@ def test_group_size_changes_only_the_summation_order():
         assert np.abs(g - g16).max() <= 1e-5 * np.abs(g16).max()
 
 
+@pytest.mark.parametrize("n", [4096, 777, 8192])
+@pytest.mark.parametrize("split,loss,act", [(True, "mse", "teacher"), (False, "mse", "teacher"),
+                                            (True, "kl", "teacher"), (True, "mse", "student"),
+                                            (False, "kl", "student")])
+def test_helper_layout_matches_the_plain_layout(n, split, loss, act):
+    """The helper-pair layout (automatic for <= two 16-env groups per CU: pairs 2, 3 of a
+    workgroup run pairs 0, 1's teacher forwards, weight gradient dW2 and -- teacher acting --
+    env steps) against the plain layout (group_envs = 16 fixed), one fused step: the env states
+    bitwise where the owner steps them (student acting) and within an ulp where the helper does
+    (the same rd::env_step inlined into another wave's code: r04 measured 1.19e-7 at most, in ~29 %
+    of the envs), the gradient to f32 reordering of the sums (the partial rows group the envs
+    differently), the Adam update where the gradient is not ~0, the step's metrics."""
+    out = {}
+    for gs in (0, 16):
+        tr = _trainer(n, loss=loss, act=act, f32_split=split, group_envs=gs, seed=5)
+        tr.step()
+        out[gs] = (tr.grad().cpu().numpy().astype(np.float64), tr.env_state().cpu().numpy(),
+                   tr.student_params().cpu().numpy().astype(np.float64), tr.metrics(1))
+        tr.close()
+    (gh, sh, ph, mh), (gp, spl, pp, mp) = out[0], out[16]
+    nd = int((sh != spl).any(0).sum())
+    print(f"helper vs plain n={n} split={split} {loss} {act}: {nd} envs differ, max {np.abs(sh - spl).max():.3g}")
+    if act == "student":   # the owner steps its envs in both layouts: bitwise
+        assert nd == 0
+    else:                  # the helper's inlined env step: measured <= 1.19e-7 (1 ulp of |x| < 1)
+        np.testing.assert_allclose(sh, spl, atol=2.5e-7, rtol=2e-7)
+    assert np.abs(gh - gp).max() <= 1e-5 * np.abs(gp).max()
+    strong = np.abs(gp) > 1e-3 * np.abs(gp).max()
+    assert np.abs(ph - pp)[strong].max() <= 1e-6
+    assert mh[0, 3] == mp[0, 3] == n                               # envs stepped
+    np.testing.assert_allclose(mh[0, :3], mp[0, :3], rtol=1e-5, atol=1e-7)
+
+
 def _limit_states(n, rs):
     """Env states where the joint-1 limit (|q1| = 3) is active in every RK stage for half of
     the envs (|q1| in [3.05, 3.3], moving outward or inward slowly) and inactive in every stage
@@ -401,12 +434,13 @@ def _null_state(n):
     return np.array([q0, q1, v0, v1, tx, ty, dx, dy], np.float32)
 
 
-@pytest.mark.parametrize("n,gs", [(64, 64), (64, 16), (128, 32)])
+@pytest.mark.parametrize("n,gs", [(64, 64), (64, 16), (128, 32), (64, 0), (128, 0)])
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("loss", ["mse", "kl"])
 def test_each_env_contribution_isolated(n, gs, split, loss):
     """Every env of a small batch, i.e. every lane 0..63 of a 64-env group (and of 16- / 32-env
-    groups), owns one env; its contribution to every gradient entry is isolated as
+    groups; gs = 0: the automatic choice, the helper-pair layout at these sizes), owns one env;
+    its contribution to every gradient entry is isolated as
     g(batch) - g(batch with env e replaced by a fixed env z) = c(x_e) - c(z) and compared with
     the oracle's per entry: |error| <= 1e-5 x (M(x_e) + M(z)) + 5e-6 x M(batch) (the second term:
     the f32 round-off of the two batch sums; measured r04a: worst error 0.014 of the round's first,
