@@ -90,15 +90,20 @@ def student_init(seed: int = 2) -> MlpPolicyParams:
 class TeacherAgent:
     """Mirror of reference teacher.py:12-20: holds ``pi`` (the MlpPolicy parameters).
 
-    ``restore`` loads a safetensors file with the flat params + filter if a path is given
-    (the reference restores a TF checkpoint we do not have); otherwise the synthetic
-    teacher is used."""
+    ``restore`` with a path loads either the reference's own TF checkpoint (``path`` is the
+    Saver prefix, e.g. ".../teacher.ckpt" with its ``.index`` / ``.data-*`` files:
+    tf_checkpoint.load_teacher) or a ``.safetensors`` file with the flat params + filter;
+    otherwise the synthetic teacher is used."""
 
     def __init__(self, env=None, sess=None, restore=False, batch=1, seed: int = 1, path: str | None = None):
         if restore and path:
-            from safetensors.numpy import load_file
-            d = load_file(path)
-            self.pi = MlpPolicyParams(d["flat"].astype(np.float32), d["ob_mean"], d["ob_std"])
+            from . import tf_checkpoint
+            if tf_checkpoint.exists(path):
+                self.pi = tf_checkpoint.load_teacher(path)
+            else:
+                from safetensors.numpy import load_file
+                d = load_file(path)
+                self.pi = MlpPolicyParams(d["flat"].astype(np.float32), d["ob_mean"], d["ob_std"])
         else:
             self.pi = synthetic_teacher(seed)
         self.batch = batch
