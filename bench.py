@@ -214,7 +214,11 @@ def copy_ceiling(gib=1.0, reps=20):
     for v, blocks in ((1, 65536), (2, 65536), (3, 0), (4, 0), (5, 0), (6, 0)):
         res[lib.copy_bw_name(v).decode()] = 1e3 * lib.copy_bw_tbs(nbytes, v, blocks, reps)   # GB/s
     best = max(res, key=res.get)
+    # the env step's own read:write mix (40 B read : 73 B written ~ 1 : 2), 16-B streaming
+    mix = {lib.copy_bw_name(v).decode(): 1e3 * lib.copy_bw_tbs(nbytes, v, 0, reps) for v in (7, 8)}
+    mbest = max(mix, key=mix.get)
     return {"best_gbs": res[best], "best": best, "variants_gbs": res, "bytes": nbytes,
+            "mix_1r2w_best_gbs": mix[mbest], "mix_1r2w_best": mbest, "mix_1r2w_gbs": mix,
             "source": "scripts/micro/copy_bw.hip (libcopybw.so), this run"}
 
 
@@ -861,6 +865,7 @@ def main():
         if ceil is not None:   # the float4 copy measured in this run
             out["roofline_env"]["copy_ceiling"] = ceil
             out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / ceil["best_gbs"]
+            out["roofline_env"]["frac_of_measured_mix"] = out["roofline_env"]["achieved"] / ceil["mix_1r2w_best_gbs"]
         else:
             out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / copy_gbs
             out["roofline_env"]["copy_ceiling"] = "torch copy_ (scripts/micro/libcopybw.so not built)"

@@ -36,6 +36,33 @@ __global__ __launch_bounds__(256) void copy4_kernel(const f32x4* __restrict__ sr
     }
 }
 
+// the env kernel's read:write mix (40 B read, 73 B written per env-step ~ 1 : 2): block b reads
+// float4s [b * 256 * U, ...) of src once and writes each twice, to dst[i] and dst[n + i] (dst
+// holds 2n float4s); bytes counted = 3 x 16 B per source float4
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void mix12_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst, size_t n) {
+    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < n) v[u] = NT ? __builtin_nontemporal_load(src + i) : src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < n) {
+            if (NT) {
+                __builtin_nontemporal_store(v[u], dst + i);
+                __builtin_nontemporal_store(v[u], dst + n + i);
+            } else {
+                dst[i] = v[u];
+                dst[n + i] = v[u];
+            }
+        }
+    }
+}
+
 template <typename F>
 static double timed(F&& launch, size_t bytes, int reps) {
     hipEvent_t e0, e1;
@@ -54,7 +81,8 @@ static double timed(F&& launch, size_t bytes, int reps) {
 }
 
 // variant: 0 = grid-stride 4 B, 1 = 8 B, 2 = 16 B (`blocks` workgroups); 3 = one-shot float4
-// x4 per lane, 4 = the same non-temporal, 5 = one-shot x8, 6 = x8 non-temporal
+// x4 per lane, 4 = the same non-temporal, 5 = one-shot x8, 6 = x8 non-temporal, 7 / 8 = the
+// 1 : 2 read:write mix (mix12_kernel), non-temporal / plain
 static double run(void* a, void* b, size_t bytes, int variant, int blocks, int reps) {
     const size_t n4 = bytes / 16;
     switch (variant) {
@@ -65,12 +93,17 @@ static double run(void* a, void* b, size_t bytes, int variant, int blocks, int r
         case 4: return timed([&] { hipLaunchKernelGGL((copy4_kernel<4, true>), dim3((n4 + 1023) / 1024), dim3(256), 0, 0, (const f32x4*)a, (f32x4*)b, n4); }, bytes, reps);
         case 5: return timed([&] { hipLaunchKernelGGL((copy4_kernel<8, false>), dim3((n4 + 2047) / 2048), dim3(256), 0, 0, (const f32x4*)a, (f32x4*)b, n4); }, bytes, reps);
         case 6: return timed([&] { hipLaunchKernelGGL((copy4_kernel<8, true>), dim3((n4 + 2047) / 2048), dim3(256), 0, 0, (const f32x4*)a, (f32x4*)b, n4); }, bytes, reps);
+        // read:write 1:2 over a third of the buffer as source (timed() counts 2 x bytes; the
+        // mix moves 3 x bytes / 3 read + 2 x bytes / 3 written = the same total)
+        case 7: { const size_t m = n4 / 3; return timed([&] { hipLaunchKernelGGL((mix12_kernel<4, true>), dim3((m + 1023) / 1024), dim3(256), 0, 0, (const f32x4*)a, (f32x4*)b, m); }, m * 16 * 3 / 2, reps); }
+        case 8: { const size_t m = n4 / 3; return timed([&] { hipLaunchKernelGGL((mix12_kernel<4, false>), dim3((m + 1023) / 1024), dim3(256), 0, 0, (const f32x4*)a, (f32x4*)b, m); }, m * 16 * 3 / 2, reps); }
         default: return -1.0;
     }
 }
 
 static const char* kName[] = {"grid-stride 4B", "grid-stride 8B", "grid-stride 16B", "one-shot 16B x4",
-                              "one-shot 16B x4 nt", "one-shot 16B x8", "one-shot 16B x8 nt"};
+                              "one-shot 16B x4 nt", "one-shot 16B x8", "one-shot 16B x8 nt",
+                              "read 1 : write 2, 16B x4 nt", "read 1 : write 2, 16B x4"};
 
 #ifdef COPY_BW_LIB
 extern "C" {
@@ -89,7 +122,7 @@ double copy_bw_tbs(size_t bytes, int variant, int blocks, int reps) {
     (void)hipFree(b);
     return t;
 }
-const char* copy_bw_name(int variant) { return variant >= 0 && variant < 7 ? kName[variant] : ""; }
+const char* copy_bw_name(int variant) { return variant >= 0 && variant < 9 ? kName[variant] : ""; }
 }
 #else
 int main() {
@@ -102,7 +135,7 @@ int main() {
         for (int v = 0; v < 3; ++v)
             printf("{\"access\": \"%s\", \"blocks\": %d, \"bytes\": %zu, \"TB_per_s\": %.3f}\n", kName[v], blocks, bytes,
                    run(a, b, bytes, v, blocks, 20));
-    for (int v = 3; v < 7; ++v)
+    for (int v = 3; v < 9; ++v)
         printf("{\"access\": \"%s\", \"bytes\": %zu, \"TB_per_s\": %.3f}\n", kName[v], bytes, run(a, b, bytes, v, 0, 20));
     (void)hipFree(a);
     (void)hipFree(b);
