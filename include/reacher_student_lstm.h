@@ -9,10 +9,13 @@
  *                                                             [x_t, h_{t-1}] . Wl + bl,
  *                                                             forget_bias 1, tanh
  *     pdflat_t = dense(tanh dense 32(tanh dense 64(tanh dense 128(tanh dense 64(h_t))))), 4)
- * Flat parameters (RDL_PARAMS = 227,012 floats) in variable-creation order, each kernel
- * W[in][out] row-major then its bias:
- *     Wp[4][32] bp | Wl[243][800] bl | W1[200][64] b1 | W2[64][128] b2 | W3[128][64] b3 |
- *     W4[64][32] b4 | W5[32][4] b5
+ * with ONE HEAD PER UNROLLED STEP: the reference calls tf.layers.dense inside its Python loop
+ * over the T steps without reuse (student_nn.py:40-47), so step t's five layers are their own
+ * variables (dense_{5t+1} .. dense_{5t+5}); the LSTMCell and the prev-pdflat dense are shared.
+ * Flat parameters (RDL_PARAMS_T(T) floats; RDL_PARAMS at the reference's T = 10) in
+ * variable-creation order, each kernel W[in][out] row-major then its bias:
+ *     Wp[4][32] bp | Wl[243][800] bl | head_0 | ... | head_{T-1},
+ *     head_t = W1[200][64] b1 | W2[64][128] b2 | W3[128][64] b3 | W4[64][32] b4 | W5[32][4] b5
  * Tensors: ob [T][B][11], prev_pdflat [T][B][4], t_pdflat / pdflat [T][B][4], LSTM state
  * [2][B][200] = (c, m) as the reference's initial_state_batch_ph (lstm_train.py:51).
  * Loss: kl_loss summed over T and B (loss.py:3-13), or action-MSE over T x rows_global.
@@ -32,7 +35,10 @@
 extern "C" {
 #endif
 
-#define RDL_PARAMS 227012
+#define RDL_CELL_PARAMS 195360                                   /* Wp bp Wl bl          */
+#define RDL_HEAD_PARAMS 31652                                    /* one step's head      */
+#define RDL_PARAMS_T(T) (RDL_CELL_PARAMS + (T) * RDL_HEAD_PARAMS)
+#define RDL_PARAMS RDL_PARAMS_T(10)                              /* 511,880              */
 #define RDL_UNITS 200
 #define RDL_LOSS_MSE 0
 #define RDL_LOSS_KL 1
@@ -61,17 +67,18 @@ typedef struct {
 
 typedef struct rdl_trainer rdl_trainer;
 
-int rdl_param_count(void);
+/* flat parameters of a trainer with `steps` unrolled steps (RDL_PARAMS_T(steps)), -1 if steps <= 0 */
+int64_t rdl_param_count(int32_t steps);
 /* the 'LSTM' scope: graph, kl_loss and Adam (lstm_train.py:35-79) */
 int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_stream);
 int rdl_destroy(rdl_trainer* t);
 int rdl_set_stream(rdl_trainer* t, void* hip_stream);
-/* initialisation / saver.restore (lstm_train.py:82-107): params [RDL_PARAMS] */
+/* initialisation / saver.restore (lstm_train.py:82-107): params [RDL_PARAMS_T(steps)] */
 int rdl_set_params(rdl_trainer* t, const float* params);
 int rdl_get_params(rdl_trainer* t, float* params);
 /* Adam slots, beta powers, step counter to zero (lstm_train.py:99) */
 int rdl_reset(rdl_trainer* t);
-/* the Adam slots m, v [RDL_PARAMS] (device pointers): with the params, what the reference's
+/* the Adam slots m, v [RDL_PARAMS_T(steps)] (device pointers): with the params, what the reference's
  * tf.train.Saver over the 'LSTM' scope checkpoints every episode and restores with -r
  * (lstm_train.py:86-87,102-107,199); the beta powers are not in that scope, so a restore
  * starts them afresh (rdl_reset, then rdl_set_params + rdl_set_slots) */

@@ -8,10 +8,14 @@ and its truncated-BPTT training step.
       c_t = sig(f + 1) c_{t-1} + sig(i) tanh(j)                   forget_bias 1, no peepholes,
       h_t = sig(o) tanh(c_t)                                      no projection)
       y_t = dense(tanh dense 32 (tanh dense 64 (tanh dense 128 (tanh dense 64 (h_t))))) (4)
+            with step t's OWN head: the reference calls tf.layers.dense inside its Python loop
+            over the T steps without reuse (student_nn.py:40-47), so every call creates new
+            variables (dense_1 .. dense_5T); the LSTMCell object and the prev dense are shared
   loss: kl_loss (loss.py:3-13, summed over T and B) or MSE; Adam lr 1e-3 (lstm_train.py:75-80).
   Flat parameters in the variables' creation order (lstm_train.py:53 builds the graph):
-      Wp[4][32] bp[32] | Wl[243][800] bl[800] | W1[200][64] b1 | W2[64][128] b2 |
-      W3[128][64] b3 | W4[64][32] b4 | W5[32][4] b5          = 227,012 floats
+      Wp[4][32] bp[32] | Wl[243][800] bl[800] | head_0 | ... | head_{T-1},
+      head_t = W1[200][64] b1 | W2[64][128] b2 | W3[128][64] b3 | W4[64][32] b4 | W5[32][4] b5
+      = 195,360 + 31,652 T floats (511,880 at the reference's T = 10)
   Dropout mask on ob (tf.nn.dropout, keep_prob): Philox4x32-10 keyed like the MLP student's
   (refnet_np.dropout) with counter word 3 = 4 t + q, so the oracle reproduces it exactly.
 
@@ -32,11 +36,16 @@ IN_X = 11 + 32
 HEAD = (UNITS, 64, 128, 64, 32, 4)
 
 
-def layout():
-    """name -> (offset, shape) in the flat vector."""
+CELL_PARAMS = 4 * 32 + 32 + (IN_X + UNITS) * 4 * UNITS + 4 * UNITS          # 195,360
+HEAD_PARAMS = sum(a * b + b for a, b in zip(HEAD[:-1], HEAD[1:]))            # 31,652
+
+
+def layout(T=10):
+    """name -> (offset, shape) in the flat vector; head t's layers are "h{t}/W1" .. "h{t}/b5"."""
     shapes = [("Wp", (4, 32)), ("bp", (32,)), ("Wl", (IN_X + UNITS, 4 * UNITS)), ("bl", (4 * UNITS,))]
-    for k, (a, b) in enumerate(zip(HEAD[:-1], HEAD[1:])):
-        shapes += [(f"W{k + 1}", (a, b)), (f"b{k + 1}", (b,))]
+    for t in range(T):
+        for k, (a, b) in enumerate(zip(HEAD[:-1], HEAD[1:])):
+            shapes += [(f"h{t}/W{k + 1}", (a, b)), (f"h{t}/b{k + 1}", (b,))]
     out, off = {}, 0
     for name, shp in shapes:
         out[name] = (off, shp)
@@ -44,19 +53,28 @@ def layout():
     return out, off
 
 
-LAYOUT, P_LSTM = layout()   # 227,012
+LAYOUT, P_LSTM = layout()   # 511,880 at T = 10
+
+
+def steps_of(p):
+    """T of a flat parameter vector (its number of heads)."""
+    t, r = divmod(np.asarray(p).size - CELL_PARAMS, HEAD_PARAMS)
+    assert r == 0 and t > 0, "not an LSTM student parameter vector"
+    return t
 
 
 def unpack(p):
     p = np.asarray(p, np.float64)
-    return {k: p[o:o + int(np.prod(s))].reshape(s) for k, (o, s) in LAYOUT.items()}
+    lay, _ = layout(steps_of(p))
+    return {k: p[o:o + int(np.prod(s))].reshape(s) for k, (o, s) in lay.items()}
 
 
-def init(seed=3):
+def init(seed=3, T=10):
     """glorot_uniform kernels (tf.layers.dense / LSTMCell defaults), zero biases."""
     rng = np.random.RandomState(seed)
-    p = np.zeros(P_LSTM, np.float32)
-    for k, (o, s) in LAYOUT.items():
+    lay, n = layout(T)
+    p = np.zeros(n, np.float32)
+    for k, (o, s) in lay.items():
         if len(s) == 2:
             lim = np.sqrt(6.0 / (s[0] + s[1]))
             p[o:o + s[0] * s[1]] = rng.uniform(-lim, lim, s[0] * s[1]).astype(np.float32)
@@ -121,8 +139,8 @@ def forward(p, ob, prev, state0=None):
             cache[k].append(v)
         a = [h]
         for k in range(1, 5):
-            a.append(np.tanh(a[-1] @ W[f"W{k}"] + W[f"b{k}"]))
-        ys.append(a[-1] @ W["W5"] + W["b5"])
+            a.append(np.tanh(a[-1] @ W[f"h{t}/W{k}"] + W[f"h{t}/b{k}"]))
+        ys.append(a[-1] @ W[f"h{t}/W5"] + W[f"h{t}/b5"])
         cache["acts"].append(a)
     return dict(pdflat=np.stack(ys), state=(c, h), cache=cache, prev=prev)
 
@@ -177,19 +195,20 @@ def bptt(steps, Wl, dh_out):
 
 def backward(p, fw, dout):
     W = unpack(p)
-    g = {k: np.zeros(s) for k, (_, s) in LAYOUT.items()}
+    lay, _ = layout(steps_of(p))
+    g = {k: np.zeros(s) for k, (_, s) in lay.items()}
     C = fw["cache"]
     T = len(C["x"])
     dh_out = []
-    for t in range(T):   # the head of every step (no recurrence through it)
+    for t in range(T):   # step t's own head (no recurrence through it)
         a = C["acts"][t]
-        gW, gb, da = dense_backward(a[4], dout[t], W["W5"])
-        g["W5"] += gW
-        g["b5"] += gb
+        gW, gb, da = dense_backward(a[4], dout[t], W[f"h{t}/W5"])
+        g[f"h{t}/W5"] += gW
+        g[f"h{t}/b5"] += gb
         for k in range(4, 0, -1):
-            gW, gb, da = dense_backward(a[k - 1], tanh_grad(a[k], da), W[f"W{k}"])
-            g[f"W{k}"] += gW
-            g[f"b{k}"] += gb
+            gW, gb, da = dense_backward(a[k - 1], tanh_grad(a[k], da), W[f"h{t}/W{k}"])
+            g[f"h{t}/W{k}"] += gW
+            g[f"h{t}/b{k}"] += gb
         dh_out.append(da)
     steps = [dict(x=C["x"][t], hprev=C["hprev"][t], cprev=C["cprev"][t], gi=C["gi"][t], gj=C["gj"][t],
                   gf=C["gf"][t], go=C["go"][t], c=C["c"][t]) for t in range(T)]
@@ -198,7 +217,7 @@ def backward(p, fw, dout):
         gW, gb, _ = dense_backward(fw["prev"][t], dxs[t][:, 11:IN_X], W["Wp"])
         g["Wp"] += gW
         g["bp"] += gb
-    return np.concatenate([g[k].ravel() for k in LAYOUT])
+    return np.concatenate([g[k].ravel() for k in lay])
 
 
 def loss_fn(p, ob, prev, t_pdflat, loss, n_global):

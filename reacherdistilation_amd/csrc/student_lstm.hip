@@ -2,14 +2,18 @@
 // steps of B windows and one truncated-BPTT distillation step, for gfx950.
 //
 // Graph (reference student_nn.py:21-49): x_t = [dropout(ob_t), dense32(prev_pdflat_t)];
-// TF1 LSTMCell(200) (gates i, j, f, o; forget_bias 1); head 200-64-128-64-32-4 (tanh).
+// TF1 LSTMCell(200) (gates i, j, f, o; forget_bias 1); head 200-64-128-64-32-4 (tanh) -- one
+// head PER UNROLLED STEP: the reference builds it with tf.layers.dense inside its Python loop
+// over the T steps without reuse, so step t has its own five layers (dense_{5t+1..5t+5}),
+// while the LSTMCell object (and the prev-pdflat dense) are shared.
 //
 // MI355X mapping.  Rows = (t, window) pairs, t-major, so every per-step slice is contiguous.
 // All GEMM-shaped work runs on one MFMA GEMM (csrc/rd_gemm.h) with fused epilogues:
 //  * the input half of the gate GEMM, [x_t] . Wl[0:43], is ONE GEMM over all T x B rows
 //    (bias fused); only the recurrent half h_{t-1} . Wl[43:243] is per step, with the cell
 //    fused into its epilogue (lstm_rec_fwd_kernel);
-//  * the head runs once over all T x B rows after the recurrence (bias + tanh fused);
+//  * the heads run once over all T x B rows after the recurrence (bias + tanh fused), step t's
+//    rows with step t's weights;
 //  * backward: each head layer's weight gradient and data gradient (tanh' of the stored
 //    activation fused) run as one grouped launch (rdg::gemm2); BPTT is one launch per step,
 //    dh_{t-1} = dz_t Wr^T with the cell backward of step t-1 in its epilogue; the LSTM weight
@@ -41,12 +45,14 @@ constexpr int H1 = 64, H2 = 128, H3 = 64, H4 = 32;
 // (tf.layers.dense order) in one launch, no column-sum pass
 constexpr int L1 = H1 + 4, L2 = H2 + 4, L3 = H3 + 4, L4 = H4 + 4;
 
-// flat parameter offsets (variable-creation order)
+// flat parameter offsets (variable-creation order): the shared part, then the T heads; OFF_W1 ..
+// OFF_B5 are offsets inside a head (head t at OFF_H + t HSZ)
 constexpr int OFF_WP = 0;
 constexpr int OFF_BP = OFF_WP + 4 * 32;
 constexpr int OFF_WL = OFF_BP + 32;
 constexpr int OFF_BL = OFF_WL + (XI + U) * G4;
-constexpr int OFF_W1 = OFF_BL + G4;
+constexpr int OFF_H = OFF_BL + G4;
+constexpr int OFF_W1 = 0;
 constexpr int OFF_B1 = OFF_W1 + U * H1;
 constexpr int OFF_W2 = OFF_B1 + H1;
 constexpr int OFF_B2 = OFF_W2 + H1 * H2;
@@ -56,11 +62,12 @@ constexpr int OFF_W4 = OFF_B3 + H3;
 constexpr int OFF_B4 = OFF_W4 + H3 * H4;
 constexpr int OFF_W5 = OFF_B4 + H4;
 constexpr int OFF_B5 = OFF_W5 + H4 * 4;
-constexpr int P_LSTM = OFF_B5 + 4;
-static_assert(P_LSTM == RDL_PARAMS, "flat layout");
-static_assert(OFF_WL % 4 == 0 && OFF_W1 % 4 == 0 && OFF_W2 % 4 == 0 && OFF_W3 % 4 == 0 && OFF_W4 % 4 == 0 &&
-                  OFF_W5 % 4 == 0 && (OFF_WL + XI * G4) % 4 == 0,
+constexpr int HSZ = OFF_B5 + 4;                 // 31,652 floats per head
+static_assert(OFF_H == RDL_CELL_PARAMS && HSZ == RDL_HEAD_PARAMS && RDL_PARAMS == OFF_H + 10 * HSZ, "flat layout");
+static_assert(OFF_WL % 4 == 0 && OFF_H % 4 == 0 && HSZ % 4 == 0 && OFF_W2 % 4 == 0 && OFF_W3 % 4 == 0 &&
+                  OFF_W4 % 4 == 0 && OFF_W5 % 4 == 0 && (OFF_WL + XI * G4) % 4 == 0,
               "16-B aligned weight matrices");
+__host__ __device__ constexpr int64_t params_of(int T) { return OFF_H + (int64_t)T * HSZ; }
 
 constexpr int N_MET = 4;
 constexpr int LOSS_BLOCK = 256;
@@ -641,15 +648,19 @@ __device__ __forceinline__ void head_stage(const float* __restrict__ src, int ld
     }
 }
 
-__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P,
-                                                       float* A1, float* A2, float* A3, float* A4, float* Y, int64_t R) {
+// workgroup (t, rb) of the grid T x nb: rows t B + 16 rb .. of step t, with step t's head
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
+                                                       float* A1, float* A2, float* A3, float* A4, float* Y, int64_t B,
+                                                       int nb) {
     __shared__ __attribute__((aligned(16))) float X0[HF_ROWS][U + 4];
     __shared__ __attribute__((aligned(16))) float X1[HF_ROWS][L1];
     __shared__ __attribute__((aligned(16))) float X2[HF_ROWS][L2];
     __shared__ __attribute__((aligned(16))) float X3[HF_ROWS][L3];
     __shared__ __attribute__((aligned(16))) float X4[HF_ROWS][L4];
     __shared__ __attribute__((aligned(16))) float X5[HF_ROWS][8];
-    const int64_t row0 = (int64_t)blockIdx.x * HF_ROWS;
+    const int ts = blockIdx.x / nb, rb = blockIdx.x - ts * nb;
+    const int64_t row0 = (int64_t)ts * B + (int64_t)rb * HF_ROWS, R = (int64_t)(ts + 1) * B;
+    const float* P = P0 + OFF_H + (int64_t)ts * HSZ;   // step ts's head
     head_stage<U, U + 4>(Hc, U, row0, R, X0);
     __syncthreads();
     head_layer<U, H1, true>(X0, X1, P + OFF_W1, P + OFF_B1, A1, L1, row0, R);
@@ -664,7 +675,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
 // and the five [dW; db] weight-gradient partials over its rows (the stored activations carry
 // the ones column; Hc gets one in LDS) as one partial row of the flat [W1 b1 ... W5 b5] range;
 // head_wgrad_reduce_kernel sums the rows in a fixed order.  Two launches instead of six.
-constexpr int HB_PART = P_LSTM - OFF_W1;   // 31,652 floats: [W1;b1][W2;b2][W3;b3][W4;b4][W5;b5]
+constexpr int HB_PART = HSZ;   // 31,652 floats: [W1;b1][W2;b2][W3;b3][W4;b4][W5;b5] of one head
 // dIn[16][NI] = (dOut[16][KO] . W^T) (* (1 - act^2) when DT); W is [NI][KO] (layer input x output)
 template <int KO, int NI, bool DT, int LD, int LI, int LA>
 __device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)[LI], const float (*act)[LA],
@@ -721,11 +732,11 @@ __device__ __forceinline__ void head_wgrad(const float (*act)[LA], const float (
     }
 }
 
-__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P,
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
                                                        const float* __restrict__ A1, const float* __restrict__ A2,
                                                        const float* __restrict__ A3, const float* __restrict__ A4,
                                                        const float* __restrict__ dY, float* __restrict__ dHh,
-                                                       float* __restrict__ part, int64_t R) {
+                                                       float* __restrict__ part, int64_t B, int nb) {
     __shared__ __attribute__((aligned(16))) float X0[HF_ROWS][U + 4];   // Hc, ones column U
     __shared__ __attribute__((aligned(16))) float X1[HF_ROWS][L1];
     __shared__ __attribute__((aligned(16))) float X2[HF_ROWS][L2];
@@ -736,8 +747,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     __shared__ __attribute__((aligned(16))) float D3[HF_ROWS][L3];
     __shared__ __attribute__((aligned(16))) float D2[HF_ROWS][L2];
     __shared__ __attribute__((aligned(16))) float D1[HF_ROWS][L1];
-    const int64_t row0 = (int64_t)blockIdx.x * HF_ROWS;
-    // rows past R are zero (activations and gradients): they add nothing to the partials
+    const int ts = blockIdx.x / nb, rb = blockIdx.x - ts * nb;   // as head_fwd_kernel
+    const int64_t row0 = (int64_t)ts * B + (int64_t)rb * HF_ROWS, R = (int64_t)(ts + 1) * B;
+    const float* P = P0 + OFF_H + (int64_t)ts * HSZ;
+    // rows past R (the step's last row) are zero (activations and gradients): they add nothing to the partials
     head_stage<U, U + 4>(Hc, U, row0, R, X0);
     head_stage<H1 + 1, L1>(A1, L1, row0, R, X1);   // with the ones column
     head_stage<H2 + 1, L2>(A2, L2, row0, R, X2);
@@ -763,19 +776,21 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     head_wgrad<H4 + 1, 4>(X4, D5, pw + (OFF_W5 - OFF_W1));
 }
 
-// grad[OFF_W1 + p] = sum over the workgroups' partial rows, in row order
-__global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part, int nwg,
+// head t's gradient (blockIdx.y = t): grad[OFF_H + t HSZ + p] = sum over step t's nb
+// workgroups' partial rows, in row order
+__global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part, int nb,
                                                                 float* __restrict__ g) {
     const int p = blockIdx.x * 256 + threadIdx.x;
     if (p >= HB_PART) return;
+    const float* q = part + (int64_t)blockIdx.y * nb * HB_PART + p;
     float a = 0.f, b = 0.f;
     int w = 0;
-    for (; w + 1 < nwg; w += 2) {
-        a += part[(int64_t)w * HB_PART + p];
-        b += part[(int64_t)(w + 1) * HB_PART + p];
+    for (; w + 1 < nb; w += 2) {
+        a += q[(int64_t)w * HB_PART];
+        b += q[(int64_t)(w + 1) * HB_PART];
     }
-    if (w < nwg) a += part[(int64_t)w * HB_PART + p];
-    g[OFF_W1 + p] = a + b;
+    if (w < nb) a += q[(int64_t)w * HB_PART];
+    g[OFF_H + (int64_t)blockIdx.y * HSZ + p] = a + b;
 }
 
 // BPTT through one cell (dh = dh_head + dh_next; dc carried in place).  The fused backward
@@ -921,13 +936,14 @@ struct AdamArgs {
     float* v;
     uint32_t* ctl;
     float lr, b1, b2, eps;
+    int64_t n;   // parameters (params_of(T))
 };
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
     const int p = blockIdx.x * 256 + threadIdx.x;
     const uint32_t S = a.ctl[4];
     const float b1p = __uint_as_float(a.ctl[5]), b2p = __uint_as_float(a.ctl[6]);
-    if (p < P_LSTM) {   // TF1 ApplyAdam (lstm_train.py:73-79)
+    if (p < a.n) {   // TF1 ApplyAdam (lstm_train.py:73-79)
         const float g = a.grad[p];
         const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
         float m = a.m[p], v = a.v[p];
@@ -966,6 +982,7 @@ struct rdl_trainer {
     int device = 0, cus = 256;
     hipStream_t stream = nullptr;
     int T = 0;
+    int64_t np = 0;   // flat parameters: the shared cell part + T heads (params_of(T))
     int64_t Bmax = 0;
     float *params = nullptr, *m = nullptr, *v = nullptr, *grad = nullptr, *own_grad = nullptr;
     float *X = nullptr, *H = nullptr, *Cs = nullptr, *Z = nullptr, *G = nullptr;
@@ -1047,7 +1064,9 @@ int pr_dbg() {   // diagnostic builds: RDL_PR_DBG bit 0 skips the exchange loads
 }
 
 bool fused_head(const rdl_trainer* t, int64_t R) {
-    return !(t->cfg.kernels & RDL_KERNELS_LAYER_HEAD) && R <= HF_MAX_ROWS;
+    // the partial rows of its T x ceil(B / 16) workgroups live in the split-K buffer
+    const int64_t nwg = (int64_t)t->T * ((R / t->T + HF_ROWS - 1) / HF_ROWS);
+    return !(t->cfg.kernels & RDL_KERNELS_LAYER_HEAD) && R <= HF_MAX_ROWS && nwg * HB_PART <= SPLIT_FLOATS;
 }
 
 bool persistent(const rdl_trainer* t, int64_t B) {
@@ -1101,19 +1120,30 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
 #endif
     }
     }
-    // head over all T x B rows (student_nn.py:42-46)
+    // step t's head over its B rows (student_nn.py:42-46, one head per unrolled step)
     const float* Hc = t->H + B * U;
     if (fused_head(t, R)) {
-        hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)((R + HF_ROWS - 1) / HF_ROWS)), dim3(256), 0, t->stream, Hc, P,
-                           t->A1, t->A2, t->A3, t->A4, out_pdflat, R);
+        const int nb = (int)((B + HF_ROWS - 1) / HF_ROWS);
+        hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)(T * nb)), dim3(256), 0, t->stream, Hc, P, t->A1, t->A2,
+                           t->A3, t->A4, out_pdflat, B, nb);
         RDL_CK(hipGetLastError(), "rdl head_fwd_kernel");
         return RD_OK;
     }
-    RDL_CK(mm(t, (int)R, H1, U, Hc, U, 0, P + OFF_W1, H1, 0, t->A1, L1, P + OFF_B1, rdg::EPI_TANH), "rdl head1");
-    RDL_CK(mm(t, (int)R, H2, H1, t->A1, L1, 0, P + OFF_W2, H2, 0, t->A2, L2, P + OFF_B2, rdg::EPI_TANH), "rdl head2");
-    RDL_CK(mm(t, (int)R, H3, H2, t->A2, L2, 0, P + OFF_W3, H3, 0, t->A3, L3, P + OFF_B3, rdg::EPI_TANH), "rdl head3");
-    RDL_CK(mm(t, (int)R, H4, H3, t->A3, L3, 0, P + OFF_W4, H4, 0, t->A4, L4, P + OFF_B4, rdg::EPI_TANH), "rdl head4");
-    RDL_CK(mm(t, (int)R, 4, H4, t->A4, L4, 0, P + OFF_W5, 4, 0, out_pdflat, 4, P + OFF_B5), "rdl head5");
+    for (int s = 0; s < T; ++s) {
+        const float* Ph = P + OFF_H + (int64_t)s * HSZ;
+        const int64_t r0 = (int64_t)s * B;
+        const int Bi = (int)B;
+        RDL_CK(mm(t, Bi, H1, U, Hc + r0 * U, U, 0, Ph + OFF_W1, H1, 0, t->A1 + r0 * L1, L1, Ph + OFF_B1, rdg::EPI_TANH),
+               "rdl head1");
+        RDL_CK(mm(t, Bi, H2, H1, t->A1 + r0 * L1, L1, 0, Ph + OFF_W2, H2, 0, t->A2 + r0 * L2, L2, Ph + OFF_B2,
+                  rdg::EPI_TANH), "rdl head2");
+        RDL_CK(mm(t, Bi, H3, H2, t->A2 + r0 * L2, L2, 0, Ph + OFF_W3, H3, 0, t->A3 + r0 * L3, L3, Ph + OFF_B3,
+                  rdg::EPI_TANH), "rdl head3");
+        RDL_CK(mm(t, Bi, H4, H3, t->A3 + r0 * L3, L3, 0, Ph + OFF_W4, H4, 0, t->A4 + r0 * L4, L4, Ph + OFF_B4,
+                  rdg::EPI_TANH), "rdl head4");
+        RDL_CK(mm(t, Bi, 4, H4, t->A4 + r0 * L4, L4, 0, Ph + OFF_W5, 4, 0, out_pdflat + r0 * 4, 4, Ph + OFF_B5),
+               "rdl head5");
+    }
     return RD_OK;
 }
 
@@ -1135,34 +1165,44 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
         RDL_CK(hipGetLastError(), "rdl metrics_kernel");
     }
     const float* Hc = t->H + B * U;
-    if (fused_head(t, R)) {   // the head backward as two launches (head_bwd_kernel + fixed-order reduce)
-        const unsigned nwg = (unsigned)((R + HF_ROWS - 1) / HF_ROWS);
-        hipLaunchKernelGGL(head_bwd_kernel, dim3(nwg), dim3(256), 0, t->stream, Hc, P, (const float*)t->A1,
-                           (const float*)t->A2, (const float*)t->A3, (const float*)t->A4, (const float*)t->dY, t->dHh,
-                           t->split, R);
+    if (fused_head(t, R)) {   // the heads' backward as two launches (head_bwd_kernel + fixed-order reduce)
+        const int nb = (int)((B + HF_ROWS - 1) / HF_ROWS);
+        hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)(T * nb)), dim3(256), 0, t->stream, Hc, P,
+                           (const float*)t->A1, (const float*)t->A2, (const float*)t->A3, (const float*)t->A4,
+                           (const float*)t->dY, t->dHh, t->split, B, nb);
         RDL_CK(hipGetLastError(), "rdl head_bwd_kernel");
-        hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((HB_PART + 255) / 256), dim3(256), 0, t->stream,
-                           (const float*)t->split, (int)nwg, g);
+        hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((HB_PART + 255) / 256, (unsigned)T), dim3(256), 0, t->stream,
+                           (const float*)t->split, nb, g);
         RDL_CK(hipGetLastError(), "rdl head_wgrad_reduce_kernel");
     } else {
-    // head backward (weight gradients over all rows; data gradients with the tanh derivative fused)
-    // per layer, [dW; db] (weight gradient, ones column) beside the data gradient with tanh'
-    RDL_CK(mm2(t, ga(H4 + 1, 4, Ri, t->A4, L4, 1, t->dY, 4, 0, g + OFF_W5, 4),
-               ga(Ri, H4, 4, t->dY, 4, 0, P + OFF_W5, 4, 1, t->D32, H4, rdg::EPI_DTANH, t->A4, L4)),
-           "rdl dW5 db5 | dZ4");
-    RDL_CK(mm2(t, ga(H3 + 1, H4, Ri, t->A3, L3, 1, t->D32, H4, 0, g + OFF_W4, H4),
-               ga(Ri, H3, H4, t->D32, H4, 0, P + OFF_W4, H4, 1, t->D64a, H3, rdg::EPI_DTANH, t->A3, L3)),
-           "rdl dW4 db4 | dZ3");
-    RDL_CK(mm2(t, ga(H2 + 1, H3, Ri, t->A2, L2, 1, t->D64a, H3, 0, g + OFF_W3, H3),
-               ga(Ri, H2, H3, t->D64a, H3, 0, P + OFF_W3, H3, 1, t->D128, H2, rdg::EPI_DTANH, t->A2, L2)),
-           "rdl dW3 db3 | dZ2");
-    RDL_CK(mm2(t, ga(H1 + 1, H2, Ri, t->A1, L1, 1, t->D128, H2, 0, g + OFF_W2, H2),
-               ga(Ri, H1, H2, t->D128, H2, 0, P + OFF_W2, H2, 1, t->D64b, H1, rdg::EPI_DTANH, t->A1, L1)),
-           "rdl dW2 db2 | dZ1");
-    RDL_CK(mm2(t, ga(U, H1, Ri, Hc, U, 1, t->D64b, H1, 0, g + OFF_W1, H1),
-               ga(Ri, U, H1, t->D64b, H1, 0, P + OFF_W1, H1, 1, t->dHh, U)),
-           "rdl dW1 | dHhead");
-    RDL_CK(colsum(t, t->D64b, R, H1, H1, g + OFF_B1), "rdl db1");
+    // step s's head backward over its B rows (weight gradients; data gradients with the tanh
+    // derivative fused): per layer, [dW; db] (weight gradient, ones column) beside the data
+    // gradient with tanh'
+    for (int s = 0; s < T; ++s) {
+        const float* Ph = P + OFF_H + (int64_t)s * HSZ;
+        float* gh = g + OFF_H + (int64_t)s * HSZ;
+        const int64_t r0 = (int64_t)s * B;
+        const int Bi = (int)B;
+        const float *a1 = t->A1 + r0 * L1, *a2 = t->A2 + r0 * L2, *a3 = t->A3 + r0 * L3, *a4 = t->A4 + r0 * L4;
+        const float* dy = t->dY + r0 * 4;
+        float *d32 = t->D32 + r0 * H4, *d64a = t->D64a + r0 * H3, *d128 = t->D128 + r0 * H2, *d64b = t->D64b + r0 * H1;
+        RDL_CK(mm2(t, ga(H4 + 1, 4, Bi, a4, L4, 1, dy, 4, 0, gh + OFF_W5, 4),
+                   ga(Bi, H4, 4, dy, 4, 0, Ph + OFF_W5, 4, 1, d32, H4, rdg::EPI_DTANH, a4, L4)),
+               "rdl dW5 db5 | dZ4");
+        RDL_CK(mm2(t, ga(H3 + 1, H4, Bi, a3, L3, 1, d32, H4, 0, gh + OFF_W4, H4),
+                   ga(Bi, H3, H4, d32, H4, 0, Ph + OFF_W4, H4, 1, d64a, H3, rdg::EPI_DTANH, a3, L3)),
+               "rdl dW4 db4 | dZ3");
+        RDL_CK(mm2(t, ga(H2 + 1, H3, Bi, a2, L2, 1, d64a, H3, 0, gh + OFF_W3, H3),
+                   ga(Bi, H2, H3, d64a, H3, 0, Ph + OFF_W3, H3, 1, d128, H2, rdg::EPI_DTANH, a2, L2)),
+               "rdl dW3 db3 | dZ2");
+        RDL_CK(mm2(t, ga(H1 + 1, H2, Bi, a1, L1, 1, d128, H2, 0, gh + OFF_W2, H2),
+                   ga(Bi, H1, H2, d128, H2, 0, Ph + OFF_W2, H2, 1, d64b, H1, rdg::EPI_DTANH, a1, L1)),
+               "rdl dW2 db2 | dZ1");
+        RDL_CK(mm2(t, ga(U, H1, Bi, Hc + r0 * U, U, 1, d64b, H1, 0, gh + OFF_W1, H1),
+                   ga(Bi, U, H1, d64b, H1, 0, Ph + OFF_W1, H1, 1, t->dHh + r0 * U, U)),
+               "rdl dW1 | dHhead");
+        RDL_CK(colsum(t, d64b, B, H1, H1, gh + OFF_B1), "rdl db1");
+    }
     }
     // BPTT (the gate buffer Z is reused for dz: the forward keeps activations in G)
     float* dZl = t->Z;
@@ -1227,8 +1267,8 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
 }
 
 int launch_adam(rdl_trainer* t) {
-    AdamArgs a{t->grad, t->params, t->m, t->v, t->ctl, t->cfg.lr, t->cfg.beta1, t->cfg.beta2, t->cfg.eps};
-    hipLaunchKernelGGL(adam_kernel, dim3((P_LSTM + 255) / 256), dim3(256), 0, t->stream, a);
+    AdamArgs a{t->grad, t->params, t->m, t->v, t->ctl, t->cfg.lr, t->cfg.beta1, t->cfg.beta2, t->cfg.eps, t->np};
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((t->np + 255) / 256)), dim3(256), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rdl adam_kernel");
     return RD_OK;
 }
@@ -1239,7 +1279,7 @@ bool bad_windows(const rdl_trainer* t, int64_t B) { return B <= 0 || B > t->Bmax
 
 extern "C" {
 
-int rdl_param_count(void) { return P_LSTM; }
+int64_t rdl_param_count(int32_t steps) { return steps > 0 ? params_of(steps) : -1; }
 
 int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_stream) {
     if (!out || !cfg) return rd::set_error(RD_EINVAL, "rdl_create: null argument");
@@ -1258,6 +1298,7 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     t->cus = cu_count(device);
     t->stream = (hipStream_t)hip_stream;
     t->T = cfg->steps;
+    t->np = params_of(t->T);
     t->Bmax = cfg->max_windows;
     const int64_t R = (int64_t)t->T * t->Bmax, B = t->Bmax;
     const int64_t nch = (R + COLSUM_CHUNK - 1) / COLSUM_CHUNK;
@@ -1267,10 +1308,10 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
         if (e == hipSuccess) e = hipMalloc((void**)p, sizeof(float) * (size_t)floats);
         if (e == hipSuccess) e = hipMemsetAsync(*p, 0, sizeof(float) * (size_t)floats, t->stream);
     };
-    alloc(&t->params, P_LSTM);
-    alloc(&t->m, P_LSTM);
-    alloc(&t->v, P_LSTM);
-    alloc(&t->own_grad, P_LSTM);
+    alloc(&t->params, t->np);
+    alloc(&t->m, t->np);
+    alloc(&t->v, t->np);
+    alloc(&t->own_grad, t->np);
     alloc(&t->X, R * XLD);
     alloc(&t->H, (R + B) * U);
     alloc(&t->Cs, (R + B) * U);
@@ -1346,7 +1387,7 @@ int rdl_set_stream(rdl_trainer* t, void* hip_stream) {
 int rdl_set_params(rdl_trainer* t, const float* params) {
     if (!t || !params) return rd::set_error(RD_EINVAL, "rdl_set_params: null argument");
     rd::DeviceGuard dg(t->device);
-    RD_HIP(hipMemcpyAsync(t->params, params, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream),
+    RD_HIP(hipMemcpyAsync(t->params, params, sizeof(float) * t->np, hipMemcpyDeviceToDevice, t->stream),
            "rdl_set_params");
     return RD_OK;
 }
@@ -1354,7 +1395,7 @@ int rdl_set_params(rdl_trainer* t, const float* params) {
 int rdl_get_params(rdl_trainer* t, float* params) {
     if (!t || !params) return rd::set_error(RD_EINVAL, "rdl_get_params: null argument");
     rd::DeviceGuard dg(t->device);
-    RD_HIP(hipMemcpyAsync(params, t->params, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream),
+    RD_HIP(hipMemcpyAsync(params, t->params, sizeof(float) * t->np, hipMemcpyDeviceToDevice, t->stream),
            "rdl_get_params");
     return RD_OK;
 }
@@ -1362,24 +1403,24 @@ int rdl_get_params(rdl_trainer* t, float* params) {
 int rdl_get_slots(rdl_trainer* t, float* m, float* v) {
     if (!t || !m || !v) return rd::set_error(RD_EINVAL, "rdl_get_slots: null argument");
     rd::DeviceGuard dg(t->device);
-    RD_HIP(hipMemcpyAsync(m, t->m, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream), "rdl_get_slots");
-    RD_HIP(hipMemcpyAsync(v, t->v, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream), "rdl_get_slots");
+    RD_HIP(hipMemcpyAsync(m, t->m, sizeof(float) * t->np, hipMemcpyDeviceToDevice, t->stream), "rdl_get_slots");
+    RD_HIP(hipMemcpyAsync(v, t->v, sizeof(float) * t->np, hipMemcpyDeviceToDevice, t->stream), "rdl_get_slots");
     return RD_OK;
 }
 
 int rdl_set_slots(rdl_trainer* t, const float* m, const float* v) {
     if (!t || !m || !v) return rd::set_error(RD_EINVAL, "rdl_set_slots: null argument");
     rd::DeviceGuard dg(t->device);
-    RD_HIP(hipMemcpyAsync(t->m, m, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream), "rdl_set_slots");
-    RD_HIP(hipMemcpyAsync(t->v, v, sizeof(float) * P_LSTM, hipMemcpyDeviceToDevice, t->stream), "rdl_set_slots");
+    RD_HIP(hipMemcpyAsync(t->m, m, sizeof(float) * t->np, hipMemcpyDeviceToDevice, t->stream), "rdl_set_slots");
+    RD_HIP(hipMemcpyAsync(t->v, v, sizeof(float) * t->np, hipMemcpyDeviceToDevice, t->stream), "rdl_set_slots");
     return RD_OK;
 }
 
 int rdl_reset(rdl_trainer* t) {
     if (!t) return rd::set_error(RD_EINVAL, "rdl_reset: null handle");
     rd::DeviceGuard dg(t->device);
-    RD_HIP(hipMemsetAsync(t->m, 0, sizeof(float) * P_LSTM, t->stream), "rdl_reset");
-    RD_HIP(hipMemsetAsync(t->v, 0, sizeof(float) * P_LSTM, t->stream), "rdl_reset");
+    RD_HIP(hipMemsetAsync(t->m, 0, sizeof(float) * t->np, t->stream), "rdl_reset");
+    RD_HIP(hipMemsetAsync(t->v, 0, sizeof(float) * t->np, t->stream), "rdl_reset");
     hipLaunchKernelGGL(init_ctl_kernel, dim3(1), dim3(64), 0, t->stream, t->ctl, t->cfg.beta1, t->cfg.beta2);
     RD_HIP(hipGetLastError(), "rdl_reset");
     return RD_OK;

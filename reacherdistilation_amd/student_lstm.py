@@ -2,12 +2,13 @@
 
 ``StudentLstmTrainer`` is the 'LSTM' scope of the reference's lstm_train.py (:35-79): the
 graph ``student_lstm_graph`` (student_nn.py:21-49: dense prev-pdflat embedding, TF1
-LSTMCell(200), 200-64-128-64-32-4 head), ``kl_loss`` (loss.py:3-13) and TF1 Adam, run by
+LSTMCell(200), a 200-64-128-64-32-4 head per unrolled step), ``kl_loss`` (loss.py:3-13) and TF1 Adam, run by
 csrc/student_lstm.hip.  Tensors are the reference's window layout: ob [T, B, 11],
 prev_pdflat [T, B, 4], t_pdflat / pdflat [T, B, 4], state [2, B, 200] = (c, m).
 
 Multi-GPU: windows sharded contiguously (row_base = first global window), one
-all_reduce(SUM) of the flat 227,012-float gradient per optimiser step.
+all_reduce(SUM) of the flat gradient (511,880 floats at T = 10: the shared cell and one
+head per unrolled step) per optimiser step.
 """
 from __future__ import annotations
 
@@ -26,10 +27,24 @@ P = nat.P
 I32, I64, U64, F32, INT = nat.I32, nat.I64, nat.U64, nat.F32, nat.INT
 
 HEAD = (NUM_UNITS, 64, 128, 64, 32, 4)
-SHAPES = [("Wp", (4, 32)), ("bp", (32,)), ("Wl", (OBSPACE_SHAPE + 32 + NUM_UNITS, 4 * NUM_UNITS)),
-          ("bl", (4 * NUM_UNITS,))] + [x for k, (a, b) in enumerate(zip(HEAD[:-1], HEAD[1:]))
-                                        for x in ((f"W{k + 1}", (a, b)), (f"b{k + 1}", (b,)))]
-N_PARAMS = sum(int(np.prod(s)) for _, s in SHAPES)   # 227,012
+CELL_SHAPES = [("Wp", (4, 32)), ("bp", (32,)), ("Wl", (OBSPACE_SHAPE + 32 + NUM_UNITS, 4 * NUM_UNITS)),
+               ("bl", (4 * NUM_UNITS,))]
+HEAD_SHAPES = [x for k, (a, b) in enumerate(zip(HEAD[:-1], HEAD[1:]))
+               for x in ((f"W{k + 1}", (a, b)), (f"b{k + 1}", (b,)))]
+
+
+def shapes(T: int = STEPS_UNROLLED):
+    """The flat layout in variable-creation order: the shared prev-pdflat dense and LSTMCell, then
+    one head per unrolled step (the reference's tf.layers.dense calls inside its loop over the T
+    steps create new variables at every step, student_nn.py:40-47; TF names dense_1..dense_5T)."""
+    return CELL_SHAPES + [(f"h{t}/{n}", s) for t in range(T) for n, s in HEAD_SHAPES]
+
+
+def n_params(T: int = STEPS_UNROLLED) -> int:
+    return sum(int(np.prod(s)) for _, s in shapes(T))
+
+
+N_PARAMS = n_params(STEPS_UNROLLED)   # 511,880 at the reference's T = 10
 LOSSES = {"mse": 0, "kl": 1}
 
 
@@ -40,7 +55,7 @@ class RdlConfig(ctypes.Structure):
 
 
 nat.register({
-    "rdl_param_count": (INT, []),
+    "rdl_param_count": (I64, [I32]),
     "rdl_create": (INT, [ctypes.POINTER(P), ctypes.POINTER(RdlConfig), INT, P]),
     "rdl_destroy": (INT, [P]),
     "rdl_set_stream": (INT, [P, P]),
@@ -61,11 +76,11 @@ nat.register({
 })
 
 
-def glorot_init(seed: int = 3) -> np.ndarray:
+def glorot_init(seed: int = 3, T: int = STEPS_UNROLLED) -> np.ndarray:
     """glorot_uniform kernels (tf.layers.dense and LSTMCell defaults), zero biases."""
     rng = np.random.RandomState(seed)
     out = []
-    for _, s in SHAPES:
+    for _, s in shapes(T):
         if len(s) == 2:
             lim = math.sqrt(6.0 / (s[0] + s[1]))
             out.append(rng.uniform(-lim, lim, s[0] * s[1]).astype(np.float32))
@@ -101,7 +116,8 @@ class StudentLstmTrainer:
         self.rank, self.world, self.pg = rank, world_size, process_group
         self.T = int(self.cfg.steps)
         self._lib = nat.load()
-        assert self._lib.rdl_param_count() == N_PARAMS
+        self.n_params = n_params(self.T)
+        assert self._lib.rdl_param_count(self.T) == self.n_params
         c = RdlConfig(loss=LOSSES[self.cfg.loss], lr=self.cfg.lr, beta1=self.cfg.beta1, beta2=self.cfg.beta2,
                       eps=self.cfg.eps, steps=self.T, max_windows=int(self.cfg.max_windows),
                       metrics_len=self.cfg.metrics_len, keep_prob=self.cfg.keep_prob,
@@ -112,9 +128,9 @@ class StudentLstmTrainer:
             nat.check(self._lib.rdl_create(ctypes.byref(h), ctypes.byref(c), self.device.index or 0,
                                            nat.stream_handle(self.device)), "rdl_create")
         self._h = h
-        self._grad = torch.zeros(N_PARAMS, dtype=torch.float32, device=self.device)
+        self._grad = torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
         nat.check(self._lib.rdl_bind_grad_buffer(self._h, nat.ptr(self._grad)), "rdl_bind_grad_buffer")
-        self.set_params(glorot_init(self.cfg.init_seed) if params is None else params)
+        self.set_params(glorot_init(self.cfg.init_seed, self.T) if params is None else params)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -134,14 +150,14 @@ class StudentLstmTrainer:
     def set_params(self, params):
         p = (params if torch.is_tensor(params) else torch.from_numpy(np.asarray(params, np.float32)))
         p = p.to(self.device, torch.float32).reshape(-1).contiguous()
-        if p.numel() != N_PARAMS:
-            raise ValueError(f"expected {N_PARAMS} parameters, got {p.numel()}")
+        if p.numel() != self.n_params:
+            raise ValueError(f"expected {self.n_params} parameters, got {p.numel()}")
         self._sync_stream()
         nat.check(self._lib.rdl_set_params(self._h, nat.ptr(p)), "rdl_set_params")
         torch.cuda.current_stream(self.device).synchronize()
 
     def params(self) -> torch.Tensor:
-        out = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
+        out = torch.empty(self.n_params, dtype=torch.float32, device=self.device)
         self._sync_stream()
         nat.check(self._lib.rdl_get_params(self._h, nat.ptr(out)), "rdl_get_params")
         return out
@@ -150,7 +166,7 @@ class StudentLstmTrainer:
         """tf.train.Saver(var_list=LSTM/*).save (reference lstm_train.py:86-87,199): the
         parameters and the Adam slots m, v, as a safetensors file (nothing executable)."""
         from safetensors.torch import save_file
-        m = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
+        m = torch.empty(self.n_params, dtype=torch.float32, device=self.device)
         v = torch.empty_like(m)
         self._sync_stream()
         nat.check(self._lib.rdl_get_slots(self._h, nat.ptr(m), nat.ptr(v)), "rdl_get_slots")
@@ -163,8 +179,8 @@ class StudentLstmTrainer:
         the Adam variables before restoring the 'LSTM' scope (:99-105)."""
         from safetensors.torch import load_file
         d = load_file(path)
-        if d["params"].numel() != N_PARAMS:
-            raise ValueError(f"{path}: {d['params'].numel()} parameters, expected {N_PARAMS}")
+        if d["params"].numel() != self.n_params:
+            raise ValueError(f"{path}: {d['params'].numel()} parameters, expected {self.n_params}")
         self.reset_optimizer()
         self.set_params(d["params"])
         m = d["adam_m"].to(self.device, torch.float32).contiguous()

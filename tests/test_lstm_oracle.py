@@ -20,9 +20,35 @@ def _batch(T, B, seed=0):
 
 
 def test_layout():
-    assert ln.P_LSTM == 227012
+    """One head per unrolled step (the reference's tf.layers.dense calls inside its loop over
+    the T steps create new variables each time, student_nn.py:40-47): 195,360 shared + 31,652
+    per step, 511,880 at the reference's T = 10; the ABI's RDL_PARAMS_T agrees."""
+    assert ln.P_LSTM == 511880 and ln.CELL_PARAMS == 195360 and ln.HEAD_PARAMS == 31652
     o, s = ln.LAYOUT["Wl"]
     assert s == (243, 800) and o == 4 * 32 + 32
+    lay, n = ln.layout(3)
+    assert n == 195360 + 3 * 31652 and lay["h0/W1"][0] == 195360 and lay["h2/b5"][0] == n - 4
+    import re as _re
+    from tests.conftest import ROOT
+    import os
+    hdr = open(os.path.join(ROOT, "include", "reacher_student_lstm.h")).read()
+    assert int(_re.search(r"#define RDL_CELL_PARAMS (\d+)", hdr).group(1)) == ln.CELL_PARAMS
+    assert int(_re.search(r"#define RDL_HEAD_PARAMS (\d+)", hdr).group(1)) == ln.HEAD_PARAMS
+
+
+def test_each_step_has_its_own_head():
+    """Changing step 1's head changes only step 1's output (the reference's per-step dense
+    variables), while the cell is shared by every step."""
+    T, B = 3, 2
+    p = ln.init(2, T)
+    ob, prev, _ = _batch(T, B, 1)
+    y0 = ln.forward(p, ob, prev)["pdflat"]
+    lay, _ = ln.layout(T)
+    q = p.copy()
+    o, s = lay["h1/W5"]
+    q[o:o + s[0] * s[1]] += 0.5
+    y1 = ln.forward(q, ob, prev)["pdflat"]
+    assert np.array_equal(y0[0], y1[0]) and np.array_equal(y0[2], y1[2]) and not np.allclose(y0[1], y1[1])
 
 
 def test_cell_matches_hand_computation():
@@ -42,19 +68,20 @@ def test_cell_matches_hand_computation():
 @pytest.mark.parametrize("loss", ["mse", "kl"])
 def test_bptt_matches_finite_differences(loss):
     rs = np.random.RandomState(4)
-    p = ln.init(5).astype(np.float64)
-    for k, (o, s) in ln.LAYOUT.items():
+    T, B = 4, 3
+    lay, n = ln.layout(T)
+    p = ln.init(5, T).astype(np.float64)
+    for k, (o, s) in lay.items():
         if len(s) == 1:
             p[o:o + s[0]] = rs.uniform(-.2, .2, s[0])
-    T, B = 4, 3
     ob, prev, t = _batch(T, B, 2)
     fw = ln.forward(p, ob, prev)
     _, d, _ = ln.loss_and_dout(fw["pdflat"], t, loss, T * B)
     g = ln.backward(p, fw, d)
-    idx = list(rs.choice(ln.P_LSTM, 40, replace=False))
-    for name in ("Wp", "bp", "bl", "b1", "b5"):
-        idx.append(ln.LAYOUT[name][0])
-    o = ln.LAYOUT["Wl"][0]
+    idx = list(rs.choice(n, 40, replace=False))
+    for name in ("Wp", "bp", "bl", "h0/b1", "h0/b5", "h3/W1", "h2/b5"):
+        idx.append(lay[name][0])
+    o = lay["Wl"][0]
     idx += [o + 5 * 800 + 3, o + 100 * 800 + 250, o + 242 * 800 + 799, o + 42 * 800 + 420]   # x and h rows, all gates
     h = 1e-6
     for k in idx:

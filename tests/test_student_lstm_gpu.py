@@ -25,10 +25,10 @@ def _batch(T, B, seed=0):
     return ob, prev, t
 
 
-def _params(seed=6):
-    p = ln.init(seed)
+def _params(seed=6, T=10):
+    p = ln.init(seed, T)
     rs = np.random.RandomState(seed + 1)
-    for k, (o, s) in ln.LAYOUT.items():
+    for k, (o, s) in ln.layout(T)[0].items():
         if len(s) == 1:
             p[o:o + s[0]] = rs.uniform(-.1, .1, s[0]).astype(np.float32)
     return p
@@ -37,7 +37,7 @@ def _params(seed=6):
 def _trainer(T=10, B=20, loss="kl", params=None, **kw):
     from reacherdistilation_amd.student_lstm import StudentLstmConfig, StudentLstmTrainer
     return StudentLstmTrainer(StudentLstmConfig(loss=loss, steps=T, max_windows=B, **kw), device=DEV,
-                              params=_params() if params is None else params)
+                              params=_params(T=T) if params is None else params)
 
 
 def _t(x):
@@ -325,7 +325,7 @@ def test_fused_head_matches_the_layer_gemms(T, B):
         out[mode] = (y.cpu().numpy(), g)
         tr.close()
     assert np.array_equal(out["1"][0], out["0"][0])
-    w1 = ln.LAYOUT["W1"][0]   # the head's [W1 b1 ... W5 b5] range starts here
+    w1 = ln.CELL_PARAMS   # the heads' [W1 b1 ... W5 b5] x T range starts here
     assert np.array_equal(out["1"][1][:w1], out["0"][1][:w1])
     h1, h0 = out["1"][1][w1:], out["0"][1][w1:]
     assert np.abs(h1 - h0).max() <= 1e-5 * np.abs(h0).max()
