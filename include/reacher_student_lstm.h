@@ -60,7 +60,8 @@ typedef struct {
 } rdl_config;
 
 /* rdl_config.kernels: by default at most 32 windows run the whole recurrence / BPTT as one
- * persistent launch each and at most 2,048 rows run the head as one launch; these bits keep
+ * persistent launch each and at most 16,384 rows run the heads as one launch each way (when
+ * their partial rows fit 256 MB at max_windows); these bits keep
  * the per-step recurrence launches / the per-layer head GEMMs at any size. */
 #define RDL_KERNELS_STEP_RECURRENCE 1
 #define RDL_KERNELS_LAYER_HEAD 2

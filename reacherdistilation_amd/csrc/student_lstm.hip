@@ -595,7 +595,8 @@ __global__ __launch_bounds__(256) void dense32_grad_kernel(const float* __restri
 // workgroup: activations stay in LDS between layers, weights stream from L2 as the B
 // operands, and every layer's output is also stored (A1..A4 for the backward, Y).  Same MFMA
 // k order and epilogue (acc + b, tanhf) as the unsplit rd_gemm launches it replaces.
-constexpr int HF_ROWS = 16, HF_MAX_ROWS = 2048;
+constexpr int HF_ROWS = 16, HF_MAX_ROWS = 1 << 18;
+constexpr int64_t HPART_MAX_FLOATS = (int64_t)512 << 20;   // the fused head's partial rows: at most 2 GB
 template <int K, int N, bool TANH, int LI, int LO>
 __device__ __forceinline__ void head_layer(const float (*in)[LI], float (*out)[LO], const float* __restrict__ W,
                                            const float* __restrict__ b, float* __restrict__ gout, int ldg,
@@ -990,6 +991,7 @@ struct rdl_trainer {
     float *D32 = nullptr, *D64a = nullptr, *D128 = nullptr, *D64b = nullptr, *dHh = nullptr, *dP = nullptr;
     float *dhn = nullptr, *dc = nullptr;
     float *split = nullptr, *colws = nullptr, *lpart = nullptr, *hist = nullptr;
+    float* hpart = nullptr;    // fused head backward: one partial row of HB_PART per (step, 16 rows)
     int64_t colws_floats = 0;
     uint32_t* ctl = nullptr;
     uint32_t* bar = nullptr;   // persistent kernels: [0] forward / [1] BPTT barrier arrivals, [2] timeout flag
@@ -1064,9 +1066,10 @@ int pr_dbg() {   // diagnostic builds: RDL_PR_DBG bit 0 skips the exchange loads
 }
 
 bool fused_head(const rdl_trainer* t, int64_t R) {
-    // the partial rows of its T x ceil(B / 16) workgroups live in the split-K buffer
-    const int64_t nwg = (int64_t)t->T * ((R / t->T + HF_ROWS - 1) / HF_ROWS);
-    return !(t->cfg.kernels & RDL_KERNELS_LAYER_HEAD) && R <= HF_MAX_ROWS && nwg * HB_PART <= SPLIT_FLOATS;
+    // the partial rows of its T x ceil(B / 16) workgroups live in hpart (sized at create for
+    // max_windows when that fits HPART_MAX_FLOATS); with one head per step, the per-layer path
+    // is T x 11 launches, so the fused head now covers up to 16,384 rows
+    return !(t->cfg.kernels & RDL_KERNELS_LAYER_HEAD) && t->hpart && R <= HF_MAX_ROWS;
 }
 
 bool persistent(const rdl_trainer* t, int64_t B) {
@@ -1169,10 +1172,10 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
         const int nb = (int)((B + HF_ROWS - 1) / HF_ROWS);
         hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)(T * nb)), dim3(256), 0, t->stream, Hc, P,
                            (const float*)t->A1, (const float*)t->A2, (const float*)t->A3, (const float*)t->A4,
-                           (const float*)t->dY, t->dHh, t->split, B, nb);
+                           (const float*)t->dY, t->dHh, t->hpart, B, nb);
         RDL_CK(hipGetLastError(), "rdl head_bwd_kernel");
         hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((HB_PART + 255) / 256, (unsigned)T), dim3(256), 0, t->stream,
-                           (const float*)t->split, nb, g);
+                           (const float*)t->hpart, nb, g);
         RDL_CK(hipGetLastError(), "rdl head_wgrad_reduce_kernel");
     } else {
     // step s's head backward over its B rows (weight gradients; data gradients with the tanh
@@ -1332,6 +1335,8 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     alloc(&t->dhn, B * U);
     alloc(&t->dc, B * U);
     alloc(&t->split, SPLIT_FLOATS);
+    const int64_t hp = (int64_t)t->T * ((t->Bmax + HF_ROWS - 1) / HF_ROWS) * HB_PART;
+    if (hp <= HPART_MAX_FLOATS) alloc(&t->hpart, hp);
     alloc(&t->colws, t->colws_floats);
     alloc(&t->lpart, 2 * ((R + LOSS_BLOCK - 1) / LOSS_BLOCK));
     alloc(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
@@ -1369,7 +1374,7 @@ int rdl_destroy(rdl_trainer* t) {
     rd::DeviceGuard dg(t->device);
     float* bufs[] = {t->params, t->m, t->v, t->own_grad, t->X, t->H, t->Cs, t->Z, t->G, t->A1, t->A2, t->A3, t->A4,
                      t->Y, t->dY, t->D32, t->D64a, t->D128, t->D64b, t->dHh, t->dP, t->dhn, t->dc, t->split,
-                     t->colws, t->lpart, t->hist, t->bpart, t->qbuf};
+                     t->colws, t->lpart, t->hist, t->bpart, t->qbuf, t->hpart};
     for (float* p : bufs)
         if (p) (void)hipFree(p);
     if (t->ctl) (void)hipFree(t->ctl);

@@ -103,7 +103,7 @@ class StudentLstmConfig:
     init_seed: int = 3
     metrics_len: int = 4096
     step_recurrence: bool = False     # force the per-step recurrence launches (else: persistent at <= 32 windows)
-    layer_head: bool = False          # force the per-layer head GEMMs (else: one launch at <= 2,048 rows)
+    layer_head: bool = False          # force the per-layer head GEMMs (else: one launch at <= 16,384 rows)
 
 
 class StudentLstmTrainer:

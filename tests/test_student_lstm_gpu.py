@@ -310,7 +310,7 @@ def test_persistent_recurrence_matches_per_step_launches(T, B, with_state):
 
 @pytest.mark.parametrize("T,B", [(10, 20), (3, 130), (1, 5)])
 def test_fused_head_matches_the_layer_gemms(T, B):
-    """At most 2,048 rows: the head's forward is one launch (head_fwd_kernel) and its backward
+    """At most 16,384 rows: the heads' forward is one launch (head_fwd_kernel) and its backward
     two (head_bwd_kernel + a fixed-order reduce).  Same MFMA k order and epilogues as the
     per-layer GEMMs for the activations and the data gradients, so the outputs, dh_head and
     everything BPTT derives from it (the LSTM's gradients) are bitwise those of
