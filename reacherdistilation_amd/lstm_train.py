@@ -18,7 +18,6 @@ broadcasts at 0 or >= T-1 records.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -36,7 +35,7 @@ def _restore(st, restore: bool, path: str | None, log):
     prints, as the reference does."""
     if not restore:
         return
-    if path and os.path.exists(path):
+    if path and st.checkpoint_exists(path):
         st.load(path)
     else:
         log("attempt to restore trained data but {0} does not exist".format(path))

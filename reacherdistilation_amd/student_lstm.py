@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -162,29 +163,55 @@ class StudentLstmTrainer:
         nat.check(self._lib.rdl_get_params(self._h, nat.ptr(out)), "rdl_get_params")
         return out
 
-    def save(self, path: str):
-        """tf.train.Saver(var_list=LSTM/*).save (reference lstm_train.py:86-87,199): the
-        parameters and the Adam slots m, v, as a safetensors file (nothing executable)."""
-        from safetensors.torch import save_file
+    def _slots(self):
         m = torch.empty(self.n_params, dtype=torch.float32, device=self.device)
         v = torch.empty_like(m)
         self._sync_stream()
         nat.check(self._lib.rdl_get_slots(self._h, nat.ptr(m), nat.ptr(v)), "rdl_get_slots")
         torch.cuda.current_stream(self.device).synchronize()
-        save_file({"params": self.params().cpu(), "adam_m": m.cpu(), "adam_v": v.cpu()}, path)
+        return m, v
+
+    def save(self, path: str):
+        """tf.train.Saver(var_list=LSTM/*).save (reference lstm_train.py:86-87,199): the
+        parameters and the Adam slots m, v.  A path ending in '.safetensors' is written as one
+        safetensors file; any other path is a TF checkpoint prefix (``path.index`` +
+        ``path.data-00000-of-00001``, the reference's own format and variable names,
+        tf_checkpoint.save_lstm).  Nothing executable either way."""
+        m, v = self._slots()
+        p = self.params()
+        if path.endswith(".safetensors"):
+            from safetensors.torch import save_file
+            save_file({"params": p.cpu(), "adam_m": m.cpu(), "adam_v": v.cpu()}, path)
+        else:
+            from . import tf_checkpoint
+            tf_checkpoint.save_lstm(path, p.cpu().numpy(), m.cpu().numpy(), v.cpu().numpy(), self.T)
+
+    @staticmethod
+    def checkpoint_exists(path: str) -> bool:
+        from . import tf_checkpoint
+        return os.path.exists(path) if path.endswith(".safetensors") else tf_checkpoint.exists(path)
 
     def load(self, path: str):
         """saver.restore (reference lstm_train.py:102-107): parameters and Adam slots from
-        `path`; the beta powers and step counter start afresh, as the reference initialises
-        the Adam variables before restoring the 'LSTM' scope (:99-105)."""
-        from safetensors.torch import load_file
-        d = load_file(path)
-        if d["params"].numel() != self.n_params:
-            raise ValueError(f"{path}: {d['params'].numel()} parameters, expected {self.n_params}")
+        `path` (format by suffix, as save); the beta powers and step counter start afresh, as
+        the reference initialises the Adam variables before restoring the 'LSTM' scope
+        (:99-105).  A TF checkpoint without Adam slots restores the parameters and zero slots."""
+        if path.endswith(".safetensors"):
+            from safetensors.torch import load_file
+            d = load_file(path)
+            p, m, v = d["params"], d["adam_m"], d["adam_v"]
+        else:
+            from . import tf_checkpoint
+            p, m, v = tf_checkpoint.load_lstm(path, self.T)
+            p = torch.from_numpy(p)
+            m = torch.zeros_like(p) if m is None else torch.from_numpy(m)
+            v = torch.zeros_like(p) if v is None else torch.from_numpy(v)
+        if p.numel() != self.n_params:
+            raise ValueError(f"{path}: {p.numel()} parameters, expected {self.n_params}")
         self.reset_optimizer()
-        self.set_params(d["params"])
-        m = d["adam_m"].to(self.device, torch.float32).contiguous()
-        v = d["adam_v"].to(self.device, torch.float32).contiguous()
+        self.set_params(p)
+        m = m.to(self.device, torch.float32).contiguous()
+        v = v.to(self.device, torch.float32).contiguous()
         self._sync_stream()
         nat.check(self._lib.rdl_set_slots(self._h, nat.ptr(m), nat.ptr(v)), "rdl_set_slots")
         torch.cuda.current_stream(self.device).synchronize()

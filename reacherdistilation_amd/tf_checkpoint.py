@@ -416,3 +416,70 @@ def save_teacher(prefix: str, p: MlpPolicyParams, vf: dict | None = None, count:
         shape = dict((n, s) for n, s, _ in TEACHER_VARS)[name]
         out[name] = np.asarray(p[key], np.float32).reshape(shape)
     write(prefix, out)
+
+
+# ------------------------------------------------------------------ the LSTM student (scope 'LSTM')
+# lstm_train.py:86-87 saves / restores tf.train.Saver(var_list=<GLOBAL_VARIABLES in scope 'LSTM'>):
+# the student's variables and their Adam slots ('<var>/Adam' = m, '<var>/Adam_1' = v; the beta
+# powers live in scope 'adam' and are not saved).  Variable names follow TF1's layer naming in
+# student_lstm_graph (student_nn.py:21-49): the prev-pdflat dense is the scope's first
+# tf.layers.dense ('dense'), the cell 'unique_lstm_cell', and step t's five head layers the
+# un-reused calls 5t+1 .. 5t+5 ('dense_1' ..).  The cell's name matches the reference's logged
+# GraphDef (LSTM/unique_lstm_cell/kernel); the dense names follow TF1's uniquing rule (the
+# logged graph is an older variant with named per-step layers), so they are unpinned.
+def lstm_variables(T: int):
+    """[(checkpoint name, flat offset, shape)] of the student in its flat order
+    (student_lstm.shapes)."""
+    from .student_lstm import CELL_SHAPES, HEAD_SHAPES, shapes
+    names = {"Wp": "LSTM/dense/kernel", "bp": "LSTM/dense/bias", "Wl": "LSTM/unique_lstm_cell/kernel",
+             "bl": "LSTM/unique_lstm_cell/bias"}
+    out, off = [], 0
+    for key, shp in shapes(T):
+        if "/" in key:   # h{t}/W{k} or h{t}/b{k}
+            t, layer = key.split("/")
+            k = int(layer[1:])
+            name = f"LSTM/dense_{5 * int(t[1:]) + k}/{'kernel' if layer[0] == 'W' else 'bias'}"
+        else:
+            name = names[key]
+        out.append((name, off, tuple(shp)))
+        off += int(np.prod(shp))
+    assert len(out) == len(CELL_SHAPES) + len(HEAD_SHAPES) * T
+    return out
+
+
+def save_lstm(prefix: str, params, m=None, v=None, T: int = 10) -> None:
+    """The flat parameters (and Adam slots m, v) as the reference's 'LSTM'-scope checkpoint."""
+    params = np.asarray(params, np.float32).ravel()
+    out = {}
+    for name, off, shp in lstm_variables(T):
+        n = int(np.prod(shp))
+        out[name] = params[off:off + n].reshape(shp)
+        for suffix, slot in (("/Adam", m), ("/Adam_1", v)):
+            if slot is not None:
+                out[name + suffix] = np.asarray(slot, np.float32).ravel()[off:off + n].reshape(shp)
+    write(prefix, out)
+
+
+def load_lstm(prefix: str, T: int = 10):
+    """(params, m, v) flat float32 arrays from an 'LSTM'-scope checkpoint (m / v None when the
+    checkpoint holds no Adam slots)."""
+    t = read(prefix)
+    var = lstm_variables(T)
+    n = var[-1][1] + int(np.prod(var[-1][2]))
+    missing = [name for name, _, _ in var if name not in t]
+    if missing:
+        raise KeyError(f"{prefix}: not a T = {T} LSTM-student checkpoint, missing {missing[:4]}"
+                       f"{' ...' if len(missing) > 4 else ''}")
+    out = []
+    for suffix in ("", "/Adam", "/Adam_1"):
+        if suffix and any(name + suffix not in t for name, _, _ in var):
+            out.append(None)
+            continue
+        flat = np.zeros(n, np.float32)
+        for name, off, shp in var:
+            a = t[name + suffix]
+            if tuple(a.shape) != shp:
+                raise ValueError(f"{name + suffix}: shape {a.shape}, expected {shp}")
+            flat[off:off + a.size] = a.astype(np.float32).ravel()
+        out.append(flat)
+    return tuple(out)

@@ -239,21 +239,25 @@ def test_bptt_variant_driver_runs():
     assert all(np.isfinite(losses)) and all(x > 0 for x in losses)
 
 
-def test_checkpoint_round_trip(tmp_path):
-    """save/load = the reference's Saver over the 'LSTM' scope (lstm_train.py:86-107,199):
-    params and Adam slots come back bitwise; the beta powers and step counter start afresh,
-    so the restored trainer's next step equals a fresh optimiser's first step from the same
-    params and slots."""
+@pytest.mark.parametrize("fmt", ["lstm.safetensors", "lstm_with_keep_probability_1.0.ckpt"])
+def test_checkpoint_round_trip(tmp_path, fmt):
+    """save/load = the reference's Saver over the 'LSTM' scope (lstm_train.py:86-107,199), as a
+    safetensors file or as a TF checkpoint with the reference's variable names: params and
+    Adam slots come back bitwise; the beta powers and step counter start afresh, so the
+    restored trainer's next step equals a fresh optimiser's first step from the same params
+    and slots."""
     T, B = 10, 20
     ob, prev, t = _batch(T, B, 51)
     a = _trainer(T, B, "kl")
     for _ in range(3):
         a.step(_t(ob), _t(prev), _t(t))
-    path = str(tmp_path / "lstm.safetensors")
+    path = str(tmp_path / fmt)
     a.save(path)
+    m0, v0 = (x.cpu().numpy() for x in a._slots())
     b = _trainer(T, B, "kl", params=ln.init(99))
     b.load(path)
     assert torch.equal(a.params(), b.params()) and b.counter() == 0
+    assert all(torch.equal(x.cpu(), torch.from_numpy(y)) for x, y in zip(b._slots(), (m0, v0)))
     # the next step from the restored state: m, v carried over, beta powers from t = 1
     p0 = b.params().cpu().numpy().copy()
     fw = ln.forward(p0, ob, prev)
@@ -261,10 +265,7 @@ def test_checkpoint_round_trip(tmp_path):
     g = b.rollout(_t(ob), _t(prev), _t(t)).cpu().numpy()
     _grad_check(g, ln.backward(p0, fw, d))
     b.apply()
-    from safetensors.torch import load_file
-    ck = load_file(path)
-    m = ck["adam_m"].numpy().astype(np.float32)
-    v = ck["adam_v"].numpy().astype(np.float32)
+    m, v = m0, v0
     m = m + (g - m) * np.float32(0.1)
     v = v + (g * g - v) * np.float32(0.001)
     alpha = np.float32(1e-3) * np.sqrt(np.float32(1) - np.float32(0.999)) / (np.float32(1) - np.float32(0.9))
@@ -272,9 +273,10 @@ def test_checkpoint_round_trip(tmp_path):
     np.testing.assert_allclose(b.params().cpu().numpy(), want, atol=1e-6, rtol=1e-5)
 
 
-def test_driver_restores_and_saves_the_student(tmp_path):
+@pytest.mark.parametrize("name", ["student.safetensors", "student.ckpt"])
+def test_driver_restores_and_saves_the_student(tmp_path, name):
     from reacherdistilation_amd import lstm_train
-    path = str(tmp_path / "student.safetensors")
+    path = str(tmp_path / name)
     msgs = []
     st, _, _ = lstm_train.train(episodes=4, warmup_episodes=2, restore=True, student_path=path, log=msgs.append)
     assert any("does not exist" in m for m in msgs)       # first run: nothing to restore, only a message

@@ -165,3 +165,43 @@ def test_load_teacher_rejects_other_checkpoints(tmp_path):
     with pytest.raises(ValueError, match="floor"):
         tc.save_teacher(str(tmp_path / "t.ckpt"), MlpPolicyParams(np.zeros(5060, np.float32), np.zeros(11, np.float32),
                                                                   np.full(11, 0.01, np.float32)))
+
+
+def test_lstm_saver_layout_matches_the_reference_graph(ref_graph):
+    """The reference's 'LSTM'-scope Saver (save_1/SaveV2 of its logged GraphDef, an older
+    per-step-named variant of student_lstm_graph) saves every variable of the scope together
+    with its '/Adam' and '/Adam_1' slots and nothing else; the cell is 'unique_lstm_cell'.
+    save_lstm writes the same structure for the current graph."""
+    nodes = ref_graph.nodes
+    saved = nodes["save_1/SaveV2"]["inputs"][3:]
+    lstm = sorted(n for n, v in nodes.items() if v["op"] == "VariableV2" and n.startswith("LSTM/"))
+    assert saved == lstm
+    base = [n for n in lstm if not n.endswith(("/Adam", "/Adam_1"))]
+    assert sorted(b + s for b in base for s in ("", "/Adam", "/Adam_1")) == lstm
+    assert "LSTM/unique_lstm_cell/kernel" in base
+    names = {n for n, _, _ in tc.lstm_variables(10)}
+    assert "LSTM/unique_lstm_cell/kernel" in names and "LSTM/unique_lstm_cell/bias" in names
+
+
+def test_lstm_round_trip(tmp_path):
+    from reacherdistilation_amd import student_lstm as sl
+    T = 3
+    n = sl.n_params(T)
+    rs = np.random.RandomState(5)
+    p, m, v = (rs.standard_normal(n).astype(np.float32) for _ in range(3))
+    pre = str(tmp_path / "lstm_with_keep_probability_1.0.ckpt")
+    tc.save_lstm(pre, p, m, v, T)
+    raw = tc.read(pre)
+    var = tc.lstm_variables(T)
+    assert len(var) == 4 + 10 * T and len(raw) == 3 * len(var)
+    assert raw["LSTM/unique_lstm_cell/kernel"].shape == (243, 800)
+    assert raw["LSTM/dense_15/bias"].shape == (4,)        # step 2's output layer (calls 11 .. 15)
+    o = dict((k, (off, s)) for k, off, s in var)["LSTM/dense_6/kernel"]   # step 1's first layer
+    assert np.array_equal(raw["LSTM/dense_6/kernel"].ravel(), p[o[0]:o[0] + 200 * 64])
+    q, qm, qv = tc.load_lstm(pre, T)
+    assert np.array_equal(q, p) and np.array_equal(qm, m) and np.array_equal(qv, v)
+    tc.save_lstm(pre, p, T=T)                              # no slots: parameters only
+    q, qm, qv = tc.load_lstm(pre, T)
+    assert np.array_equal(q, p) and qm is None and qv is None
+    with pytest.raises(KeyError, match="missing"):
+        tc.load_lstm(pre, T + 1)
