@@ -85,6 +85,35 @@ class DeviceDataset:
                   out=self.curr[self.curr_len])
         self.curr_len += 1
 
+    def write_episodes(self, rec: torch.Tensor, lens=None) -> int:
+        """Append a block of whole episodes, rec [E, EPISODE_STEPS, 21] (the ring's record
+        layout), as E write() x 50 + flush() calls would (batched collectors,
+        teacher.collect_reward); ``lens`` gives incomplete episodes' record counts.  Returns E."""
+        if self.curr_len:
+            raise RuntimeError("write_episodes: an episode is open; flush() first")
+        rec = rec.to(self.device, torch.float32)
+        if rec.dim() != 3 or rec.shape[1:] != (EPISODE_STEPS, REC):
+            raise ValueError(f"rec must be [E, {EPISODE_STEPS}, {REC}], not {tuple(rec.shape)}")
+        E = rec.shape[0]
+        lens = [EPISODE_STEPS] * E if lens is None else [int(x) for x in lens]
+        if len(lens) != E:
+            raise ValueError("lens: one length per episode")
+        first = max(0, E - self.capacity)   # the ring keeps the newest `capacity` of them
+        self.num_total_episodes += first
+        keep, kl = rec[first:], lens[first:]
+        s0 = self.num_total_episodes % self.capacity
+        k = min(len(kl), self.capacity - s0)   # contiguous slots s0.., then from slot 0
+        self.ring[s0:s0 + k].copy_(keep[:k])
+        if len(kl) > k:
+            self.ring[:len(kl) - k].copy_(keep[k:])
+        slots = [(s0 + q) % self.capacity for q in range(len(kl))]
+        for slot, ln in zip(slots, kl):
+            self.lens[slot] = ln
+        new = set(slots)   # data_in_memory: the overwritten episodes leave it
+        self._mem_slots = [x for x in self._mem_slots if x not in new] + slots
+        self.num_total_episodes += len(kl)
+        return E
+
     def _field(self, x, n):
         if x is None:
             return self._zeros[:n]

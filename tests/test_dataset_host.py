@@ -120,3 +120,33 @@ def test_bptt_windows_slide_by_one_step_over_fixed_episodes():
         assert np.array_equal(t[..., 1].numpy(), step.astype(np.float32))
         assert np.array_equal(prev[..., 1].numpy(), np.where(step > 0, step - 1, 0).astype(np.float32))
     assert list(DeviceDataset(device="cpu").bptt_batches()) == []
+
+
+@pytest.mark.parametrize("cap,before,block", [(8, 0, 5), (8, 6, 5), (4, 1, 11), (5, 3, 5)])
+def test_write_episodes_equals_write_and_flush(cap, before, block):
+    """The batched append (teacher.collect_reward) leaves the ring, lengths, episode count and
+    data_in_memory as the same episodes written record by record and flushed would, through
+    ring wrap-around and blocks larger than the ring."""
+    a = DeviceDataset(capacity=cap, device="cpu")
+    b = DeviceDataset(capacity=cap, device="cpu")
+    _fill(a, before)
+    _fill(b, before)
+    c = DeviceDataset(capacity=block + 1, device="cpu")
+    for e in range(block):
+        for k in range(50 if e % 3 else 37):            # some incomplete episodes
+            c.write(ob=np.full(11, 1000.0 + 100 * e + k), reward=0.25 * k, t_pdflat=np.array([e, k, 1, 2], float))
+        c.flush()
+    for e in range(block):
+        for k in range(c.lens[e]):
+            a.write(ob=c.ring[e, k, :11], reward=c.ring[e, k, 11], t_pdflat=c.ring[e, k, 12:16])
+        a.flush()
+    assert b.write_episodes(c.ring[:block], c.lens[:block]) == block
+    assert a.num_episodes() == b.num_episodes() == before + block
+    assert torch.equal(a.ring, b.ring) and a.lens == b.lens
+    assert sorted(a._mem_slots) == sorted(b._mem_slots)
+    assert [a.lens[s] for s in a._mem_slots[-min(block, cap):]] == [b.lens[s] for s in b._mem_slots[-min(block, cap):]]
+    with pytest.raises(ValueError):
+        b.write_episodes(torch.zeros(2, 49, 21))
+    b.write(ob=np.ones(11))
+    with pytest.raises(RuntimeError):
+        b.write_episodes(c.ring[:1])
