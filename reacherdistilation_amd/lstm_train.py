@@ -54,7 +54,7 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = TOTAL_EP
     (driver_env.DriverEnv; gym_env=True through the gym-API env), window losses read once per
     episode."""
     env = DriverEnv(seed, device, gym_api=gym_env)
-    teacher = TeacherAgent(restore=restore, path=teacher_path)
+    teacher = TeacherAgent(restore=teacher_path is not None, path=teacher_path)   # always restored (ref. :29)
     tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
     st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
                                               steps=STEPS_UNROLLED, max_windows=LSTM_BATCH_SIZE), device=device)
@@ -123,7 +123,7 @@ def train_bptt(train: bool = True, restore: bool = False, *, episodes: int = TOT
     Returns (student trainer, dataset, per-episode summed training loss).  Env I/O as in
     train()."""
     env = DriverEnv(seed, device, gym_api=gym_env)
-    teacher = TeacherAgent(restore=restore, path=teacher_path)
+    teacher = TeacherAgent(restore=teacher_path is not None, path=teacher_path)   # always restored (ref. :29)
     tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=device, teacher=teacher.pi)
     st = StudentLstmTrainer(StudentLstmConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed,
                                               steps=STEPS_UNROLLED, max_windows=LSTM_BATCH_SIZE), device=device)

@@ -53,7 +53,7 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
     if student not in ("policy", "mlp"):
         raise ValueError(f"unknown student {student!r}")
     env = DriverEnv(seed, device, gym_api=gym_env)
-    teacher = TeacherAgent(restore=restore, path=teacher_path)
+    teacher = TeacherAgent(restore=teacher_path is not None, path=teacher_path)   # always restored (ref. :29)
     tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr), device=device, teacher=teacher.pi)
     sm = StudentMlpTrainer(StudentMlpConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed),
                            device=device) if student == "mlp" else None
