@@ -8,7 +8,9 @@
 Paths as the reference's config.py:40-45 and teacher.py:20, under ``--data-dir`` (default
 ~/reacher/data): the LSTM checkpoint ``lstm_with_keep_probability_{KEEP}.ckpt`` (a TF
 checkpoint, tf_checkpoint), the teacher ``teacher.ckpt`` (restored when present, else the
-synthetic teacher, with a message) and the dataset pages ``dataset_kp_{KEEP}/``.  Fixed here:
+synthetic teacher, with a message) and the run's dataset pages
+``<date>/<time>/{lstm,mlp}/dataset_kp_{KEEP}/``.  Both drivers train with the keep
+probability (``-k``, default config KEEP_PROB; lstm_train.py:150, mlp_train.py:151).  Fixed here:
 ``-k`` reaches the LSTM driver (the reference's ``global KEEP_PROB`` in main.py:17-19 never
 does), and ``-ch`` prints the tensors (main.py:23 calls an undefined ``chkp``).  Added:
 ``--episodes``, ``--warmup``, ``--device``, ``--data-dir``.
@@ -16,18 +18,24 @@ does), and ``-ch`` prints the tensors (main.py:23 calls an undefined ``chkp``). 
 from __future__ import annotations
 
 import argparse
+import datetime
 import os
 import sys
 
 import numpy as np
 
-from .config import KEEP_PROB, LSTM_BATCH_SIZE, MLP_BATCH_SIZE, MLP_EPISODE_BUDGET, TOTAL_EPISODES
+from .config import KEEP_PROB, MLP_EPISODE_BUDGET, TOTAL_EPISODES
 
 
-def paths(data_dir: str, keep: float) -> dict:
+def paths(data_dir: str, keep: float, stamp: str | None = None) -> dict:
+    """config.py:14-15,36-45 and mlp_train.py:101-106: the dataset pages of a run go to a new
+    <date>/<time>/{lstm,mlp}/dataset_kp_<keep> directory."""
+    stamp = stamp or datetime.datetime.now().strftime("%Y%m%d/%H%M%S")
+    run = os.path.join(data_dir, *stamp.split("/"))
     return {"lstm": os.path.join(data_dir, f"lstm_with_keep_probability_{keep}.ckpt"),
             "teacher": os.path.join(data_dir, "teacher.ckpt"),
-            "dataset": os.path.join(data_dir, f"dataset_kp_{keep}")}
+            "dataset_lstm": os.path.join(run, "lstm", f"dataset_kp_{keep}"),
+            "dataset_mlp": os.path.join(run, "mlp", f"dataset_kp_{keep}")}
 
 
 def print_tensors(prefix: str, out=print) -> None:
@@ -65,19 +73,17 @@ def main(argv=None, log=print) -> int:
     teacher = p["teacher"] if tf_checkpoint.exists(p["teacher"]) else None
     if teacher is None:
         log(f"teacher checkpoint {p['teacher']} not found: using the synthetic teacher")
-    os.makedirs(p["dataset"], exist_ok=True)
+    extra = {} if args.warmup is None else {"warmup_episodes": args.warmup}
     if args.lstm_train:
         from . import lstm_train
-        kw = {} if args.warmup is None else {"warmup_episodes": args.warmup}
         lstm_train.train(True, args.restore, episodes=args.episodes or TOTAL_EPISODES, keep_prob=keep,
-                         device=args.device, teacher_path=teacher, student_path=p["lstm"], store_dir=p["dataset"],
-                         log=log, **{"warmup_episodes": 2 * LSTM_BATCH_SIZE, **kw})
+                         device=args.device, teacher_path=teacher, student_path=p["lstm"],
+                         store_dir=p["dataset_lstm"], log=log, **extra)
     else:
         from . import mlp_train
-        kw = {} if args.warmup is None else {"warmup_episodes": args.warmup}
-        mlp_train.train(True, args.restore, episodes=args.episodes or MLP_EPISODE_BUDGET, device=args.device,
-                        teacher_path=teacher, student="mlp", store_dir=p["dataset"], log=log,
-                        **{"warmup_episodes": 2 * MLP_BATCH_SIZE, **kw})
+        mlp_train.train(True, args.restore, episodes=args.episodes or MLP_EPISODE_BUDGET, keep_prob=keep,
+                        device=args.device, teacher_path=teacher, student="mlp", store_dir=p["dataset_mlp"],
+                        log=log, **extra)
     return 0
 
 

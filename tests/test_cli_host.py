@@ -7,9 +7,10 @@ from reacherdistilation_amd import tf_checkpoint as tc
 
 
 def test_paths_follow_the_reference_config():
-    p = cli.paths("/d", 0.5)   # config.py:40-45, teacher.py:20
-    assert p["lstm"] == "/d/lstm_with_keep_probability_0.5.ckpt"
-    assert p["teacher"] == "/d/teacher.ckpt" and p["dataset"] == "/d/dataset_kp_0.5"
+    p = cli.paths("/d", 0.5, "20261017/120000")   # config.py:14-15,36-45, teacher.py:20, mlp_train.py:101-106
+    assert p["lstm"] == "/d/lstm_with_keep_probability_0.5.ckpt" and p["teacher"] == "/d/teacher.ckpt"
+    assert p["dataset_lstm"] == "/d/20261017/120000/lstm/dataset_kp_0.5"
+    assert p["dataset_mlp"] == "/d/20261017/120000/mlp/dataset_kp_0.5"
 
 
 def test_check_prints_every_tensor(tmp_path):
