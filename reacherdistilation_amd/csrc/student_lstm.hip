@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 
 #include "../../include/reacher_student_lstm.h"
@@ -634,17 +635,17 @@ __device__ __forceinline__ void head_layer(const float (*in)[LI], float (*out)[L
 // load of the thread issued before its first LDS store (one round trip, not one per element)
 template <int COLS, int LDD>
 __device__ __forceinline__ void head_stage(const float* __restrict__ src, int ld, int64_t row0, int64_t R,
-                                           float (*dst)[LDD]) {
+                                           float (*dst)[LDD], int tid) {
     constexpr int PER = (HF_ROWS * COLS + 255) / 256;
     float v[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int x = threadIdx.x + 256 * j, row = x / COLS, c = x - row * COLS;
+        const int x = tid + 256 * j, row = x / COLS, c = x - row * COLS;
         v[j] = (x < HF_ROWS * COLS && row0 + row < R) ? src[(row0 + row) * ld + c] : 0.0f;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int x = threadIdx.x + 256 * j, row = x / COLS, c = x - row * COLS;
+        const int x = tid + 256 * j, row = x / COLS, c = x - row * COLS;
         if (x < HF_ROWS * COLS) dst[row][c] = v[j];
     }
 }
@@ -662,7 +663,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
     const int ts = blockIdx.x / nb, rb = blockIdx.x - ts * nb;
     const int64_t row0 = (int64_t)ts * B + (int64_t)rb * HF_ROWS, R = (int64_t)(ts + 1) * B;
     const float* P = P0 + OFF_H + (int64_t)ts * HSZ;   // step ts's head
-    head_stage<U, U + 4>(Hc, U, row0, R, X0);
+    head_stage<U, U + 4>(Hc, U, row0, R, X0, threadIdx.x);
     __syncthreads();
     head_layer<U, H1, true>(X0, X1, P + OFF_W1, P + OFF_B1, A1, L1, row0, R);
     head_layer<H1, H2, true>(X1, X2, P + OFF_W2, P + OFF_B2, A2, L2, row0, R);
@@ -680,8 +681,9 @@ constexpr int HB_PART = HSZ;   // 31,652 floats: [W1;b1][W2;b2][W3;b3][W4;b4][W5
 // dIn[16][NI] = (dOut[16][KO] . W^T) (* (1 - act^2) when DT); W is [NI][KO] (layer input x output)
 template <int KO, int NI, bool DT, int LD, int LI, int LA>
 __device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)[LI], const float (*act)[LA],
-                                           const float* __restrict__ W, float* gout, int ldg, int64_t row0, int64_t R) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
+                                           const float* __restrict__ W, float* gout, int ldg, int64_t row0, int64_t R,
+                                           int tid) {
+    const int wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     constexpr int NB = (NI + 15) / 16;
 #pragma unroll
     for (int it = 0; it < (NB + 3) / 4; ++it) {   // unrolled: every weight load of the layer in flight at once
@@ -711,7 +713,7 @@ __device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)
     }
 }
 // part[m][n] = sum over the 16 rows of act[row][m] d[row][n], m < M (the last input row is the
-// ones column: the bias gradient), n < N
+// ones column: the bias gradient), n < N (one tile of rows: head_bwd_kernel<false>)
 template <int M, int N, int LA, int LD>
 __device__ __forceinline__ void head_wgrad(const float (*act)[LA], const float (*d)[LD], float* __restrict__ part) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
@@ -732,12 +734,56 @@ __device__ __forceinline__ void head_wgrad(const float (*act)[LA], const float (
         }
     }
 }
+// acc += sum over the 16 rows of act[row][m] d[row][n], m < M (the last input row is the ones
+// column: the bias gradient), n < N: 16x16 output tiles t = wave, wave + 4, ...; the
+// accumulators stay in registers over a workgroup's tiles of rows (head_bwd_kernel)
+template <int M, int N>
+constexpr int wq() { return (((M + 15) / 16) * ((N + 15) / 16) + 3) / 4; }
+template <int M, int N, int LA, int LD>
+__device__ __forceinline__ void head_wgrad_acc(const float (*act)[LA], const float (*d)[LD],
+                                               rdg::f32x4 (&acc)[wq<M, N>()], int tid) {
+    const int wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
+    constexpr int MB = (M + 15) / 16, NB = (N + 15) / 16;
+#pragma unroll
+    for (int q = 0; q < wq<M, N>(); ++q) {
+        const int t = wave + 4 * q;
+        if (t >= MB * NB) break;
+        const int m0 = 16 * (t / NB), n0 = 16 * (t % NB);
+        const int mc = m0 + i < M ? m0 + i : M - 1, nc = n0 + i < N ? n0 + i : N - 1;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = 4 * s + gq;
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(act[k][mc], d[k][nc], acc[q], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one tile's LDS operands live at a time
+    }
+}
+// part[m][n] = the accumulated tiles
+template <int M, int N>
+__device__ __forceinline__ void head_wgrad_store(const rdg::f32x4 (&acc)[wq<M, N>()], float* __restrict__ part) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
+    constexpr int MB = (M + 15) / 16, NB = (N + 15) / 16;
+#pragma unroll
+    for (int q = 0; q < wq<M, N>(); ++q) {
+        const int t = wave + 4 * q;
+        if (t >= MB * NB) break;
+        const int m0 = 16 * (t / NB), n0 = 16 * (t % NB);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * gq + r, n = n0 + i;
+            if (m < M && n < N) part[m * N + n] = acc[q][r];
+        }
+    }
+}
 
+// MT: tpb tiles per workgroup with the weight-gradient accumulators in registers over all of them
+// (360 VGPRs: one workgroup per CU), for large batches; else one tile and 68 VGPRs
+template <bool MT>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
                                                        const float* __restrict__ A1, const float* __restrict__ A2,
                                                        const float* __restrict__ A3, const float* __restrict__ A4,
                                                        const float* __restrict__ dY, float* __restrict__ dHh,
-                                                       float* __restrict__ part, int64_t B, int nb) {
+                                                       float* __restrict__ part, int64_t B, int nb, int tpb) {
     __shared__ __attribute__((aligned(16))) float X0[HF_ROWS][U + 4];   // Hc, ones column U
     __shared__ __attribute__((aligned(16))) float X1[HF_ROWS][L1];
     __shared__ __attribute__((aligned(16))) float X2[HF_ROWS][L2];
@@ -748,33 +794,66 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     __shared__ __attribute__((aligned(16))) float D3[HF_ROWS][L3];
     __shared__ __attribute__((aligned(16))) float D2[HF_ROWS][L2];
     __shared__ __attribute__((aligned(16))) float D1[HF_ROWS][L1];
-    const int ts = blockIdx.x / nb, rb = blockIdx.x - ts * nb;   // as head_fwd_kernel
-    const int64_t row0 = (int64_t)ts * B + (int64_t)rb * HF_ROWS, R = (int64_t)(ts + 1) * B;
+    // workgroup (t, rb): rows t B + 16 tpb rb .. of step t, tpb tiles of 16 rows in turn; the
+    // weight-gradient accumulators run over all of them and leave one partial row
+    const int ts = blockIdx.x / nb, rb = blockIdx.x - ts * nb;
+    const int64_t R = (int64_t)(ts + 1) * B;
     const float* P = P0 + OFF_H + (int64_t)ts * HSZ;
-    // rows past R (the step's last row) are zero (activations and gradients): they add nothing to the partials
-    head_stage<U, U + 4>(Hc, U, row0, R, X0);
-    head_stage<H1 + 1, L1>(A1, L1, row0, R, X1);   // with the ones column
-    head_stage<H2 + 1, L2>(A2, L2, row0, R, X2);
-    head_stage<H3 + 1, L3>(A3, L3, row0, R, X3);
-    head_stage<H4 + 1, L4>(A4, L4, row0, R, X4);
-    head_stage<4, 8>(dY, 4, row0, R, D5);
-    if (threadIdx.x < HF_ROWS) X0[threadIdx.x][U] = row0 + threadIdx.x < R ? 1.0f : 0.0f;
-    __syncthreads();
-    head_dgrad<4, H4, true>(D5, D4, X4, P + OFF_W5, nullptr, 0, row0, R);
-    __syncthreads();
-    head_dgrad<H4, H3, true>(D4, D3, X3, P + OFF_W4, nullptr, 0, row0, R);
-    __syncthreads();
-    head_dgrad<H3, H2, true>(D3, D2, X2, P + OFF_W3, nullptr, 0, row0, R);
-    __syncthreads();
-    head_dgrad<H2, H1, true>(D2, D1, X1, P + OFF_W2, nullptr, 0, row0, R);
-    __syncthreads();
-    head_dgrad<H1, U, false>(D1, (float(*)[U + 4]) nullptr, X0, P + OFF_W1, dHh, U, row0, R);   // dh_head
     float* pw = part + (int64_t)blockIdx.x * HB_PART;
-    head_wgrad<U + 1, H1>(X0, D1, pw);                                   // [dW1; db1]
-    head_wgrad<H1 + 1, H2>(X1, D2, pw + (OFF_W2 - OFF_W1));              // [dW2; db2]
-    head_wgrad<H2 + 1, H3>(X2, D3, pw + (OFF_W3 - OFF_W1));
-    head_wgrad<H3 + 1, H4>(X3, D4, pw + (OFF_W4 - OFF_W1));
-    head_wgrad<H4 + 1, 4>(X4, D5, pw + (OFF_W5 - OFF_W1));
+    rdg::f32x4 a1[wq<U + 1, H1>()], a2[wq<H1 + 1, H2>()], a3[wq<H2 + 1, H3>()], a4[wq<H3 + 1, H4>()],
+        a5[wq<H4 + 1, 4>()];
+#define RDL_ZERO(a) _Pragma("unroll") for (auto& x : a) x = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+    RDL_ZERO(a1) RDL_ZERO(a2) RDL_ZERO(a3) RDL_ZERO(a4) RDL_ZERO(a5)
+#undef RDL_ZERO
+    for (int k = 0; k < (MT ? tpb : 1); ++k) {
+        const int64_t row0 = (int64_t)ts * B + ((int64_t)rb * tpb + k) * HF_ROWS;
+        if (row0 >= R) break;   // workgroup-uniform
+        // loop-invariant weights and lane indices: opaque copies keep their loads and address
+        // arithmetic inside the loop (hoisted, every layer's operands and addresses would be live
+        // at once and spill)
+        const float* Pk = P;
+        int tid = threadIdx.x;
+        asm volatile("" : "+s"(Pk), "+v"(tid));
+        // rows past R (the step's last row) are zero (activations and gradients): they add nothing
+        head_stage<U, U + 4>(Hc, U, row0, R, X0, tid);
+        head_stage<H1 + 1, L1>(A1, L1, row0, R, X1, tid);   // with the ones column
+        head_stage<H2 + 1, L2>(A2, L2, row0, R, X2, tid);
+        head_stage<H3 + 1, L3>(A3, L3, row0, R, X3, tid);
+        head_stage<H4 + 1, L4>(A4, L4, row0, R, X4, tid);
+        head_stage<4, 8>(dY, 4, row0, R, D5, tid);
+        if (tid < HF_ROWS) X0[tid][U] = row0 + tid < R ? 1.0f : 0.0f;
+        __syncthreads();
+        head_dgrad<4, H4, true>(D5, D4, X4, Pk + OFF_W5, nullptr, 0, row0, R, tid);
+        __syncthreads();
+        head_dgrad<H4, H3, true>(D4, D3, X3, Pk + OFF_W4, nullptr, 0, row0, R, tid);
+        __syncthreads();
+        head_dgrad<H3, H2, true>(D3, D2, X2, Pk + OFF_W3, nullptr, 0, row0, R, tid);
+        __syncthreads();
+        head_dgrad<H2, H1, true>(D2, D1, X1, Pk + OFF_W2, nullptr, 0, row0, R, tid);
+        __syncthreads();
+        head_dgrad<H1, U, false>(D1, (float(*)[U + 4]) nullptr, X0, Pk + OFF_W1, dHh, U, row0, R, tid);   // dh_head
+        if constexpr (MT) {   // [dW1; db1] .. [dW5; db5] accumulated over the tiles
+            head_wgrad_acc<U + 1, H1>(X0, D1, a1, tid);
+            head_wgrad_acc<H1 + 1, H2>(X1, D2, a2, tid);
+            head_wgrad_acc<H2 + 1, H3>(X2, D3, a3, tid);
+            head_wgrad_acc<H3 + 1, H4>(X3, D4, a4, tid);
+            head_wgrad_acc<H4 + 1, 4>(X4, D5, a5, tid);
+            __syncthreads();   // the next tile restages the LDS rows
+        } else {              // one tile: each layer's partial stored at once
+            head_wgrad<U + 1, H1>(X0, D1, pw);
+            head_wgrad<H1 + 1, H2>(X1, D2, pw + (OFF_W2 - OFF_W1));
+            head_wgrad<H2 + 1, H3>(X2, D3, pw + (OFF_W3 - OFF_W1));
+            head_wgrad<H3 + 1, H4>(X3, D4, pw + (OFF_W4 - OFF_W1));
+            head_wgrad<H4 + 1, 4>(X4, D5, pw + (OFF_W5 - OFF_W1));
+        }
+    }
+    if constexpr (MT) {
+        head_wgrad_store<U + 1, H1>(a1, pw);
+        head_wgrad_store<H1 + 1, H2>(a2, pw + (OFF_W2 - OFF_W1));
+        head_wgrad_store<H2 + 1, H3>(a3, pw + (OFF_W3 - OFF_W1));
+        head_wgrad_store<H3 + 1, H4>(a4, pw + (OFF_W4 - OFF_W1));
+        head_wgrad_store<H4 + 1, 4>(a5, pw + (OFF_W5 - OFF_W1));
+    }
 }
 
 // head t's gradient (blockIdx.y = t): grad[OFF_H + t HSZ + p] = sum over step t's nb
@@ -991,7 +1070,7 @@ struct rdl_trainer {
     float *D32 = nullptr, *D64a = nullptr, *D128 = nullptr, *D64b = nullptr, *dHh = nullptr, *dP = nullptr;
     float *dhn = nullptr, *dc = nullptr;
     float *split = nullptr, *colws = nullptr, *lpart = nullptr, *hist = nullptr;
-    float* hpart = nullptr;    // fused head backward: one partial row of HB_PART per (step, 16 rows)
+    float* hpart = nullptr;    // fused head backward: one partial row of HB_PART per workgroup (head_nb)
     int64_t colws_floats = 0;
     uint32_t* ctl = nullptr;
     uint32_t* bar = nullptr;   // persistent kernels: [0] forward / [1] BPTT barrier arrivals, [2] timeout flag
@@ -1065,8 +1144,20 @@ int pr_dbg() {   // diagnostic builds: RDL_PR_DBG bit 0 skips the exchange loads
 #endif
 }
 
+// head_bwd_kernel's 16-row tiles per workgroup: one while the T x ceil(B / 16) tiles fill at
+// most ~4 workgroups per CU, then up to 8, so the partial rows (HB_PART floats each) and their
+// reduce shrink with the batch
+int head_tpb(int T, int64_t B) {
+    const int64_t tiles = (B + HF_ROWS - 1) / HF_ROWS;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)T * tiles / 1024));
+}
+int head_nb(int T, int64_t B) {
+    const int64_t tiles = (B + HF_ROWS - 1) / HF_ROWS, tpb = head_tpb(T, B);
+    return (int)((tiles + tpb - 1) / tpb);
+}
+
 bool fused_head(const rdl_trainer* t, int64_t R) {
-    // the partial rows of its T x ceil(B / 16) workgroups live in hpart (sized at create for
+    // the partial rows of its T x head_nb workgroups live in hpart (sized at create for
     // max_windows when that fits HPART_MAX_FLOATS); with one head per step, the per-layer path
     // is T x 11 launches, so the fused head now covers up to 16,384 rows
     return !(t->cfg.kernels & RDL_KERNELS_LAYER_HEAD) && t->hpart && R <= HF_MAX_ROWS;
@@ -1169,10 +1260,11 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     }
     const float* Hc = t->H + B * U;
     if (fused_head(t, R)) {   // the heads' backward as two launches (head_bwd_kernel + fixed-order reduce)
-        const int nb = (int)((B + HF_ROWS - 1) / HF_ROWS);
-        hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)(T * nb)), dim3(256), 0, t->stream, Hc, P,
+        const int nb = head_nb(T, B), tpb = head_tpb(T, B);
+        hipLaunchKernelGGL(tpb > 1 ? head_bwd_kernel<true> : head_bwd_kernel<false>, dim3((unsigned)(T * nb)),
+                           dim3(256), 0, t->stream, Hc, P,
                            (const float*)t->A1, (const float*)t->A2, (const float*)t->A3, (const float*)t->A4,
-                           (const float*)t->dY, t->dHh, t->hpart, B, nb);
+                           (const float*)t->dY, t->dHh, t->hpart, B, nb, tpb);
         RDL_CK(hipGetLastError(), "rdl head_bwd_kernel");
         hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((HB_PART + 255) / 256, (unsigned)T), dim3(256), 0, t->stream,
                            (const float*)t->hpart, nb, g);
@@ -1335,7 +1427,9 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     alloc(&t->dhn, B * U);
     alloc(&t->dc, B * U);
     alloc(&t->split, SPLIT_FLOATS);
-    const int64_t hp = (int64_t)t->T * ((t->Bmax + HF_ROWS - 1) / HF_ROWS) * HB_PART;
+    int64_t nbmax = 0;   // the most workgroups of any batch up to Bmax (head_nb is not monotone)
+    for (int64_t b = HF_ROWS; b < t->Bmax + HF_ROWS; b += HF_ROWS) nbmax = std::max<int64_t>(nbmax, head_nb(t->T, b));
+    const int64_t hp = (int64_t)t->T * nbmax * HB_PART;
     if (hp <= HPART_MAX_FLOATS) alloc(&t->hpart, hp);
     alloc(&t->colws, t->colws_floats);
     alloc(&t->lpart, 2 * ((R + LOSS_BLOCK - 1) / LOSS_BLOCK));
