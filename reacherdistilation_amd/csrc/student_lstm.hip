@@ -633,19 +633,19 @@ __device__ __forceinline__ void head_layer(const float (*in)[LI], float (*out)[L
 
 // rows row0.. of a [R][ld] matrix, columns 0..COLS-1 -> dst[16][LDD] (zero past R): every
 // load of the thread issued before its first LDS store (one round trip, not one per element)
-template <int COLS, int LDD>
+template <int COLS, int LDD, int NT = 256>
 __device__ __forceinline__ void head_stage(const float* __restrict__ src, int ld, int64_t row0, int64_t R,
                                            float (*dst)[LDD], int tid) {
-    constexpr int PER = (HF_ROWS * COLS + 255) / 256;
+    constexpr int PER = (HF_ROWS * COLS + NT - 1) / NT;
     float v[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int x = tid + 256 * j, row = x / COLS, c = x - row * COLS;
+        const int x = tid + NT * j, row = x / COLS, c = x - row * COLS;
         v[j] = (x < HF_ROWS * COLS && row0 + row < R) ? src[(row0 + row) * ld + c] : 0.0f;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int x = tid + 256 * j, row = x / COLS, c = x - row * COLS;
+        const int x = tid + NT * j, row = x / COLS, c = x - row * COLS;
         if (x < HF_ROWS * COLS) dst[row][c] = v[j];
     }
 }
@@ -679,15 +679,15 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
 // head_wgrad_reduce_kernel sums the rows in a fixed order.  Two launches instead of six.
 constexpr int HB_PART = HSZ;   // 31,652 floats: [W1;b1][W2;b2][W3;b3][W4;b4][W5;b5] of one head
 // dIn[16][NI] = (dOut[16][KO] . W^T) (* (1 - act^2) when DT); W is [NI][KO] (layer input x output)
-template <int KO, int NI, bool DT, int LD, int LI, int LA>
+template <int KO, int NI, bool DT, int NW = 4, int LD, int LI, int LA>
 __device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)[LI], const float (*act)[LA],
                                            const float* __restrict__ W, float* gout, int ldg, int64_t row0, int64_t R,
                                            int tid) {
     const int wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     constexpr int NB = (NI + 15) / 16;
 #pragma unroll
-    for (int it = 0; it < (NB + 3) / 4; ++it) {   // unrolled: every weight load of the layer in flight at once
-        const int cb = wave + 4 * it;
+    for (int it = 0; it < (NB + NW - 1) / NW; ++it) {   // unrolled: every weight load of the layer in flight at once
+        const int cb = wave + NW * it;
         if (cb >= NB) break;
         const int col = 16 * cb + i;
         const bool cv = col < NI;
@@ -737,16 +737,16 @@ __device__ __forceinline__ void head_wgrad(const float (*act)[LA], const float (
 // acc += sum over the 16 rows of act[row][m] d[row][n], m < M (the last input row is the ones
 // column: the bias gradient), n < N: 16x16 output tiles t = wave, wave + 4, ...; the
 // accumulators stay in registers over a workgroup's tiles of rows (head_bwd_kernel)
-template <int M, int N>
-constexpr int wq() { return (((M + 15) / 16) * ((N + 15) / 16) + 3) / 4; }
-template <int M, int N, int LA, int LD>
+template <int M, int N, int NW = 4>
+constexpr int wq() { return (((M + 15) / 16) * ((N + 15) / 16) + NW - 1) / NW; }
+template <int M, int N, int NW = 4, int LA, int LD>
 __device__ __forceinline__ void head_wgrad_acc(const float (*act)[LA], const float (*d)[LD],
-                                               rdg::f32x4 (&acc)[wq<M, N>()], int tid) {
+                                               rdg::f32x4 (&acc)[wq<M, N, NW>()], int tid) {
     const int wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     constexpr int MB = (M + 15) / 16, NB = (N + 15) / 16;
 #pragma unroll
-    for (int q = 0; q < wq<M, N>(); ++q) {
-        const int t = wave + 4 * q;
+    for (int q = 0; q < wq<M, N, NW>(); ++q) {
+        const int t = wave + NW * q;
         if (t >= MB * NB) break;
         const int m0 = 16 * (t / NB), n0 = 16 * (t % NB);
         const int mc = m0 + i < M ? m0 + i : M - 1, nc = n0 + i < N ? n0 + i : N - 1;
@@ -759,13 +759,13 @@ __device__ __forceinline__ void head_wgrad_acc(const float (*act)[LA], const flo
     }
 }
 // part[m][n] = the accumulated tiles
-template <int M, int N>
-__device__ __forceinline__ void head_wgrad_store(const rdg::f32x4 (&acc)[wq<M, N>()], float* __restrict__ part) {
+template <int M, int N, int NW = 4>
+__device__ __forceinline__ void head_wgrad_store(const rdg::f32x4 (&acc)[wq<M, N, NW>()], float* __restrict__ part) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     constexpr int MB = (M + 15) / 16, NB = (N + 15) / 16;
 #pragma unroll
-    for (int q = 0; q < wq<M, N>(); ++q) {
-        const int t = wave + 4 * q;
+    for (int q = 0; q < wq<M, N, NW>(); ++q) {
+        const int t = wave + NW * q;
         if (t >= MB * NB) break;
         const int m0 = 16 * (t / NB), n0 = 16 * (t % NB);
 #pragma unroll
@@ -777,9 +777,9 @@ __device__ __forceinline__ void head_wgrad_store(const rdg::f32x4 (&acc)[wq<M, N
 }
 
 // MT: tpb tiles per workgroup with the weight-gradient accumulators in registers over all of them
-// (360 VGPRs: one workgroup per CU), for large batches; else one tile and 68 VGPRs
+// (eight waves share them), for large batches; else one tile, four waves, 64 VGPRs
 template <bool MT>
-__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
+__global__ __launch_bounds__(MT ? 512 : 256) void head_bwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
                                                        const float* __restrict__ A1, const float* __restrict__ A2,
                                                        const float* __restrict__ A3, const float* __restrict__ A4,
                                                        const float* __restrict__ dY, float* __restrict__ dHh,
@@ -800,8 +800,9 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     const int64_t R = (int64_t)(ts + 1) * B;
     const float* P = P0 + OFF_H + (int64_t)ts * HSZ;
     float* pw = part + (int64_t)blockIdx.x * HB_PART;
-    rdg::f32x4 a1[wq<U + 1, H1>()], a2[wq<H1 + 1, H2>()], a3[wq<H2 + 1, H3>()], a4[wq<H3 + 1, H4>()],
-        a5[wq<H4 + 1, 4>()];
+    constexpr int NW = MT ? 8 : 4, NT = 64 * NW;   // MT: eight waves share the accumulators
+    rdg::f32x4 a1[wq<U + 1, H1, NW>()], a2[wq<H1 + 1, H2, NW>()], a3[wq<H2 + 1, H3, NW>()],
+        a4[wq<H3 + 1, H4, NW>()], a5[wq<H4 + 1, 4, NW>()];
 #define RDL_ZERO(a) _Pragma("unroll") for (auto& x : a) x = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
     RDL_ZERO(a1) RDL_ZERO(a2) RDL_ZERO(a3) RDL_ZERO(a4) RDL_ZERO(a5)
 #undef RDL_ZERO
@@ -815,29 +816,29 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
         int tid = threadIdx.x;
         asm volatile("" : "+s"(Pk), "+v"(tid));
         // rows past R (the step's last row) are zero (activations and gradients): they add nothing
-        head_stage<U, U + 4>(Hc, U, row0, R, X0, tid);
-        head_stage<H1 + 1, L1>(A1, L1, row0, R, X1, tid);   // with the ones column
-        head_stage<H2 + 1, L2>(A2, L2, row0, R, X2, tid);
-        head_stage<H3 + 1, L3>(A3, L3, row0, R, X3, tid);
-        head_stage<H4 + 1, L4>(A4, L4, row0, R, X4, tid);
-        head_stage<4, 8>(dY, 4, row0, R, D5, tid);
+        head_stage<U, U + 4, NT>(Hc, U, row0, R, X0, tid);
+        head_stage<H1 + 1, L1, NT>(A1, L1, row0, R, X1, tid);   // with the ones column
+        head_stage<H2 + 1, L2, NT>(A2, L2, row0, R, X2, tid);
+        head_stage<H3 + 1, L3, NT>(A3, L3, row0, R, X3, tid);
+        head_stage<H4 + 1, L4, NT>(A4, L4, row0, R, X4, tid);
+        head_stage<4, 8, NT>(dY, 4, row0, R, D5, tid);
         if (tid < HF_ROWS) X0[tid][U] = row0 + tid < R ? 1.0f : 0.0f;
         __syncthreads();
-        head_dgrad<4, H4, true>(D5, D4, X4, Pk + OFF_W5, nullptr, 0, row0, R, tid);
+        head_dgrad<4, H4, true, NW>(D5, D4, X4, Pk + OFF_W5, nullptr, 0, row0, R, tid);
         __syncthreads();
-        head_dgrad<H4, H3, true>(D4, D3, X3, Pk + OFF_W4, nullptr, 0, row0, R, tid);
+        head_dgrad<H4, H3, true, NW>(D4, D3, X3, Pk + OFF_W4, nullptr, 0, row0, R, tid);
         __syncthreads();
-        head_dgrad<H3, H2, true>(D3, D2, X2, Pk + OFF_W3, nullptr, 0, row0, R, tid);
+        head_dgrad<H3, H2, true, NW>(D3, D2, X2, Pk + OFF_W3, nullptr, 0, row0, R, tid);
         __syncthreads();
-        head_dgrad<H2, H1, true>(D2, D1, X1, Pk + OFF_W2, nullptr, 0, row0, R, tid);
+        head_dgrad<H2, H1, true, NW>(D2, D1, X1, Pk + OFF_W2, nullptr, 0, row0, R, tid);
         __syncthreads();
-        head_dgrad<H1, U, false>(D1, (float(*)[U + 4]) nullptr, X0, Pk + OFF_W1, dHh, U, row0, R, tid);   // dh_head
+        head_dgrad<H1, U, false, NW>(D1, (float(*)[U + 4]) nullptr, X0, Pk + OFF_W1, dHh, U, row0, R, tid);   // dh_head
         if constexpr (MT) {   // [dW1; db1] .. [dW5; db5] accumulated over the tiles
-            head_wgrad_acc<U + 1, H1>(X0, D1, a1, tid);
-            head_wgrad_acc<H1 + 1, H2>(X1, D2, a2, tid);
-            head_wgrad_acc<H2 + 1, H3>(X2, D3, a3, tid);
-            head_wgrad_acc<H3 + 1, H4>(X3, D4, a4, tid);
-            head_wgrad_acc<H4 + 1, 4>(X4, D5, a5, tid);
+            head_wgrad_acc<U + 1, H1, NW>(X0, D1, a1, tid);
+            head_wgrad_acc<H1 + 1, H2, NW>(X1, D2, a2, tid);
+            head_wgrad_acc<H2 + 1, H3, NW>(X2, D3, a3, tid);
+            head_wgrad_acc<H3 + 1, H4, NW>(X3, D4, a4, tid);
+            head_wgrad_acc<H4 + 1, 4, NW>(X4, D5, a5, tid);
             __syncthreads();   // the next tile restages the LDS rows
         } else {              // one tile: each layer's partial stored at once
             head_wgrad<U + 1, H1>(X0, D1, pw);
@@ -848,11 +849,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
         }
     }
     if constexpr (MT) {
-        head_wgrad_store<U + 1, H1>(a1, pw);
-        head_wgrad_store<H1 + 1, H2>(a2, pw + (OFF_W2 - OFF_W1));
-        head_wgrad_store<H2 + 1, H3>(a3, pw + (OFF_W3 - OFF_W1));
-        head_wgrad_store<H3 + 1, H4>(a4, pw + (OFF_W4 - OFF_W1));
-        head_wgrad_store<H4 + 1, 4>(a5, pw + (OFF_W5 - OFF_W1));
+        head_wgrad_store<U + 1, H1, NW>(a1, pw);
+        head_wgrad_store<H1 + 1, H2, NW>(a2, pw + (OFF_W2 - OFF_W1));
+        head_wgrad_store<H2 + 1, H3, NW>(a3, pw + (OFF_W3 - OFF_W1));
+        head_wgrad_store<H3 + 1, H4, NW>(a4, pw + (OFF_W4 - OFF_W1));
+        head_wgrad_store<H4 + 1, 4, NW>(a5, pw + (OFF_W5 - OFF_W1));
     }
 }
 
@@ -1262,7 +1263,7 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     if (fused_head(t, R)) {   // the heads' backward as two launches (head_bwd_kernel + fixed-order reduce)
         const int nb = head_nb(T, B), tpb = head_tpb(T, B);
         hipLaunchKernelGGL(tpb > 1 ? head_bwd_kernel<true> : head_bwd_kernel<false>, dim3((unsigned)(T * nb)),
-                           dim3(256), 0, t->stream, Hc, P,
+                           dim3(tpb > 1 ? 512 : 256), 0, t->stream, Hc, P,
                            (const float*)t->A1, (const float*)t->A2, (const float*)t->A3, (const float*)t->A4,
                            (const float*)t->dY, t->dHh, t->hpart, B, nb, tpb);
         RDL_CK(hipGetLastError(), "rdl head_bwd_kernel");
