@@ -679,10 +679,11 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
 // head_wgrad_reduce_kernel sums the rows in a fixed order.  Two launches instead of six.
 constexpr int HB_PART = HSZ;   // 31,652 floats: [W1;b1][W2;b2][W3;b3][W4;b4][W5;b5] of one head
 // dIn[16][NI] = (dOut[16][KO] . W^T) (* (1 - act^2) when DT); W is [NI][KO] (layer input x output)
-template <int KO, int NI, bool DT, int NW = 4, int LD, int LI, int LA>
-__device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)[LI], const float (*act)[LA],
-                                           const float* __restrict__ W, float* gout, int ldg, int64_t row0, int64_t R,
-                                           int tid) {
+// wf(it, kq, cv, col, k): the weight W[col][k] of this lane's column block it, k step kq (zero
+// past NI): streamed from L2 (head_dgrad) or held in registers (head_bwd_kernel<true>)
+template <int KO, int NI, bool DT, int NW, int LD, int LI, int LA, class WF>
+__device__ __forceinline__ void head_dgrad_f(const float (*dout)[LD], float (*din)[LI], const float (*act)[LA], WF wf,
+                                             float* gout, int ldg, int64_t row0, int64_t R, int tid) {
     const int wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     constexpr int NB = (NI + 15) / 16;
 #pragma unroll
@@ -695,7 +696,7 @@ __device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)
 #pragma unroll
         for (int kq = 0; kq < KO / 4; ++kq) {
             const int k = 4 * kq + gq;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dout[i][k], cv ? W[col * KO + k] : 0.0f, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dout[i][k], wf(it, kq, cv, col, k), acc, 0, 0, 0);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -712,6 +713,31 @@ __device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)
         }
     }
 }
+template <int KO, int NI, bool DT, int NW = 4, int LD, int LI, int LA>
+__device__ __forceinline__ void head_dgrad(const float (*dout)[LD], float (*din)[LI], const float (*act)[LA],
+                                           const float* __restrict__ W, float* gout, int ldg, int64_t row0, int64_t R,
+                                           int tid) {
+    head_dgrad_f<KO, NI, DT, NW>(dout, din, act,
+                                 [W](int, int, bool cv, int col, int k) { return cv ? W[col * KO + k] : 0.0f; }, gout,
+                                 ldg, row0, R, tid);
+}
+// this lane's weights of head_dgrad_f's column blocks (it) and k steps (kq), loaded once
+template <int KO, int NI, int NW>
+struct HeadW {
+    static constexpr int NB = (NI + 15) / 16, IT = (NB + NW - 1) / NW;
+    float w[IT][KO / 4];
+    __device__ __forceinline__ void load(const float* __restrict__ W, int tid) {
+        const int wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int cb = wave + NW * it, col = 16 * cb + i;
+            const bool cv = cb < NB && col < NI;
+#pragma unroll
+            for (int kq = 0; kq < KO / 4; ++kq) w[it][kq] = cv ? W[col * KO + 4 * kq + gq] : 0.0f;
+        }
+    }
+    __device__ __forceinline__ float operator()(int it, int kq, bool, int, int) const { return w[it][kq]; }
+};
 // part[m][n] = sum over the 16 rows of act[row][m] d[row][n], m < M (the last input row is the
 // ones column: the bias gradient), n < N (one tile of rows: head_bwd_kernel<false>)
 template <int M, int N, int LA, int LD>
@@ -806,6 +832,19 @@ __global__ __launch_bounds__(MT ? 512 : 256) void head_bwd_kernel(const float* _
 #define RDL_ZERO(a) _Pragma("unroll") for (auto& x : a) x = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
     RDL_ZERO(a1) RDL_ZERO(a2) RDL_ZERO(a3) RDL_ZERO(a4) RDL_ZERO(a5)
 #undef RDL_ZERO
+    // MT: this lane's share of step ts's head weights held in registers over all the tiles
+    HeadW<4, H4, NW> w5;
+    HeadW<H4, H3, NW> w4;
+    HeadW<H3, H2, NW> w3;
+    HeadW<H2, H1, NW> w2;
+    HeadW<H1, U, NW> w1;
+    if constexpr (MT) {
+        w5.load(P + OFF_W5, threadIdx.x);
+        w4.load(P + OFF_W4, threadIdx.x);
+        w3.load(P + OFF_W3, threadIdx.x);
+        w2.load(P + OFF_W2, threadIdx.x);
+        w1.load(P + OFF_W1, threadIdx.x);
+    }
     for (int k = 0; k < (MT ? tpb : 1); ++k) {
         const int64_t row0 = (int64_t)ts * B + ((int64_t)rb * tpb + k) * HF_ROWS;
         if (row0 >= R) break;   // workgroup-uniform
@@ -824,15 +863,27 @@ __global__ __launch_bounds__(MT ? 512 : 256) void head_bwd_kernel(const float* _
         head_stage<4, 8, NT>(dY, 4, row0, R, D5, tid);
         if (tid < HF_ROWS) X0[tid][U] = row0 + tid < R ? 1.0f : 0.0f;
         __syncthreads();
-        head_dgrad<4, H4, true, NW>(D5, D4, X4, Pk + OFF_W5, nullptr, 0, row0, R, tid);
-        __syncthreads();
-        head_dgrad<H4, H3, true, NW>(D4, D3, X3, Pk + OFF_W4, nullptr, 0, row0, R, tid);
-        __syncthreads();
-        head_dgrad<H3, H2, true, NW>(D3, D2, X2, Pk + OFF_W3, nullptr, 0, row0, R, tid);
-        __syncthreads();
-        head_dgrad<H2, H1, true, NW>(D2, D1, X1, Pk + OFF_W2, nullptr, 0, row0, R, tid);
-        __syncthreads();
-        head_dgrad<H1, U, false, NW>(D1, (float(*)[U + 4]) nullptr, X0, Pk + OFF_W1, dHh, U, row0, R, tid);   // dh_head
+        if constexpr (MT) {
+            head_dgrad_f<4, H4, true, NW>(D5, D4, X4, w5, nullptr, 0, row0, R, tid);
+            __syncthreads();
+            head_dgrad_f<H4, H3, true, NW>(D4, D3, X3, w4, nullptr, 0, row0, R, tid);
+            __syncthreads();
+            head_dgrad_f<H3, H2, true, NW>(D3, D2, X2, w3, nullptr, 0, row0, R, tid);
+            __syncthreads();
+            head_dgrad_f<H2, H1, true, NW>(D2, D1, X1, w2, nullptr, 0, row0, R, tid);
+            __syncthreads();
+            head_dgrad_f<H1, U, false, NW>(D1, (float(*)[U + 4]) nullptr, X0, w1, dHh, U, row0, R, tid);   // dh_head
+        } else {
+            head_dgrad<4, H4, true, NW>(D5, D4, X4, Pk + OFF_W5, nullptr, 0, row0, R, tid);
+            __syncthreads();
+            head_dgrad<H4, H3, true, NW>(D4, D3, X3, Pk + OFF_W4, nullptr, 0, row0, R, tid);
+            __syncthreads();
+            head_dgrad<H3, H2, true, NW>(D3, D2, X2, Pk + OFF_W3, nullptr, 0, row0, R, tid);
+            __syncthreads();
+            head_dgrad<H2, H1, true, NW>(D2, D1, X1, Pk + OFF_W2, nullptr, 0, row0, R, tid);
+            __syncthreads();
+            head_dgrad<H1, U, false, NW>(D1, (float(*)[U + 4]) nullptr, X0, Pk + OFF_W1, dHh, U, row0, R, tid);
+        }
         if constexpr (MT) {   // [dW1; db1] .. [dW5; db5] accumulated over the tiles
             head_wgrad_acc<U + 1, H1, NW>(X0, D1, a1, tid);
             head_wgrad_acc<H1 + 1, H2, NW>(X1, D2, a2, tid);
