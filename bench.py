@@ -387,28 +387,52 @@ def _make_comm(kind, dev, world):
     return None, why or "failed its self-check on another rank"
 
 
-def strong_leg(wl, total, sdt, split, dev, lr, steps, warmup, rank, world, comm, settle_ms=0.0):
+def comm_view(comm, dev, world):
+    """Every rank's communicator as the library sees it (rd_comm_query: RCCL's own
+    ncclCommCount / ncclCommUserRank / ncclCommCuDevice, or an xGMI communicator's creation
+    values), gathered to every rank: [{rank, count, user_rank, device, from_rccl}]."""
+    import torch
+    import torch.distributed as dist
+    q = comm.query()
+    mine = torch.tensor([dist.get_rank(), q["count"], q["user_rank"], q["device"], int(q["from_rccl"])],
+                        dtype=torch.int64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    allq = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allq, mine)
+    rows = [dict(zip(("rank", "count", "user_rank", "device", "from_rccl"), t.cpu().tolist())) for t in allq]
+    for r in rows:
+        r["from_rccl"] = bool(r["from_rccl"])
+    return {"ranks": rows, "consistent": all(r["count"] == world and r["user_rank"] == r["rank"] for r in rows),
+            "distinct_devices": len({r["device"] for r in rows}) == world}
+
+
+def strong_leg(wl, total, sdt, split, dev, lr, steps, warmup, rank, world, comm, settle_ms=0.0, accum=1):
     """BASELINE config 4's own wording, "262 144 envs sharded across 8 x MI355X": the
     workload's fixed global batch split over the ranks (`n_envs_global`, contiguous shards,
     Philox key = global env id), timed like the headline (barrier + synchronize around
-    exactly `steps` fused steps, MAX over ranks).  Reported beside the weak-scaling value."""
+    exactly `steps` fused steps, MAX over ranks).  Reported beside the weak-scaling value.
+    accum = K > 1: one optimiser step (+ all-reduce) per K env steps in one K-step launch
+    (rdd_step_accum, SURVEY §8d's K = 50 reading); `steps` env steps = steps / K calls."""
     import torch
     import torch.distributed as dist
 
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
     tr = DistillTrainer(DistillConfig(n_envs_global=total, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
-                                      student_dtype=sdt, f32_split=split),
+                                      student_dtype=sdt, f32_split=split, accum_steps=accum),
                         device=dev, rank=rank, world_size=world, comm=comm)
-    settle(tr.step, dev, settle_ms, world)
-    for _ in range(warmup):
-        tr.step()
+    K = max(1, accum)
+    step = tr.step if K == 1 else tr.step_accum
+    calls = max(1, steps // K)
+    steps = calls * K
+    settle(step, dev, settle_ms / K if K > 1 else settle_ms, world)
+    for _ in range(max(1, warmup // K)):
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        tr.step()
+    for _ in range(calls):
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -419,12 +443,14 @@ def strong_leg(wl, total, sdt, split, dev, lr, steps, warmup, rank, world, comm,
     el = float(t.item())
     same = tr.replicas_identical() if world > 1 else True
     out = {"envs_total": total, "envs_per_gpu": tr.n_local, "steps": steps, "value": total * steps / el,
-           "ms_per_step": el * 1e3 / steps, "replicas_identical": same, "scaling": "strong"}
+           "ms_per_step": el * 1e3 / steps, "replicas_identical": same, "scaling": "strong",
+           "accum_steps": K, "launch": "rdd_step (one optimiser step per env step)" if K == 1 else
+           f"rdd_step_accum (one {K}-env-step launch + reduce + all-reduce + Adam per optimiser step)"}
     tr.close()
     return out
 
 
-def strong_projection(wl, sdt, split, dev, lr, steps, settle_ms):
+def strong_projection(wl, sdt, split, dev, lr, steps, settle_ms, accum=50):
     """the compute side of c4's 1/2/4/8-GPU curve measured on one GPU --
     one-process steps at the 2/4/8-GPU strong shards of the 262,144-env global batch (131,072 /
     65,536 / 32,768 envs) and the sharded step's extra launch (rollout, reduce, [exchange], Adam:
@@ -443,22 +469,28 @@ def strong_projection(wl, sdt, split, dev, lr, steps, settle_ms):
     out = {"global_envs": total, "target_speedup_8": 6.0, "exchange_us_model": {"low": xlo, "high": xhi},
            "model": ("strong: t1 / (t_shard + t_split + x); weak: N t1 / (t1 + t_split(t1) + x); "
                      "t_* measured on one GPU here, x (the all-reduce) modelled"), "shards": {}}
-    t1 = split1 = None
+    t1 = split1 = t1k = None
+    K = accum
+    out["accum_steps"] = K
+    out["model_k"] = (f"K = {K} (one optimiser step per {K} env steps, one K-step launch, SURVEY §8d): per env step "
+                      f"t_K(shard) + (t_split_K + x) / K against t1 (K = 1, the headline's step) and t1_K (262,144 "
+                      f"envs at K = {K} on one GPU)")
+
+    def timeit(fn, calls=steps, per=1, warm=20):
+        for _ in range(warm):
+            fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) * 1e6 / (calls * per)
+
     for N in (1, 2, 4, 8):
         n = total // N
         tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
                                           student_dtype=sdt, f32_split=split), device=dev)
         settle(tr.step, dev, settle_ms)
-
-        def timeit(fn):
-            for _ in range(20):
-                fn()
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                fn()
-            torch.cuda.synchronize(dev)
-            return (time.perf_counter() - t0) * 1e6 / steps
 
         def three():   # the sharded step's launches with a zero-cost exchange
             tr.launch(tr.STAGE_ROLLOUT)
@@ -467,18 +499,41 @@ def strong_projection(wl, sdt, split, dev, lr, steps, settle_ms):
         us = timeit(tr.step)
         split_us = max(0.0, timeit(three) - us)
         tr.close()
+        kus = ksplit = None
+        if K > 1:   # the K-step launch: per env step, and its sharded form's extra launch per optimiser step
+            tk = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
+                                              student_dtype=sdt, f32_split=split, accum_steps=K), device=dev)
+            kcalls = max(4, (steps * 2) // K)
+            kus = timeit(tk.step_accum, kcalls, K, warm=2)
+
+            def kthree():   # the K-step launch + reduce, then Adam: the sharded form with a zero-cost exchange
+                tk.rollout_accum()
+                tk.launch(tk.STAGE_APPLY)
+            ksplit = max(0.0, timeit(kthree, kcalls, 1, warm=2) - kus * K)
+            tk.close()
         if N == 1:
             t1, split1 = us, split_us
             out["t1_us"], out["t1_split_overhead_us"] = us, split_us
+            if kus is not None:
+                t1k = kus
+                out["t1_k_us_per_env_step"] = kus
             continue
-        out["shards"][str(N)] = {
+        sh = out["shards"][str(N)] = {
             "envs_per_gpu": n, "step_us": us, "split_overhead_us": split_us,
             "strong_speedup": {"x_high": t1 / (us + split_us + xhi), "x_low": t1 / (us + split_us + xlo)},
             "weak_speedup": {"x_high": N * t1 / (t1 + split1 + xhi), "x_low": N * t1 / (t1 + split1 + xlo)},
             "strong_step_budget_for_6x_at_8_us": t1 / 6.0}
+        if kus is not None:
+            per = {x: kus + (ksplit + xv) / K for x, xv in (("x_high", xhi), ("x_low", xlo))}
+            sh["k"] = {"us_per_env_step": kus, "split_overhead_us_per_opt_step": ksplit,
+                       "us_per_env_step_with_exchange": per,
+                       "strong_speedup_vs_t1": {x: t1 / v for x, v in per.items()},
+                       "strong_speedup_vs_t1_k": {x: t1k / v for x, v in per.items()}}
     s8 = out["shards"]["8"]
     out["meets_6x_at_8"] = {"strong": {k: v >= 6.0 for k, v in s8["strong_speedup"].items()},
                             "weak": {k: v >= 6.0 for k, v in s8["weak_speedup"].items()}}
+    if "k" in s8:
+        out["meets_6x_at_8"]["strong_k_vs_t1"] = {k: v >= 6.0 for k, v in s8["k"]["strong_speedup_vs_t1"].items()}
     return out
 
 
@@ -656,6 +711,7 @@ def main():
                 exchange[f"{kind}_us"] = f"unavailable: {why}"
                 continue
             exchange[f"{kind}_us"] = exchange_latency(c, dev)["us"]
+            exchange[f"{kind}_view"] = comm_view(c, dev, world)
             cands[kind] = c
         exchange["floats"] = 5060
         exchange["timing"] = "200 back-to-back in-place all-reduces of 5,060 floats, HIP events, trainer stream"
@@ -745,30 +801,43 @@ def main():
 
     accum = None
     if args.accum > 1:   # secondary line: one optimiser step (+ all-reduce) per K env-steps
-        tk = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr,
-                                          student_dtype=sdt, accum_steps=args.accum, f32_split=split),
-                            device=dev, rank=rank, world_size=world, comm=comm)
-        ksteps = 2 * args.accum
-        for _ in range(args.accum):
-            tk.step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for _ in range(ksteps):
-            tk.step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        tt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        accum = {"accum_steps": args.accum, "steps": ksteps, "value": n * world * ksteps / float(tt.item()),
-                 "ms_per_step": float(tt.item()) * 1e3 / ksteps,
-                 "replicas_identical": tk.replicas_identical() if world > 1 else True}
-        tk.close()
+        K = args.accum
+        accum = {"accum_steps": K}
+        # fused: one K-step launch per optimiser step (rdd_step_accum); staged: K rollout launches
+        # each reduced into the gradient, then (all-reduce +) Adam (rdd_launch_stage)
+        for form, opt_steps in (("fused", max(4, (2 * args.steps) // K)), ("staged", 2)):
+            tk = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr,
+                                              student_dtype=sdt, accum_steps=K, f32_split=split),
+                                device=dev, rank=rank, world_size=world, comm=comm)
+
+            def opt_step():
+                if form == "fused":
+                    tk.step_accum()
+                else:
+                    for _ in range(K):
+                        tk.step()
+            opt_step()
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for _ in range(opt_steps):
+                opt_step()
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            tt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            ksteps = opt_steps * K
+            accum[form] = {"env_steps": ksteps, "opt_steps": opt_steps, "value": n * world * ksteps / float(tt.item()),
+                           "us_per_env_step": float(tt.item()) * 1e6 / ksteps,
+                           "replicas_identical": tk.replicas_identical() if world > 1 else True}
+            tk.close()
+        accum["value"] = accum["fused"]["value"]
+        accum["ms_per_step"] = accum["fused"]["us_per_env_step"] * 1e-3
 
     # the strong-scaling reading of the workload (its fixed global batch over the ranks); at
     # one GPU it is the headline run itself (c4: 262,144 envs on one GPU)
@@ -777,6 +846,10 @@ def main():
     if world > 1 and not args.no_strong and not args.envs_per_gpu:
         strong = strong_leg(wl, total, sdt, split, dev, args.lr, max(args.steps, 100), args.warmup, rank, world, comm,
                             settle_ms=min(args.settle_ms, 100.0))
+        if args.accum > 1:   # the same fixed global batch at one optimiser step per K env steps (K-step launch)
+            strong["accum"] = strong_leg(wl, total, sdt, split, dev, args.lr, max(args.steps, 2 * args.accum),
+                                         args.warmup, rank, world, comm, settle_ms=min(args.settle_ms, 100.0),
+                                         accum=args.accum)
 
     # student action-MSE vs teacher over the last steps (all ranks)
     met = tr.metrics(min(10, tr.counter()))
@@ -870,7 +943,8 @@ def main():
             out["roofline_env"]["frac_of_measured_copy"] = out["roofline_env"]["achieved"] / copy_gbs
             out["roofline_env"]["copy_ceiling"] = "torch copy_ (scripts/micro/libcopybw.so not built)"
         if world == 1 and args.workload == "c4" and not args.no_strong_projection and not args.envs_per_gpu:
-            out["strong_projection"] = strong_projection(wl, sdt, split, dev, args.lr, 200, min(args.settle_ms, 100.0))
+            out["strong_projection"] = strong_projection(wl, sdt, split, dev, args.lr, 200, min(args.settle_ms, 100.0),
+                                                         accum=max(1, args.accum))
         if world == 1 and args.fixture_steps > 0:
             out["convergence_fixture"] = convergence_fixture(dev, args.lr, args.fixture_steps, args.fixture_ref_steps)
         if world == 1 and not args.no_cpu_baseline:

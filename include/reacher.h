@@ -67,6 +67,12 @@ int rd_set_reset_mode(rd_env* env, int mode, const float* draws, int32_t n_episo
  * out: host buffer [n_episodes][6] (q0, q1, v0, v1, tx, ty). */
 int rd_gym_reset_draws(uint64_t seed, int32_t n_episodes, double* out);
 
+/* HOST function: CRC32C (Castagnoli, reflected 0x82F63B78) of n bytes of host memory,
+ * continuing from `crc` (0 to start) -- the checksum of the TF1 V2 checkpoint bundles the
+ * reference's tf.train.Saver writes (lstm_train.py:86-107,199; teacher.py:17-20), computed
+ * natively for tf_checkpoint.py (slicing-by-8). */
+uint32_t rd_crc32c(const uint8_t* data, int64_t n, uint32_t crc);
+
 /* Which kernel variant / library build is loaded (for provenance checks). */
 const char* rd_version(void);
 const char* rd_last_error(void);

@@ -51,6 +51,10 @@ int rd_comm_create(rd_comm** out, const uint8_t* id, int nranks, int rank, int d
 int rd_comm_allreduce_f32(rd_comm* c, float* buf, int64_t n, void* hip_stream);
 
 int rd_comm_nranks(const rd_comm* c);
+/* RCCL's own view of the communicator: ncclCommCount, ncclCommUserRank, ncclCommCuDevice
+ * (from_rccl = 1); for an xGMI communicator (no RCCL object) the values it was created with
+ * (from_rccl = 0).  Host-synchronous. */
+int rd_comm_query(rd_comm* c, int* count, int* user_rank, int* device, int* from_rccl);
 int rd_comm_destroy(rd_comm* c);
 
 /* The same exchange without RCCL: a one-shot push over xGMI (rd_xgmi.hip).  Each rank

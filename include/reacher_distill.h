@@ -119,6 +119,17 @@ int rdd_reset(rdd_trainer* tr);
 int rdd_rollout(rdd_trainer* tr);
 int rdd_apply(rdd_trainer* tr);
 int rdd_step(rdd_trainer* tr);
+/* One optimiser step of K = accum_steps env steps in ONE rollout launch (SURVEY.md §8d's
+ * K = 50 reading, the reference's MpiAdam step per batch of backup/student_rollout.py:658-709):
+ * the weight images stay in LDS and the per-workgroup gradient partials in registers over
+ * the K env steps (the student is frozen between optimiser steps, and each env's next step
+ * depends only on its own state), so the image prologue, the partial row, the reduction and
+ * the launch gaps are paid once per K env steps.  The same gradient as K x (rdd_launch_stage
+ * ROLLOUT, REDUCE(_ACCUM)) up to f32 reordering of the sums, the same env states (bitwise)
+ * and metrics slot.  rdd_rollout_accum: the launch + reduction into rdd_grad_buffer() and
+ * env clock += K; rdd_step_accum: + the bound all-reduce + Adam.  accum_steps <= 1: K = 1. */
+int rdd_rollout_accum(rdd_trainer* tr);
+int rdd_step_accum(rdd_trainer* tr);
 /* Observation-batch mode: the same fused teacher relabel + student forward/backward +
  * loss, on caller-given observation rows obs [n][11] (device) instead of the envs' state,
  * and no env step -- the reference's training on windows drawn from its dataset buffer

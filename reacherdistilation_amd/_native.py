@@ -38,6 +38,7 @@ SIGNATURES = {
     "rd_get_state": (INT, [P, P, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "rd_set_reset_mode": (INT, [P, INT, P, I32]),
     "rd_gym_reset_draws": (INT, [U64, I32, P]),
+    "rd_crc32c": (ctypes.c_uint32, [P, I64, ctypes.c_uint32]),
     "rd_version": (ctypes.c_char_p, []),
     "rd_last_error": (ctypes.c_char_p, []),
     # reacher_comm.h
@@ -46,6 +47,7 @@ SIGNATURES = {
     "rd_comm_create": (INT, [ctypes.POINTER(P), P, INT, INT, INT, ctypes.c_double]),
     "rd_comm_allreduce_f32": (INT, [P, P, I64, P]),
     "rd_comm_nranks": (INT, [P]),
+    "rd_comm_query": (INT, [P, P, P, P, P]),
     "rd_comm_destroy": (INT, [P]),
     "rd_xcomm_create": (INT, [ctypes.POINTER(P), INT, INT, INT, I64, ctypes.c_double, P]),
     "rd_xcomm_connect": (INT, [P, P]),

@@ -29,6 +29,17 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Werror",
           "-Wno-unused-function", "-munsafe-fp-atomics"]
 LDFLAGS = ["-shared", f"--offload-arch={ARCH}", "-ldl"]
+# Per-source flags.  distill.hip (the fused rollout) is compiled without SLP vectorisation: the
+# SLP pass packed the producer's dW3 / db3 accumulators into v_pk_fma_f32 / v_pk_add_f32 at the
+# tile loop's latch, whose operands the next tile's first LDS loads overwrite; on gfx950 a
+# packed-f32 op queued behind MFMAs can read its operands after such a load landed, and lanes
+# 48-63 of gw3b came out different run to run (DESIGN.md §3 "PKWAR", scripts/isa/hazards.py).
+# The packed tanh / split pairs written explicitly as f32x2 stay.
+SRC_FLAGS = {"distill.hip": ["-fno-slp-vectorize"]}
+
+
+def src_flags(path):
+    return SRC_FLAGS.get(os.path.basename(path), [])
 FLAGS = CFLAGS + LDFLAGS   # one-command form (resource_usage, scripts)
 
 
@@ -62,7 +73,7 @@ def _link(out, opts=(), verbose=True):
 
     def cc(pair):
         s, o = pair
-        cmd = [HIPCC, *CFLAGS, *opts, "-c", "-o", o, s]
+        cmd = [HIPCC, *CFLAGS, *src_flags(s), *opts, "-c", "-o", o, s]
         r = subprocess.run(cmd, capture_output=True, text=True)
         return cmd, r
 
@@ -91,7 +102,7 @@ def build(force: bool = False, verbose: bool = True, extra=()):
 def resource_usage():
     """Print per-kernel VGPR/SGPR/LDS/occupancy (hipcc -Rpass-analysis)."""
     for s in sources():
-        subprocess.call([HIPCC, *CFLAGS, "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/dev/null", s])
+        subprocess.call([HIPCC, *CFLAGS, *src_flags(s), "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/dev/null", s])
 
 
 def build_stamps():

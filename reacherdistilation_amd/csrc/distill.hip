@@ -157,6 +157,7 @@ struct RolloutArgs {
     int loss, act_student, stagger;
     float inv_n_global;
     int gs;                                // envs per group (16, 32 or 64)
+    int ksteps;                            // env steps of this launch (rdd_step_accum: accum_steps)
     unsigned long long* dbg;               // RD_STAMPS builds: [grid*WAVES][NSTAMP] stamp sums
     const float* obs_in;                   // observation-batch mode: [n][11] rows, no env step
     const float* timg;                     // prepacked LDS images (pack_net_kernel)
@@ -1039,6 +1040,12 @@ __device__ __forceinline__ void copy_images(float* L, const float* ta, const flo
     }
 }
 
+// kTanhScale * x as four scalar multiplies: a vector multiply would be a v_pk_mul_f32, and packed-f32
+// ops are kept out of the rollout's hot loops (PKWAR)
+__device__ __forceinline__ f32x4 scale4(f32x4 x) {
+    return f32x4{kTanhScale * x[0], kTanhScale * x[1], kTanhScale * x[2], kTanhScale * x[3]};
+}
+
 // bf16-student forward of a 16-env tile (same outputs/layouts as mlp_forward).
 __device__ __forceinline__ void mlp_forward_bf16(const float* L, const float* ob, int j, int g, f32x4 (&H1)[4],
                                                  f32x4 (&H2)[4], float& m0, float& m1) {
@@ -1058,7 +1065,7 @@ __device__ __forceinline__ void mlp_forward_bf16(const float* L, const float* ob
     for (int fb = 0; fb < 4; ++fb) acc[fb] = mfma_k32(ldbf8(L + NB_W1, ((g * 4 + fb) * 16 + j) * 8), zb, acc[fb]);
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
-        H1[fb] = tanh4(kTanhScale * acc[fb]);
+        H1[fb] = tanh4(scale4(acc[fb]));
     // layer 2: two K = 32 steps over the permuted feature order kperm
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) acc[fb] = ld4(L + NB_B2 + 16 * fb + 4 * g);
@@ -1074,7 +1081,7 @@ __device__ __forceinline__ void mlp_forward_bf16(const float* L, const float* ob
     for (int fb = 0; fb < 4; ++fb) {
         const f32x4 wa = ld4(L + NB_W3 + (16 * fb + 4 * g) * 2);
         const f32x4 wb = ld4(L + NB_W3 + (16 * fb + 4 * g) * 2 + 4);
-        H2[fb] = tanh4(kTanhScale * acc[fb]);
+        H2[fb] = tanh4(scale4(acc[fb]));
         p0 = fmaf(H2[fb][0], wa[0], p0); p1 = fmaf(H2[fb][0], wa[1], p1);
         p0 = fmaf(H2[fb][1], wa[2], p0); p1 = fmaf(H2[fb][1], wa[3], p1);
         p0 = fmaf(H2[fb][2], wb[0], p0); p1 = fmaf(H2[fb][2], wb[1], p1);
@@ -1203,7 +1210,9 @@ static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NETB_S
 // student, one 16-env tile per pair's group, launch_rollout): pairs 0, 1 own the groups and
 // pairs 2, 3 run their tiles' teacher forwards on the other two SIMDs
 constexpr int MD_TEACHER = 0, MD_ROWS = 1, MD_HELPER = 2;
-template <bool BS, bool SPL, bool CP, int MD>
+// KS: a.ksteps env steps in one launch (rdd_step_accum); the K = 1 instances are compiled without
+// the step loop.
+template <bool BS, bool SPL, bool CP, int MD, bool KS = false>
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     constexpr bool TGT = MD == MD_ROWS, HLP = MD == MD_HELPER;
     static_assert(!HLP || !BS, "helper pairs: f32 student kernels only");
@@ -1227,6 +1236,15 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     // HLP: the owner pairs 0, 1 take the groups (one each), pairs 2, 3 none (they help).  The
     // layout holds at most one group per owner (launch_rollout): a launch that breaks this ends
     // at once with the hand-off error raised (rdd_counter reports it)
+    // KS (K env steps in one launch): the producer re-reads the state its own lanes wrote, so
+    // the consumer-side env step (CP), the helper layout and the observation modes stay K = 1
+    static_assert(!KS || (!CP && MD == MD_TEACHER), "K-step launches: teacher mode, producer-side env step");
+    if constexpr (KS) {
+        if (a.obs_in) {
+            if (threadIdx.x == 0) __hip_atomic_store(a.ctl + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
     if constexpr (HLP) {
         if (ngroups > 2u * gridDim.x) {
             if (threadIdx.x == 0) __hip_atomic_store(a.ctl + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1281,7 +1299,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     // snapshot of the step words for reduce_adam_kernel, which rewrites ctl[0..3]; ctl[12]
     // tells it whether this launch stepped the envs (the env clock advances only then)
     if (blockIdx.x == 0 && threadIdx.x < 4) a.ctl[4 + threadIdx.x] = a.ctl[threadIdx.x];
-    if (blockIdx.x == 0 && threadIdx.x == 4) a.ctl[12] = a.obs_in ? 0u : 1u;
+    if (blockIdx.x == 0 && threadIdx.x == 4) a.ctl[12] = a.obs_in ? 0u : (KS ? (uint32_t)a.ksteps : 1u);
     __syncthreads();
     STAMP(1);
 
@@ -1328,8 +1346,16 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 STAMP(23);
             }
         }
+        // K env steps per launch (rdd_step_accum): the images stay in LDS and the gradient
+        // partials in registers over all K; a pair that owns one group keeps its envs' state in
+        // registers from one step to the next (the rest re-read the state they wrote)
+        // (KS: st0 carries it over)
+        const uint32_t K = KS ? (uint32_t)a.ksteps : 1u;
+        const bool resident = KS && gfirst + gstride >= ngroups;
+        for (uint32_t kk = 0;; ++kk) {   // (K = 1: no loop; the K = 1 instances' ISA is that of round 4)
         for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++k) {
             STAMP(8);
+            const uint32_t Ck = C + kk;   // the episode clock of this env step
             const uint32_t base = grp * (uint32_t)gs;
             const uint32_t i = base + (uint32_t)lane;   // n <= 2^31 (rdd_create)
             const bool lvalid = lane < gs && i < n32;   // this lane has an env
@@ -1338,6 +1364,9 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             rd::State st{};   // this lane's env, kept in registers for the env.step after the tiles
             if (k == 0) {
                 st = st0;   // observations formed in the prologue
+            } else if (resident) {
+                if (lvalid) st = st0;   // the state this lane stepped at the previous env step
+                group_obs(k, i, lvalid, st);
             } else {
                 if (!a.obs_in && lvalid) load_state(a.state, a.n, i, st);
                 group_obs(k, i, lvalid, st);
@@ -1381,14 +1410,16 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                         else mlp_forward_pair<true>(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
                     }
                 } else if constexpr (BS) {
-                    // CP: in this kernel's schedule the compiler issues loads into the SrcC
+                    // CP, KS: in these kernels' schedules the compiler issues loads into the SrcC
                     // registers of the exact teacher's f32 MFMAs: fenced (see mfma())
                     if constexpr (SPL) mlp_forward_split(LT, obt, j, g, mt0, mt1);
-                    else mlp_forward<CP>(LT, obt, j, g, H1, H2, mt0, mt1);
+                    else mlp_forward<CP || KS>(LT, obt, j, g, H1, H2, mt0, mt1);
                     mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
                 } else {
+                    // KS (exact f32): the K-step kernel's schedule puts a W3 load into the SrcC of
+                    // layer 2's last in-flight f32 MFMA (hazards.py LDSRC): fenced (see mfma())
                     if constexpr (SPL) mlp_forward_pair_split(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
-                    else mlp_forward_pair(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                    else mlp_forward_pair<KS>(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
                 }
                 STAMP(12);
                 // loss
@@ -1463,10 +1494,13 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     // the helper pair steps these envs (above)
                 } else {
                     wave_sync();   // act[] rows were written by the g = 0 lanes of each tile
-                    if (lane < gs) met_r += env_step_group(a, C, i, lvalid, act[lane * 2], act[lane * 2 + 1], st, met_n);
+                    if (lane < gs) met_r += env_step_group(a, Ck, i, lvalid, act[lane * 2], act[lane * 2 + 1], st, met_n);
                 }
             }
+            if constexpr (KS) st0 = st;
             STAMP(5);
+        }
+        if (!KS || !ok || kk + 1 >= K) break;
         }
         // ------------------------------------------------------------ this wave's share
 #pragma unroll
@@ -1706,7 +1740,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             return true;
         };
         // after the last tile of a group (envs base ...): CP steps the envs
-        auto end_group = [&](uint32_t base) {
+        auto end_group = [&](uint32_t base, uint32_t Ck) {
             const uint32_t i = base + (uint32_t)lane;
             const bool lvalid = lane < gs && i < n32;
             if constexpr (CP) {
@@ -1716,7 +1750,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 } else if (lane < gs) {   // act[] rows: published with the group's tiles
                     rd::State st{};
                     if (lvalid) load_state(a.state, a.n, i, st);
-                    met_r += env_step_group(a, C, i, lvalid, act0, act1, st, met_n);
+                    met_r += env_step_group(a, Ck, i, lvalid, act0, act1, st, met_n);
                 }
                 STAMP(5);
             }
@@ -1768,12 +1802,15 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 STAMP(22);
             }
         }
+        for (uint32_t kk = 0;; ++kk) {
         for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride) {
             const uint32_t base = grp * (uint32_t)gs;
             const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
             for (int t = 0; ok && t < ntile; ++t) ok = bwd_tile(t);
             if (!ok) break;
-            end_group(base);
+            end_group(base, C + kk);
+        }
+        if (!KS || !ok || kk + 1 >= (uint32_t)a.ksteps) break;
         }
         // ------------------------------------------------------------ this wave's share
 #pragma unroll
@@ -2016,8 +2053,9 @@ ReduceArgs reduce_args(const rdd_trainer* t, int reduce, int adam, int accum) {
 }
 
 int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs = 0, int64_t n_obs_global = 0,
-                   const float* tflat_in = nullptr) {
+                   const float* tflat_in = nullptr, int ksteps = 1) {
     RolloutArgs a;
+    a.ksteps = ksteps;
     a.n = obs_in ? n_obs : t->cfg.n_envs;
     a.obs_in = obs_in;
     a.timg = t->timg;
@@ -2047,13 +2085,17 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     // 3 run the owners' teacher forwards on the other SIMDs instead (c2: DESIGN.md §3)
     const int64_t ngroups = (a.n + a.gs - 1) / a.gs;
     const bool hlp = !bs && !tflat_in && a.gs == TILE && ngroups <= 2 * (int64_t)t->ws_rows &&
-                     t->cfg.group_envs == 0;   // a fixed group size keeps the plain layout
+                     t->cfg.group_envs == 0 &&   // a fixed group size keeps the plain layout
+                     ksteps == 1;                // K env steps per launch: the plain layout
     if (hlp) grid = (int)((ngroups + 1) / 2);
     t->last_grid = grid;
     void (*k)(RolloutArgs) =
         bs ? (spl ? rollout_kernel<true, true, true, MD_TEACHER> : rollout_kernel<true, false, true, MD_TEACHER>)
            : hlp ? (spl ? rollout_kernel<false, true, false, MD_HELPER> : rollout_kernel<false, false, false, MD_HELPER>)
                  : (spl ? rollout_kernel<false, true, false, MD_TEACHER> : rollout_kernel<false, false, false, MD_TEACHER>);
+    if (ksteps > 1)   // K steps per launch: the producer steps the envs it reads (no CP)
+        k = bs ? (spl ? rollout_kernel<true, true, false, MD_TEACHER, true> : rollout_kernel<true, false, false, MD_TEACHER, true>)
+               : (spl ? rollout_kernel<false, true, false, MD_TEACHER, true> : rollout_kernel<false, false, false, MD_TEACHER, true>);
     if (tflat_in)   // the teacher is not run: the bf16 student's kernel does not depend on the teacher's mode
         k = bs ? rollout_kernel<true, false, false, MD_ROWS>
                : (spl ? rollout_kernel<false, true, false, MD_ROWS> : rollout_kernel<false, false, false, MD_ROWS>);
@@ -2208,6 +2250,14 @@ static int comm_ok(const rdd_trainer* t, const char* what) {
     return RD_OK;
 }
 
+int rdd_rollout_accum(rdd_trainer* t) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdd_rollout_accum: null handle");
+    rd::DeviceGuard g(t->device);
+    RD_HIP(g.err, "rdd_rollout_accum: hipSetDevice");
+    if (int rc = launch_rollout(t, nullptr, 0, 0, nullptr, t->accum)) return rc;
+    return launch_reduce(t, 1, 0);
+}
+
 int rdd_apply(rdd_trainer* t) {
     if (!t) return rd::set_error(RD_EINVAL, "rdd_apply: null handle");
     if (int rc = comm_ok(t, "rdd_apply")) return rc;
@@ -2224,6 +2274,18 @@ int rdd_step(rdd_trainer* t) {
     if (int rc = launch_rollout(t)) return rc;
     if (!t->comm) return launch_reduce(t, 1, 1);
     // sharded step: the exchange sits between the reduction and Adam, all on one stream
+    if (int rc = launch_reduce(t, 1, 0)) return rc;
+    if (int rc = rd_comm_allreduce_f32(t->comm, t->grad, P_TOT, t->stream)) return rc;
+    return launch_reduce(t, 0, 1);
+}
+
+int rdd_step_accum(rdd_trainer* t) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdd_step_accum: null handle");
+    if (int rc = comm_ok(t, "rdd_step_accum")) return rc;
+    rd::DeviceGuard g(t->device);
+    RD_HIP(g.err, "rdd_step_accum: hipSetDevice");
+    if (int rc = launch_rollout(t, nullptr, 0, 0, nullptr, t->accum)) return rc;
+    if (!t->comm) return launch_reduce(t, 1, 1);
     if (int rc = launch_reduce(t, 1, 0)) return rc;
     if (int rc = rd_comm_allreduce_f32(t->comm, t->grad, P_TOT, t->stream)) return rc;
     return launch_reduce(t, 0, 1);

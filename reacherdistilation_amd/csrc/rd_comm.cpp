@@ -30,6 +30,9 @@ struct Rccl {
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommCount) count = nullptr;
+    decltype(&ncclCommUserRank) user_rank = nullptr;
+    decltype(&ncclCommCuDevice) cu_device = nullptr;
     bool ok = false;
     char why[256] = "";
 };
@@ -51,8 +54,11 @@ const Rccl& rccl() {
         r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
         r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
         r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+        r.count = (decltype(r.count))dlsym(h, "ncclCommCount");
+        r.user_rank = (decltype(r.user_rank))dlsym(h, "ncclCommUserRank");
+        r.cu_device = (decltype(r.cu_device))dlsym(h, "ncclCommCuDevice");
         r.ok = r.get_unique_id && r.init_rank_config && r.async_error && r.abort && r.all_reduce && r.destroy &&
-               r.error_string;
+               r.error_string && r.count && r.user_rank && r.cu_device;
         if (!r.ok) snprintf(r.why, sizeof r.why, "librccl.so.1 lacks an nccl* entry point");
     });
     return r;
@@ -152,6 +158,24 @@ int rd_comm_allreduce_f32(rd_comm* c, float* buf, int64_t n, void* hip_stream) {
 }
 
 int rd_comm_nranks(const rd_comm* c) { return c ? c->nranks : 0; }
+
+int rd_comm_query(rd_comm* c, int* count, int* user_rank, int* device, int* from_rccl) {
+    if (!c || !count || !user_rank || !device || !from_rccl) return rd::set_error(RD_EINVAL, "rd_comm_query: bad argument");
+    if (c->xgmi || !c->comm) {   // the xGMI push has no RCCL communicator: what it was created with
+        *count = c->nranks;
+        *user_rank = c->rank;
+        *device = c->device;
+        *from_rccl = 0;
+        return RD_OK;
+    }
+    if (int rc = wait_ready(c, "rd_comm_query")) return rc;
+    const Rccl& r = rccl();
+    if (ncclResult_t e = r.count(c->comm, count); e != ncclSuccess) return nccl_fail(e, "ncclCommCount");
+    if (ncclResult_t e = r.user_rank(c->comm, user_rank); e != ncclSuccess) return nccl_fail(e, "ncclCommUserRank");
+    if (ncclResult_t e = r.cu_device(c->comm, device); e != ncclSuccess) return nccl_fail(e, "ncclCommCuDevice");
+    *from_rccl = 1;
+    return RD_OK;
+}
 
 int rd_comm_destroy(rd_comm* c) {
     if (!c) return RD_OK;

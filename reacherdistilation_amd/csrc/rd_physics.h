@@ -16,6 +16,13 @@
 
 namespace rd {
 
+// Rounding fixed by the source, not by the inlining context: within these functions a * b + c
+// fuses into one FMA only inside one expression (clang fp contract "on"), never across
+// statements by the backend (-ffp-contract=fast-honor-pragmas, HIP's default).  So every kernel
+// that inlines the env step -- the fused rollout's K = 1 and K-step instances, the helper pairs,
+// the gym-API env kernel, PPO's rollout -- rounds it identically (bitwise the same states).
+#define FP_SOURCE_ROUNDING() _Pragma("clang fp contract(on)")
+
 // ------------------------------------------------------------------ constants
 constexpr double kPi = 3.14159265358979323846;
 constexpr double kMl = 1000.0 * kPi * 0.01 * 0.01 * 0.11;
@@ -48,6 +55,7 @@ struct State {
 // angles of episodes at most 50 steps old (|q| < ~200 rad).
 template <bool kWideRange = true>
 __device__ __forceinline__ void sincos_acc(float x, float* s, float* c) {
+    FP_SOURCE_ROUNDING();
     if (kWideRange && __builtin_expect(fabsf(x) > 8192.0f, 0)) {
         sincosf(x, s, c);
         return;
@@ -74,6 +82,7 @@ __device__ __forceinline__ void sincos_acc(float x, float* s, float* c) {
 // One MuJoCo forward pass -> constrained qacc of the two arm dofs; (s, c) = sin, cos q1.
 __device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, float v1, float c0, float c1,
                                         float& a0, float& a1) {
+    FP_SOURCE_ROUNDING();
     const float A0 = (float)kA0, I2 = (float)kI2, HC = (float)kHC;
     const float m11 = A0 + I2 + 2.0f * HC * c + 1.0f;
     const float m12 = I2 + HC * c;
@@ -104,6 +113,7 @@ __device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, fl
 
 template <bool kWideRange = true>
 __device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, float c1, float& a0, float& a1) {
+    FP_SOURCE_ROUNDING();
     float s, c;
     sincos_acc<kWideRange>(q1, &s, &c);
     qacc_sc(q1, s, c, v0, v1, c0, c1, a0, a1);
@@ -113,6 +123,7 @@ __device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, flo
 // float32 ctrl cost of the UNCLIPPED action), advances the state by 2 RK4 substeps.
 template <bool kWideRange = true>
 __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
+    FP_SOURCE_ROUNDING();
     const float h = 0.01f;
     const float r = -__builtin_amdgcn_sqrtf(st.dx * st.dx + st.dy * st.dy) - (a0 * a0 + a1 * a1);   // 1 ulp
     const float c0 = fminf(fmaxf(a0, -1.0f), 1.0f);   // ctrlrange +-1 (ctrllimited)
@@ -150,6 +161,7 @@ __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
 
 // reset_model + set_state + sim.forward(): kinematics fresh at the reset position.
 __device__ __forceinline__ void env_reset(State& st, const float* d /*q0 q1 v0 v1 tx ty*/) {
+    FP_SOURCE_ROUNDING();
     st.q0 = d[0]; st.q1 = d[1]; st.v0 = d[2]; st.v1 = d[3]; st.tx = d[4]; st.ty = d[5];
     float s0, c0, s01, c01;
     sincos_acc(st.q0, &s0, &c0);
@@ -161,6 +173,7 @@ __device__ __forceinline__ void env_reset(State& st, const float* d /*q0 q1 v0 v
 // gym ReacherEnv._get_obs: [cos q, sin q, target, qvel, fingertip - target (x,y,0)]
 template <bool kWideRange = true>
 __device__ __forceinline__ void observe(const State& st, float* ob) {
+    FP_SOURCE_ROUNDING();
     float s0, c0, s1, c1;
     sincos_acc<kWideRange>(st.q0, &s0, &c0);
     sincos_acc<kWideRange>(st.q1, &s1, &c1);
@@ -189,6 +202,7 @@ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 
 // draws (q0,q1,v0,v1,tx,ty) with ReacherEnv.reset_model's ranges
 __device__ __forceinline__ void philox_draw(uint64_t seed, uint64_t env_id, uint32_t episode, float d[6]) {
+    FP_SOURCE_ROUNDING();
     uint32_t o[4], p[4];
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     philox((uint32_t)env_id, (uint32_t)(env_id >> 32), episode, 0u, k0, k1, o);

@@ -130,6 +130,19 @@ class RcclComm:
                                                   nat.stream_handle(self.device)), "rd_comm_allreduce_f32")
         return t
 
+    def query(self) -> dict:
+        """RCCL's own view of this communicator (rd_comm_query: ncclCommCount, ncclCommUserRank,
+        ncclCommCuDevice), not the values it was created with; an xGMI communicator reports
+        those (from_rccl False)."""
+        import ctypes
+
+        from . import _native as nat
+        c, r, d, f = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        nat.check(self._lib.rd_comm_query(self.handle, ctypes.byref(c), ctypes.byref(r), ctypes.byref(d),
+                                          ctypes.byref(f)), "rd_comm_query")
+        return {"count": c.value, "user_rank": r.value, "device": d.value, "from_rccl": bool(f.value),
+                "created_rank": self.rank, "created_world": self.world}
+
     def self_check(self) -> bool:
         """One all-reduce of a known pattern: every element must come back as the sum over
         ranks (the bench falls back to torch's collective if not)."""

@@ -50,6 +50,8 @@ nat.register({
     "rdd_rollout": (INT, [P]),
     "rdd_apply": (INT, [P]),
     "rdd_step": (INT, [P]),
+    "rdd_rollout_accum": (INT, [P]),
+    "rdd_step_accum": (INT, [P]),
     "rdd_launch_stage": (INT, [P, INT]),
     "rdd_grad_buffer": (P, [P]),
     "rdd_bind_grad_buffer": (INT, [P, P]),
@@ -195,6 +197,27 @@ class DistillTrainer:
             self._k = 0 if last else k + 1
         self.steps += 1
 
+    def step_accum(self):
+        """One optimiser step of K = accum_steps env steps in ONE rollout launch
+        (rdd_step_accum): the weight images stay in LDS and the gradient partials in registers
+        over the K env steps, then one reduction, (all-reduce,) TF1 Adam.  Same result as K
+        step() calls up to f32 reordering of the gradient sums; the envs step bitwise alike."""
+        K = max(1, int(self.cfg.accum_steps))
+        if self._k:
+            raise RuntimeError("step_accum inside a staged accumulation (step() was called "
+                               f"{self._k} of {K} times)")
+        if self.world == 1 or self.comm is not None:
+            nat.check(self._lib.rdd_step_accum(self._h), "rdd_step_accum")
+        else:
+            nat.check(self._lib.rdd_rollout_accum(self._h), "rdd_rollout_accum")
+            self.allreduce_grad()
+            nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
+        self.steps += K
+
+    def rollout_accum(self):
+        """The K env steps of step_accum and their gradient sum in grad() (no Adam)."""
+        nat.check(self._lib.rdd_rollout_accum(self._h), "rdd_rollout_accum")
+
     # -- observation-batch mode (the reference's dataset-window training) ---------------
     def step_obs(self, obs: torch.Tensor):
         """One distillation step on given observation rows [n, 11] (no env step): teacher
@@ -259,21 +282,23 @@ class DistillTrainer:
     def set_stream(self, stream: torch.cuda.Stream):
         nat.check(self._lib.rdd_set_stream(self._h, ctypes.c_void_p(stream.cuda_stream)), "rdd_set_stream")
 
-    def capture(self, steps: int = 1) -> torch.cuda.CUDAGraph:
+    def capture(self, steps: int = 1, fused: bool = False) -> torch.cuda.CUDAGraph:
         """Capture `steps` single-rank steps into a HIP graph (replay = `steps` steps, no
-        host launches).  The trainer's stream is restored afterwards."""
+        host launches).  fused: `steps` step_accum() calls (K env steps each).  The trainer's
+        stream is restored afterwards."""
         if self.world != 1:
             raise RuntimeError("graph capture is for the single-rank step")
         g = torch.cuda.CUDAGraph()
         prev = torch.cuda.current_stream(self.device)
         torch.cuda.synchronize(self.device)
-        if max(1, int(self.cfg.accum_steps)) > 1 and steps % self.cfg.accum_steps:
+        if not fused and max(1, int(self.cfg.accum_steps)) > 1 and steps % self.cfg.accum_steps:
             raise ValueError("capture whole optimiser steps: steps must be a multiple of accum_steps")
+        s0 = self.steps
         with torch.cuda.graph(g):
             self.set_stream(torch.cuda.current_stream(self.device))
             for _ in range(steps):
-                self.step()
-        self.steps -= steps   # capture only records launches
+                self.step_accum() if fused else self.step()
+        self.steps = s0   # capture only records launches
         self.set_stream(prev)
         return g
 

@@ -42,12 +42,27 @@ for _i in range(256):
 _TABLE = np.array(_TABLE, np.uint32)
 
 
-def crc32c(data: bytes, crc: int = 0) -> int:
+def crc32c_py(data: bytes, crc: int = 0) -> int:
+    """The per-byte table form (the definition the native one is tested against)."""
     c = crc ^ 0xFFFFFFFF
     t = _TABLE
     for b in data:
         c = int(t[(c ^ b) & 0xFF]) ^ (c >> 8)
     return c ^ 0xFFFFFFFF
+
+
+def crc32c(data: bytes, crc: int = 0) -> int:
+    """CRC32C of `data`, continuing from `crc`: the native slicing-by-8 form (rd_crc32c in
+    libreacher.so; ~1 GB/s, where the per-byte loop runs at ~2 MB/s), else crc32c_py."""
+    try:
+        from . import _native
+        lib = _native.load()
+    except Exception:   # noqa: BLE001  (host utility: the library is the fast path, not a requirement)
+        return crc32c_py(data, crc)
+    import ctypes
+    b = bytes(data)
+    buf = ctypes.create_string_buffer(b, len(b)) if b else None
+    return int(lib.rd_crc32c(buf, len(b), crc & 0xFFFFFFFF))
 
 
 def _mask(crc: int) -> int:

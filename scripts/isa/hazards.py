@@ -27,6 +27,17 @@ from four rollout kernels and one class to EVERY function of every .hip source a
   TRANS  a VALU reads the result of a transcendental (v_exp/log/rcp/rsq/sqrt/sin/cos) 1
   SGPRV  a VALU-written SGPR (v_readfirstlane/readlane/cmp) read by a VMEM     5
          instruction as address / descriptor / offset (§5.7 item 2: `s_nop 4`)
+  PKWAR  a DS / VMEM load writes a source VGPR of an earlier packed-f32 VALU   completion
+         instruction (v_pk_fma/mul/add_f32) that nothing has read the result of yet: (an
+         the load may land before the packed op has read that operand for its last  interlock)
+         lanes (48-63).  Found in round 5: the rollout's dW3 accumulators, 16
+         v_pk_fma_f32 at the tile loop's latch whose H2 / dmean sources the next tile's first
+         LDS loads overwrite -- gw3b[.][0, 2] (the low results reading src1's high dword) of
+         lanes 48-63 came out different run to run in the K-step launch (3/3 launches at c3),
+         and the same signature is the rounds 2-4 "first launch differs in a lanes-48-63 dW3
+         entry".  No wait-state count is known to suffice (the loads came 18+ instructions
+         after), so the requirement is an interlock: some instruction reads the packed op's
+         destination before the load issues (scan_pkwar).
 
 The VALU-side requirements are calibrated against hipcc's own output (the smallest distance it
 emits for that class in any product kernel: e.g. it writes an in-flight f32 MFMA's SrcC with a
@@ -257,6 +268,46 @@ def scan_code(code, window=24):
     return sorted(best.values(), key=lambda h: (h[3], h[5], h[0]))
 
 
+PK_F32 = ("v_pk_fma_f32", "v_pk_mul_f32", "v_pk_add_f32")
+
+
+def scan_pkwar(code, window=64):
+    """PKWAR hits [(kind, instructions between, window + 1, line, op, line2, instruction2)] of one
+    function (always below the requirement: every hit is a violation): a load whose
+    destination overlaps a source VGPR of an earlier v_pk_*_f32 on some control-flow path with
+    no instruction reading that packed op's destination in between (the RAW interlock that
+    makes the op complete first).  A VALU write of the sources (in-order behind the packed op)
+    or of the destination ends the path."""
+    insts, succ = _cfg(code)
+    parsed = [(ln, l, *classify(l)) for ln, l in insts]
+    out = {}
+    for idx, (ln, l, op, w, r, sd) in enumerate(parsed):
+        if not op.startswith(PK_F32):
+            continue
+        dst, src = vset(w), vset(r) - vset(w)
+        if not src:
+            continue
+        seen = {}
+        stack = [(k, 1) for k in succ[idx]]
+        while stack:
+            k2, steps = stack.pop()
+            if k2 >= len(parsed) or steps > window or seen.get(k2, 1 << 30) <= steps:
+                continue
+            seen[k2] = steps
+            ln2, l2, op2, w2, r2, sd2 = parsed[k2]
+            if vset(r2) & dst:   # the packed op's result is read: interlocked, complete
+                continue
+            ld2 = op2.startswith(LOAD) or (op2.startswith(VMEM) and "atomic" in op2) or "_rtn" in op2
+            if ld2 and vset(w2) & src:
+                if (idx, k2) not in out or steps < out[(idx, k2)][1]:
+                    out[(idx, k2)] = ("PKWAR", steps, window + 1, ln, op, ln2, l2)
+                continue
+            if op2.startswith("v_") and not op2.startswith(("v_mfma", "v_smfmac")) and vset(w2) & (src | dst):
+                continue
+            stack.extend((k3, steps + 1) for k3 in succ[k2])
+    return sorted(out.values(), key=lambda h: (h[3], h[5]))
+
+
 def scan(path, sym, window=24):
     """Hits of the first function whose name contains `sym` (round-3 interface), and its code."""
     fns = functions(path)
@@ -297,7 +348,7 @@ def main():
     for name, code in fns.items():
         if sym and sym not in name:
             continue
-        print(summary(name, scan_code(code, window), code, window))
+        print(summary(name, scan_code(code, window) + scan_pkwar(code), code, window))
 
 
 if __name__ == "__main__":

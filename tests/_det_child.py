@@ -21,6 +21,9 @@ CASES = {
     "c2_helper": dict(n_envs=4096, f32_split=True),
     "c3_kl": dict(n_envs=65536, loss="kl", f32_split=True),
     "c4_exact": dict(n_envs=262144, f32_split=False),
+    # the K-step launch (rdd_step_accum): two optimiser steps of K env steps each
+    "c3_k50": dict(n_envs=65536, loss="kl", f32_split=True, accum_steps=50),
+    "shard8_k50": dict(n_envs=32768, f32_split=True, accum_steps=50),
 }
 
 
@@ -38,7 +41,7 @@ def main(names):
         for _ in range(2):
             tr = DistillTrainer(DistillConfig(seed=11, **CASES[name]), device="cuda:0")
             for _ in range(2):
-                tr.step()
+                tr.step_accum() if CASES[name].get("accum_steps", 1) > 1 else tr.step()
             torch.cuda.synchronize()
             tr.counter()   # raises on a timed-out hand-off
             runs.append(digest(tr))

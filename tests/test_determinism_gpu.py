@@ -5,7 +5,9 @@ gradient entries of lane group 48-63) but its FIRST rollout in a process differe
 ones in c4 and the 300-workgroup grid (profiles/r04i_imgdma_nondeterminism.txt); the in-process
 repeat checks of the suite start after that launch.  Here each config runs in two fresh
 processes, two trainers each (the first trainer's launches are the process's first of that
-kernel): all four digests must be equal."""
+kernel): all four digests must be equal.  Round 5 adds the K-step launch (rdd_step_accum), whose
+first build reproduced the lanes-48-63 dW3 signature in most launches: the SLP-packed dW3
+accumulators at the tile loop's latch (PKWAR), now unpacked."""
 import json
 import os
 import subprocess
@@ -25,7 +27,7 @@ def _child(names):
 
 @pytest.mark.gpu
 def test_first_launch_of_a_process_is_reproducible():
-    names = ["c4_split", "grid300_split", "c5_bf16", "c2_helper", "c3_kl", "c4_exact"]
+    names = ["c4_split", "grid300_split", "c5_bf16", "c2_helper", "c3_kl", "c4_exact", "c3_k50", "shard8_k50"]
     a, b = _child(names), _child(names)
     bad = {n: (a[n], b[n]) for n in names if len(set(a[n] + b[n])) != 1}
     assert not bad, bad

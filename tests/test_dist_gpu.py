@@ -89,6 +89,11 @@ def test_native_rccl_allreduce_one_rank():
         torch.cuda.synchronize()
         assert torch.equal(x, want)
         assert c._lib.rd_comm_allreduce_f32(c.handle, None, 4, None) != 0   # bad argument -> error
+        # RCCL's own view of the communicator (ncclCommCount / UserRank / CuDevice)
+        cnt, r, d, f = (ctypes.c_int() for _ in range(4))
+        nat.check(c._lib.rd_comm_query(c.handle, ctypes.byref(cnt), ctypes.byref(r), ctypes.byref(d),
+                                       ctypes.byref(f)), "rd_comm_query")
+        assert (cnt.value, r.value, d.value, f.value) == (1, 0, 0, 1)
     finally:
         c.close()
 
@@ -127,6 +132,8 @@ def _rccl_rank(rank, world, port, out):
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     comm = RcclComm(dev, timeout=60.0)
     assert comm.self_check()
+    q = comm.query()
+    assert (q["count"], q["user_rank"], q["device"], q["from_rccl"]) == (world, rank, rank, True), q
     tr = DistillTrainer(DistillConfig(n_envs_global=N_GLOBAL, seed=7, lr=1e-3), device=dev,
                         rank=rank, world_size=world, comm=comm)
     for _ in range(STEPS):

@@ -41,16 +41,19 @@ def test_product_library_reads_no_environment(libpath):
 
 def test_consumer_side_step_only_for_the_bf16_student(libpath):
     blob = open(libpath, "rb").read()
-    names = set(re.findall(rb"rollout_kernelILb[01]ELb[01]ELb[01]ELi[0-9]E", blob))
+    names = set(re.findall(rb"rollout_kernelILb[01]ELb[01]ELb[01]ELi[0-9]ELb[01]E", blob))
     assert names, "rollout_kernel instantiations not found in the offload bundle"
-    # <bf16 student, f32 mode, consumer-side step, MD>: f32 student -> producer-side, bf16 ->
-    # consumer-side; MD 1 (rows: no env step) -> no consumer-side step, no teacher; MD 2 (helper
-    # pairs of a small batch) -> f32 student only
-    assert names == {b"rollout_kernelILb0ELb0ELb0ELi0E", b"rollout_kernelILb0ELb1ELb0ELi0E",
-                     b"rollout_kernelILb1ELb0ELb1ELi0E", b"rollout_kernelILb1ELb1ELb1ELi0E",
-                     b"rollout_kernelILb0ELb0ELb0ELi1E", b"rollout_kernelILb0ELb1ELb0ELi1E",
-                     b"rollout_kernelILb1ELb0ELb0ELi1E",
-                     b"rollout_kernelILb0ELb0ELb0ELi2E", b"rollout_kernelILb0ELb1ELb0ELi2E"}, sorted(names)
+    # <bf16 student, f32 mode, consumer-side step, MD, K steps per launch>: f32 student ->
+    # producer-side, bf16 -> consumer-side; MD 1 (rows: no env step) -> no consumer-side step, no
+    # teacher; MD 2 (helper pairs of a small batch) -> f32 student only; the K-step launches
+    # (rdd_step_accum) -> teacher mode, producer-side step, both students
+    assert names == {b"rollout_kernelILb0ELb0ELb0ELi0ELb0E", b"rollout_kernelILb0ELb1ELb0ELi0ELb0E",
+                     b"rollout_kernelILb1ELb0ELb1ELi0ELb0E", b"rollout_kernelILb1ELb1ELb1ELi0ELb0E",
+                     b"rollout_kernelILb0ELb0ELb0ELi1ELb0E", b"rollout_kernelILb0ELb1ELb0ELi1ELb0E",
+                     b"rollout_kernelILb1ELb0ELb0ELi1ELb0E",
+                     b"rollout_kernelILb0ELb0ELb0ELi2ELb0E", b"rollout_kernelILb0ELb1ELb0ELi2ELb0E",
+                     b"rollout_kernelILb0ELb0ELb0ELi0ELb1E", b"rollout_kernelILb0ELb1ELb0ELi0ELb1E",
+                     b"rollout_kernelILb1ELb0ELb0ELi0ELb1E", b"rollout_kernelILb1ELb1ELb0ELi0ELb1E"}, sorted(names)
 
 
 def _hz():
@@ -73,8 +76,8 @@ def product_isa():
     def cc(f):
         out = os.path.join(d, f[:-4] + ".s")
         subprocess.run([build.HIPCC, "-O3", "-std=c++17", f"--offload-arch={build.ARCH}", "-munsafe-fp-atomics",
-                        "-Wno-unused-command-line-argument", "--cuda-device-only", "-S", "-o", out,
-                        os.path.join(build.CSRC, f)], check=True, capture_output=True)
+                        *build.src_flags(f), "-Wno-unused-command-line-argument", "--cuda-device-only", "-S",
+                        "-o", out, os.path.join(build.CSRC, f)], check=True, capture_output=True)
         return f, out
 
     with ThreadPoolExecutor(len(srcs)) as ex:
@@ -89,13 +92,39 @@ def test_no_load_into_an_inflight_f32_mfma_srcc(product_isa):
     within the scan at all (their f32 MFMAs are dW1 only)."""
     hz = _hz()
     out = product_isa["distill.hip"]
-    for sym, split in (("rollout_kernelILb0ELb0ELb0ELi0E", False), ("rollout_kernelILb0ELb1ELb0ELi0E", True),
-                       ("rollout_kernelILb1ELb0ELb1ELi0E", False), ("rollout_kernelILb1ELb1ELb1ELi0E", True),
-                       ("rollout_kernelILb0ELb0ELb0ELi2E", False), ("rollout_kernelILb0ELb1ELb0ELi2E", True)):
+    for sym, split in (("rollout_kernelILb0ELb0ELb0ELi0ELb0E", False), ("rollout_kernelILb0ELb1ELb0ELi0ELb0E", True),
+                       ("rollout_kernelILb1ELb0ELb1ELi0ELb0E", False), ("rollout_kernelILb1ELb1ELb1ELi0ELb0E", True),
+                       ("rollout_kernelILb0ELb0ELb0ELi2ELb0E", False), ("rollout_kernelILb0ELb1ELb0ELi2ELb0E", True),
+                       ("rollout_kernelILb0ELb0ELb0ELi0ELb1E", False), ("rollout_kernelILb0ELb1ELb0ELi0ELb1E", True),
+                       ("rollout_kernelILb1ELb0ELb0ELi0ELb1E", False), ("rollout_kernelILb1ELb1ELb0ELi0ELb1E", True)):
         hits = [h for h in hz.scan(out, sym, 40)[0] if h[0] == "LDSRC" and "16x16x4" in h[4]]
         assert all(h[1] >= 10 for h in hits), (sym, [h[:6] for h in hits if h[1] < 10][:5])
         if split:
             assert not hits, (sym, [h[:6] for h in hits][:5])
+
+
+ROLLOUT_SYMS = ("rollout_kernelILb0ELb0ELb0ELi0ELb0E", "rollout_kernelILb0ELb1ELb0ELi0ELb0E",
+                "rollout_kernelILb1ELb0ELb1ELi0ELb0E", "rollout_kernelILb1ELb1ELb1ELi0ELb0E",
+                "rollout_kernelILb0ELb0ELb0ELi1ELb0E", "rollout_kernelILb0ELb1ELb0ELi1ELb0E",
+                "rollout_kernelILb1ELb0ELb0ELi1ELb0E",
+                "rollout_kernelILb0ELb0ELb0ELi2ELb0E", "rollout_kernelILb0ELb1ELb0ELi2ELb0E",
+                "rollout_kernelILb0ELb0ELb0ELi0ELb1E", "rollout_kernelILb0ELb1ELb0ELi0ELb1E",
+                "rollout_kernelILb1ELb0ELb0ELi0ELb1E", "rollout_kernelILb1ELb1ELb0ELi0ELb1E")
+
+
+def test_no_packed_f32_accumulator_overwritten_by_a_load(product_isa):
+    """PKWAR (scripts/isa/hazards.py): in every rollout kernel no LDS / global load
+    overwrites a source of a packed-f32 op (v_pk_fma/mul/add_f32) that nothing has read yet, more
+    than 5 instructions after it.  The violating pattern was the SLP-packed dW3 accumulation at the
+    tile loop's latch (gw3b lanes 48-63 different run to run); distill.hip is built without SLP
+    (build.SRC_FLAGS) and the explicit f32x2 pairs (tanh, the operand splits) are consumed within a
+    few instructions (>= 200 repeated rollouts bitwise identical, tests/test_determinism_gpu.py)."""
+    hz = _hz()
+    fns = hz.functions(product_isa["distill.hip"])
+    for sym in ROLLOUT_SYMS:
+        name = next(n for n in fns if sym in n)
+        far = [h[:6] for h in hz.scan_pkwar(fns[name]) if h[1] > 5]
+        assert not far, (sym, far[:5])
 
 
 def test_no_hazard_below_its_requirement_in_any_kernel(product_isa):

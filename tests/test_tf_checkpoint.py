@@ -21,6 +21,35 @@ def test_crc32c_check_value():
         assert tc._unmask(tc._mask(v)) == v
 
 
+def test_native_crc32c_matches_the_table_definition():
+    """rd_crc32c (libreacher.so, slicing-by-8) = the per-byte table form on every length 0..70
+    (all tail cases of the 8-byte loop), on a 1 MB buffer, and when continued in pieces."""
+    rs = np.random.RandomState(0)
+    data = rs.randint(0, 256, 1 << 20).astype(np.uint8).tobytes()
+    for n in range(71):
+        assert tc.crc32c(data[:n]) == tc.crc32c_py(data[:n]), n
+    big = tc.crc32c(data)
+    assert big == tc.crc32c_py(data)
+    assert tc.crc32c(data[600_001:], tc.crc32c(data[:600_001])) == big
+
+
+def test_lstm_checkpoint_round_trip_is_fast(tmp_path):
+    """a T = 10 LSTM checkpoint with its Adam slots (6.1 MB) is written and read back
+    (every CRC checked) in well under a second -- lstm_train saves one every episode."""
+    import time
+    T = 10
+    P = tc.lstm_variables(T)
+    n = sum(int(np.prod(shape)) for _, _, shape in P)
+    rs = np.random.RandomState(1)
+    p, m, v = (rs.standard_normal(n).astype(np.float32) for _ in range(3))
+    t0 = time.perf_counter()
+    tc.save_lstm(str(tmp_path / "lstm.ckpt"), p, m, v, T)
+    q, qm, qv = tc.load_lstm(str(tmp_path / "lstm.ckpt"), T)
+    el = time.perf_counter() - t0
+    assert np.array_equal(q, p) and np.array_equal(qm, m) and np.array_equal(qv, v)
+    assert el < 0.5, el
+
+
 def _tensors(rs):
     return {
         "a/kernel": rs.standard_normal((11, 64)).astype(np.float32),
