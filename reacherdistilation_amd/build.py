@@ -111,11 +111,11 @@ def build_stamps():
 
 
 def build_variant(name, *defines):
-    """Diagnostic build as libreacher_<name>.so; never the product.  Macros: RD_DIAG_KNOBS
-    (the measurement-only environment variables RDM_ROWS, RDL_PR_DBG), RD_MFMA_SRCC_FENCE
-    (every f32 MFMA group of the rollout SrcC-fenced), or a compiler flag such as
-    -fno-slp-vectorize.  The rollout's rejected schedule / ablation variants are kept as
-    profiles/r04_removed_diagnostic_variants.diff."""
+    """Diagnostic build as libreacher_<name>.so; never the product.  Macros: RD_STAMPS,
+    RD_MFMA_SRCC_FENCE (every f32 MFMA group of the rollout SrcC-fenced), or a compiler flag.
+    The rejected schedule / ablation variants are kept as profiles/r04_removed_diagnostic_variants.diff
+    (rollout) and profiles/r05_removed_diagnostic_variants.diff (LSTM, GEMM, PPO, env, reference
+    student)."""
     opts = tuple(d if d.startswith("-") else f"-D{d}" for d in defines)
     return _link(os.path.join(HERE, f"libreacher_{name}.so"), opts)
 

@@ -562,12 +562,7 @@ rdg::GemmArgs gm(int M, int N, int K, const float* A, int64_t lda, int ta, const
 
 // the policy's and the value net's GEMM of one layer as one grouped launch (rdg::gemm2)
 hipError_t mm2(rdp_trainer* t, const rdg::GemmArgs& pol, const rdg::GemmArgs& vf) {
-#ifdef RD_PPO_UNGROUPED   // diagnostic build: one launch per net (A/B of the grouping)
-    if (hipError_t e = rdg::gemm(t->stream, pol, t->split, SPLIT_FLOATS, t->cus)) return e;
-    return rdg::gemm(t->stream, vf, t->split, SPLIT_FLOATS, t->cus);
-#else
     return rdg::gemm2(t->stream, pol, vf, t->split, SPLIT_FLOATS, t->cus);
-#endif
 }
 
 

@@ -78,10 +78,7 @@ constexpr int TK = 16, GEMM_THREADS = 256;
 // MFMA phase.  Measured (LSTM 20 / 1,024 / 16,384 windows, PPO iteration): depth 1 0.467 /
 // 0.679 / 4.31 ms, 63.1 ms; depth 3 0.474 / 0.691 / 4.37, 64.9; depth 5 0.472 / 0.693 / 4.41,
 // 65.6; the previous loop (next tile loaded at the top of the step) 0.485 / 0.709 / 4.42, 70.0.
-#ifndef RDG_PF
-#define RDG_PF 1
-#endif
-constexpr int PF = RDG_PF;
+constexpr int PF = 1;
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, int row, int col, float v) {
     if (g.bias) v += g.bias[col];
@@ -539,9 +536,6 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
     if (g.M <= 0 || g.N <= 0) return hipSuccess;
     // 128 x 128 tiles (half the operand re-reads, 4x the MFMAs per LDS read) when both
     // dimensions fill them; 64 x 64 otherwise
-#ifdef RD_GEMM_BT   // diagnostic builds (build.py --variant): force one tile size / kernel
-    const int BT = RD_GEMM_BT;
-#else
     // the 16x16x4 64 x 64 kernel everywhere: on every LSTM / PPO shape it beats both the
     // 16x16x4 128-tile variant and the 32x32x2 128 x 128 x 32 kernel (BT 129), which are kept
     // for diagnostic builds (scripts/gemm_tile_compare.sh): the LSTM's GEMMs
@@ -550,7 +544,6 @@ inline hipError_t gemm(hipStream_t st, GemmArgs g, float* part, int64_t part_flo
     // Also measured slower: the 64 tile with k-contiguous LDS staging read by
     // ds_read_b128, 16 or 32 deep
     const int BT = 64;
-#endif
     const int TILE = BT == 129 ? 128 : BT;
     const int tm = (g.M + TILE - 1) / TILE, tn = (g.N + TILE - 1) / TILE;
     gemm_plan(g, TILE, BT == 129 ? 2 : 8, part, part_floats, cus);   // the big kernel's 80 KB of LDS: 2 per CU
@@ -616,7 +609,6 @@ inline Group2 group2(const GemmArgs& g0, const GemmArgs& g1) {
 }
 
 inline hipError_t gemm2(hipStream_t st, GemmArgs g0, GemmArgs g1, float* part, int64_t part_floats, int cus) {
-#ifndef RD_GEMM_BT
     const bool pair = g0.M > 0 && g0.N > 0 && g1.M > 0 && g1.N > 0 && g0.ta == g1.ta && g0.tb == g1.tb &&
                       gemm_vec(g0) == gemm_vec(g1);
     if (pair) {
@@ -671,7 +663,6 @@ inline hipError_t gemm2(hipStream_t st, GemmArgs g0, GemmArgs g1, float* part, i
             hipLaunchKernelGGL(splitk_reduce_g2<0>, dim3((unsigned)(nb0 + nb1)), dim3(256), 0, st, g0, g1, nb0);
         return hipGetLastError();
     }
-#endif
     hipError_t e = gemm(st, g0, part, part_floats, cus);
     if (e != hipSuccess) return e;
     return gemm(st, g1, part, part_floats, cus);

@@ -26,11 +26,7 @@ constexpr int kBlock = 256;
 // kernel, so they are stored non-temporal: +1 % at 16.8M envs, +3.5 % at 4.2M, +4.5 % at 1M
 // against plain stores (profiles/r03n_env_nt.txt; same bits).
 template <class T> __device__ __forceinline__ void ost(T* p, T v) { __builtin_nontemporal_store(v, p); }
-#ifdef RD_ENV_NTLD   // diagnostic build: the state and action read as non-temporal streams
-template <class T> __device__ __forceinline__ T ild(const T* p) { return __builtin_nontemporal_load(p); }
-#else
 template <class T> __device__ __forceinline__ T ild(const T* p) { return *p; }
-#endif
 
 struct ResetSrc {
     int mode;              // RD_RESET_PHILOX / RD_RESET_TABLE

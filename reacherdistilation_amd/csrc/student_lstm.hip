@@ -295,7 +295,7 @@ __device__ __forceinline__ void stage_rows(int B, float (*S)[PR_HS], L&& ld4) {
 __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ Z,
                                                                const float* __restrict__ state0, float* __restrict__ G,
                                                                float* __restrict__ Cs, float* __restrict__ H, int B,
-                                                               int T, uint32_t* bar, int dbg) {
+                                                               int T, uint32_t* bar) {
     __shared__ __attribute__((aligned(16))) float Ws[PR_K][PR_WS];
     __shared__ __attribute__((aligned(16))) float Hs[PR_K][PR_HS];
     __shared__ __attribute__((aligned(16))) float Zl[PR_ROWS][PR_ZS];
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
     for (int s = 0; s < T; ++s) {
         // A operand: h_s [B][U] -> Hs[k][row] (step 0: the initial state, read directly)
         const float* hs = s == 0 ? (state0 ? state0 + (int64_t)B * U : nullptr) : H + (int64_t)s * B * U;
-        if (!(dbg & 1)) {
+        {
             if (s > 0) {   // h_s: written in this launch (sc1)
                 const int64_t base = (int64_t)s * B * U;
                 stage_rows<1>(B, Hs, [&](int row, int c) { return pr_load4(rH, base + (int64_t)row * U + c); });
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
         // one accumulation chain per gate block and k order as lstm_rec_fwd_kernel (bitwise);
         // the two blocks' chains interleave
         rdg::f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        if (!(dbg & 2)) {
+        {
             for (int kt = 0; kt < PR_K / 16; ++kt) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
         }
         if (s + 1 < T) {
             load_zx(s + 1);
-            if (!(dbg & 4) && !pr_grid_sync(bar, (uint32_t)(s + 1) * gridDim.x, bar + 2)) return;
+            if (!pr_grid_sync(bar, (uint32_t)(s + 1) * gridDim.x, bar + 2)) return;
         }
     }
 }
@@ -419,8 +419,7 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
                                                                 const float* __restrict__ G, const float* __restrict__ Cs,
                                                                 float* __restrict__ dZ, float* __restrict__ part,
                                                                 float* __restrict__ dbl, const float* __restrict__ prev,
-                                                                float* __restrict__ Q, int B, int T, uint32_t* bar,
-                                                                int dbg) {
+                                                                float* __restrict__ Q, int B, int T, uint32_t* bar) {
     __shared__ __attribute__((aligned(16))) float Wb[64][PB_N];        // [local gate col y*16+c][unit]
     __shared__ __attribute__((aligned(16))) float As[64][PR_HS];       // dz_s of the local columns: [col][row]
     static_assert(PR_HS >= 40, "As also holds the 5 x 8 row-group sums at the end");
@@ -475,7 +474,7 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
     uint32_t nsync = 0;
     for (int s = T - 1; s >= 0; --s) {
         float dhn[4] = {0.f, 0.f, 0.f, 0.f};
-        if (s < T - 1 && act && !(dbg & 1)) {   // (1) dh_next: the 13 partials of step s+1, fixed order
+        if (s < T - 1 && act) {   // (1) dh_next: the 13 partials of step s+1, fixed order
             const int64_t pb = (int64_t)((s + 1) & 1) * PR_GRID * PB_PART + (int64_t)u * PR_ROWS + 4 * r4;
             rdg::f32x4 v[PR_GRID];
 #pragma unroll
@@ -520,7 +519,7 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
         rdg::f32x4 acc[7];
 #pragma unroll
         for (int q = 0; q < 7; ++q) acc[q] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
-        if (!(dbg & 2)) {
+        {
 #pragma unroll
             for (int kq = 0; kq < 16; ++kq) {
                 const int kk = 4 * kq + gq;
@@ -539,7 +538,7 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
                                                        0, 16);
         }
         __syncthreads();   // As is rewritten by the next step's cell
-        if (!(dbg & 4) && !pr_grid_sync(bar + 1, ++nsync * gridDim.x, bar + 2)) return;
+        if (!pr_grid_sync(bar + 1, ++nsync * gridDim.x, bar + 2)) return;
     }
     // dbl (the gate bias gradient) and Q = prev^T dz of the local columns: the 8 row groups'
     // sums, in order (As[col][8 j + r4] holds sum j of row group r4)
@@ -1159,12 +1158,7 @@ rdg::GemmArgs ga(int M, int N, int K, const float* A, int64_t lda, int ta, const
 // two independent GEMMs as one grouped launch (rdg::gemm2): a head layer's weight gradient
 // beside its data gradient, the two halves of the LSTM weight gradient
 hipError_t mm2(rdl_trainer* t, const rdg::GemmArgs& g0, const rdg::GemmArgs& g1) {
-#ifdef RD_LSTM_UNGROUPED   // diagnostic build: one launch per GEMM
-    if (hipError_t e = rdg::gemm(t->stream, g0, t->split, SPLIT_FLOATS, t->cus)) return e;
-    return rdg::gemm(t->stream, g1, t->split, SPLIT_FLOATS, t->cus);
-#else
     return rdg::gemm2(t->stream, g0, g1, t->split, SPLIT_FLOATS, t->cus);
-#endif
 }
 
 hipError_t colsum(rdl_trainer* t, const float* src, int64_t M, int N, int64_t ld, float* out) {
@@ -1187,14 +1181,6 @@ hipError_t colsum(rdl_trainer* t, const float* src, int64_t M, int N, int64_t ld
 // the persistent recurrence kernels for batches of at most PR_ROWS windows, and the
 // one-launch head for at most HF_MAX_ROWS rows; rdl_config.kernels can select the per-step /
 // per-layer launches instead (RDL_KERNELS_*: tests compare the two paths)
-int pr_dbg() {   // diagnostic builds: RDL_PR_DBG bit 0 skips the exchange loads, 1 the MFMAs, 2 the barrier
-#ifdef RD_DIAG_KNOBS
-    const char* e = getenv("RDL_PR_DBG");
-    return e ? atoi(e) : 0;
-#else
-    return 0;
-#endif
-}
 
 // head_bwd_kernel's 16-row tiles per workgroup: one while the T x ceil(B / 16) tiles fill at
 // most ~4 workgroups per CU, then up to 8, so the partial rows (HB_PART floats each) and their
@@ -1234,7 +1220,7 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     if (persistent(t, B)) {   // Zx, then all T recurrent steps in one launch (it writes the step-0 state rows)
         RDL_CK(mm(t, (int)R, G4, XI, t->X, XLD, 0, P + OFF_WL, G4, 0, t->Z, G4, P + OFF_BL), "rdl gemm Zx");
         hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
-                           (const float*)t->Z, state0, t->G, t->Cs, t->H, (int)B, T, t->bar, pr_dbg());
+                           (const float*)t->Z, state0, t->G, t->Cs, t->H, (int)B, T, t->bar);
         RDL_CK(hipGetLastError(), "rdl lstm_fwd_persist_kernel");
     } else {
     if (state0) {
@@ -1249,21 +1235,11 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     RDL_CK(mm(t, (int)R, G4, XI, t->X, XLD, 0, P + OFF_WL, G4, 0, t->Z, G4, P + OFF_BL), "rdl gemm Zx");
     for (int s = 0; s < T; ++s) {
         float* Zs = t->Z + (int64_t)s * B * G4;
-#ifdef RD_LSTM_UNFUSED   // diagnostic build: the recurrent GEMM and the cell as two launches
-        RDL_CK(mm(t, (int)B, G4, U, t->H + (int64_t)s * B * U, U, 0, P + OFF_WL + XI * G4, G4, 0, Zs, G4, nullptr,
-                  rdg::EPI_NONE, nullptr, 0, 1),
-               "rdl gemm recurrent");
-        hipLaunchKernelGGL(cell_fwd_kernel, dim3((unsigned)((B * U + 255) / 256)), dim3(256), 0, t->stream,
-                           (const float*)Zs, (const float*)(t->Cs + (int64_t)s * B * U), t->G + (int64_t)s * B * G4,
-                           t->Cs + (int64_t)(s + 1) * B * U, t->H + (int64_t)(s + 1) * B * U, B);
-        RDL_CK(hipGetLastError(), "rdl cell_fwd_kernel");
-#else
         hipLaunchKernelGGL(lstm_rec_fwd_kernel, dim3((U + RF_UNITS - 1) / RF_UNITS, (unsigned)((B + RF_ROWS - 1) / RF_ROWS)),
                            dim3(256), 0, t->stream, (const float*)(t->H + (int64_t)s * B * U), P + OFF_WL + XI * G4,
                            (const float*)Zs, (const float*)(t->Cs + (int64_t)s * B * U), t->G + (int64_t)s * B * G4,
                            t->Cs + (int64_t)(s + 1) * B * U, t->H + (int64_t)(s + 1) * B * U, B);
         RDL_CK(hipGetLastError(), "rdl lstm_rec_fwd_kernel");
-#endif
     }
     }
     // step t's head over its B rows (student_nn.py:42-46, one head per unrolled step)
@@ -1356,23 +1332,11 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     if (persistent(t, B)) {
         hipLaunchKernelGGL(lstm_bptt_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
                            (const float*)t->dHh, (const float*)t->G, (const float*)t->Cs, dZl, t->bpart, g + OFF_BL,
-                           prev, t->qbuf, (int)B, T, t->bar, pr_dbg());
+                           prev, t->qbuf, (int)B, T, t->bar);
         RDL_CK(hipGetLastError(), "rdl lstm_bptt_persist_kernel");
     } else {
     RDL_CK(hipMemsetAsync(t->dc, 0, sizeof(float) * B * U, t->stream), "rdl bptt");
     const unsigned cb = (unsigned)((B * U + 255) / 256);
-#ifdef RD_LSTM_UNFUSED   // diagnostic build: dh GEMM and cell backward as two launches per step
-    for (int s = T - 1; s >= 0; --s) {
-        hipLaunchKernelGGL(cell_bwd_kernel, dim3(cb), dim3(256), 0, t->stream, (const float*)(t->dHh + (int64_t)s * B * U),
-                           (const float*)t->dhn, s < T - 1 ? 1 : 0, (const float*)(t->G + (int64_t)s * B * G4),
-                           (const float*)(t->Cs + (int64_t)(s + 1) * B * U), (const float*)(t->Cs + (int64_t)s * B * U),
-                           t->dc, dZl + (int64_t)s * B * G4, B);
-        RDL_CK(hipGetLastError(), "rdl cell_bwd_kernel");
-        if (s > 0)   // dh_{s-1} = dz_s . Wr^T
-            RDL_CK(mm(t, (int)B, U, G4, dZl + (int64_t)s * B * G4, G4, 0, P + OFF_WL + XI * G4, G4, 1, t->dhn, U),
-                   "rdl gemm dh");
-    }
-#else
     // the last step's cell alone; then per step s the GEMM dh_{s-1} = dz_s . Wr^T whose
     // epilogue (or split-K reduce) runs the cell backward of step s-1 -> dz_{s-1}, dc
     hipLaunchKernelGGL(cell_bwd_kernel, dim3(cb), dim3(256), 0, t->stream,
@@ -1395,7 +1359,6 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
         g.lz = dZl + (int64_t)(s - 1) * B * G4;
         RDL_CK(rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus), "rdl gemm dh + cell");
     }
-#endif
     }
     // LSTM weights: dWl = [x | h_prev]^T dz over all rows; dbl; then dp -> dWp, dbp
     RDL_CK(mm2(t, ga(XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4),

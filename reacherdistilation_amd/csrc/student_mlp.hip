@@ -265,12 +265,8 @@ __device__ __forceinline__ void wgrad_layer(const float* H, const float* D, f32x
     }
 }
 
-// partial-row stores: -DRD_MLP_NT (diagnostic build) makes them non-temporal
-#ifdef RD_MLP_NT
-__device__ __forceinline__ void wst(float* p, float v) { __builtin_nontemporal_store(v, p); }
-#else
+// partial-row stores (non-temporal measured no gain: profiles/r05_removed_diagnostic_variants.diff)
 __device__ __forceinline__ void wst(float* p, float v) { *p = v; }
-#endif
 
 template <int L>
 __device__ __forceinline__ void store_wgrad(float* ws, const f32x4 (&G)[WG<L>::Q], int wave, int i, int g) {
@@ -602,11 +598,7 @@ namespace {
 // step 21.8 us vs 35.8 us with 64-row blocks, 1,024 rows 27.2 vs 37.4 us).  Every workgroup
 // writes a 104 KB partial row, so once the 16-row blocks would occupy more than half of the
 // workgroups the 64-row kernel wins (4,096 rows: 51.2 vs 42.4 us).
-// Diagnostic builds (RD_DIAG_KNOBS): RDM_ROWS=16|64 overrides (measurement only).
 bool use_small_rows(int64_t n, int grid) {
-#ifdef RD_DIAG_KNOBS
-    if (const char* e = getenv("RDM_ROWS")) return atoi(e) == 16;
-#endif
     return (n + 15) / 16 <= grid / 2;
 }
 

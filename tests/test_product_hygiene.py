@@ -2,10 +2,10 @@
 item 2): no run-time knobs, no diagnostic kernels, the ctypes mirrors match the C headers
 byte for byte, and the bench's headline mode is the library's default mode.
 
-- libreacher.so imports no getenv: every measurement-only switch (RDM_ROWS, RDL_PR_DBG) exists
-  only in build_variant builds (-DRD_DIAG_KNOBS); the tests' path selections are config fields
+- libreacher.so imports no getenv: the tests' path selections are config fields
   (rdd_config.group_envs, rdl_config.kernels).  distill.hip keeps two diagnostic macros
-  (RD_STAMPS, RD_MFMA_SRCC_FENCE); its rejected variants live in profiles/*.diff.
+  (RD_STAMPS, RD_MFMA_SRCC_FENCE), the other sources none; the rejected variants live in
+  profiles/*.diff.
 - The consumer-side env step is instantiated only for the bf16 student (rollout_kernel<true, *,
   true>), whose f32 MFMAs (the exact teacher's) are SrcC-fenced.
 - Statically, in the product's ISA no LDS / global load is issued into a register that an
@@ -173,11 +173,16 @@ def test_hazard_scanner_detects_each_class(kind, snippet):
 
 
 def test_distill_keeps_only_two_diagnostic_macros():
-    """VERDICT r3 item 8: the rejected schedule / ablation variants live in
-    profiles/r04_removed_diagnostic_variants.diff, not in the product source."""
-    txt = open(os.path.join(ROOT, "reacherdistilation_amd", "csrc", "distill.hip")).read()
-    macros = set(re.findall(r"^#\s*if(?:n?def)?\s+(?:defined\()?(\w+)", txt, re.M))
-    assert macros <= {"RD_STAMPS", "RD_MFMA_SRCC_FENCE"}, macros
+    """VERDICT r3 item 8 / r4 item 7: the rejected schedule / ablation variants live in
+    profiles/r04_removed_diagnostic_variants.diff and profiles/r05_removed_diagnostic_variants.diff,
+    not in the product sources: distill.hip keeps RD_STAMPS and RD_MFMA_SRCC_FENCE, the other
+    sources no conditional compilation at all."""
+    from reacherdistilation_amd import build
+    for src in build.sources() + [os.path.join(build.CSRC, f) for f in os.listdir(build.CSRC) if f.endswith(".h")]:
+        txt = open(src).read()
+        macros = set(re.findall(r"^#\s*if(?:n?def)?\s+(?:defined\()?(\w+)", txt, re.M))
+        allowed = {"RD_STAMPS", "RD_MFMA_SRCC_FENCE"} if src.endswith("distill.hip") else set()
+        assert macros <= allowed, (os.path.basename(src), macros)
 
 
 def _c_layout(struct, header, fields):
