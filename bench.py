@@ -105,6 +105,10 @@ def parse():
                     help="the same leg's steps for the reference graph student (student_nn.py:51-57)")
     ap.add_argument("--no-strong-projection", action="store_true",
                     help="at N = 1 skip timing c4's 2/4/8-GPU strong shards (strong_projection)")
+    ap.add_argument("--teacher", default="synthetic", choices=["synthetic", "fitted"],
+                    help="fixed teacher of the run and its convergence legs: the seeded synthetic MlpPolicy, or the "
+                         "reference teacher's structure fitted to the fixture's 1,050 teacher records "
+                         "(teacher.fit_teacher); the line carries a fitted-teacher convergence block either way")
     return ap.parse_args()
 
 
@@ -573,6 +577,36 @@ def convergence_fixture(dev, lr, steps, ref_steps):
     return out
 
 
+def fitted_teacher(dev):
+    """teacher.fit_teacher on the fixture's 21 teacher-stepped episodes (1,050 records): the
+    reference teacher's structure (teacher.py:14-16) fitted to the reference's own teacher data,
+    with its fit quality on those records and on the LSTM student's episodes 21-24."""
+    import numpy as np
+    import torch
+
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    from reacherdistilation_amd.teacher import fit_teacher
+    path = os.path.join(ROOT, "tests", "golden", "reacher_fixture.npz")
+    if not os.path.exists(path):
+        return None, None
+    d = np.load(path)
+    ob, t = d["ob"], d["t"]
+    t0 = time.perf_counter()
+    p, hist = fit_teacher(ob[:21], t[:21], seed=0, device=dev)
+    el = time.perf_counter() - t0
+    tr = DistillTrainer(DistillConfig(n_envs=64, seed=0), device=dev, teacher=p)
+
+    def mse(lo, hi):
+        tq, _ = tr.forward(torch.from_numpy(ob[lo:hi].reshape(-1, 11).astype(np.float32)).to(dev), student=False)
+        return float(np.mean((tq[:, :2].double().cpu().numpy() - t[lo:hi].reshape(-1, 4)[:, :2]) ** 2))
+    info = {"fit": "teacher.fit_teacher: obfilter of the records + 2x64 tanh MlpPolicy + the records' logstd, "
+                   "rows mode (recorded pdflat as MSE target), 30,000 Adam steps at lr 1e-3 then 20,000 at 1e-4",
+            "records": int(21 * 50), "seconds": el, "train_mse": mse(0, 21), "eps21_24_mse": mse(21, 25),
+            "reference_lstm_student_mse_eps21_24": REF_LSTM_STUDENT_MSE}
+    tr.close()
+    return p, info
+
+
 def cpu_baseline(workload, seconds, threads, n):
     """Time the oracle's C f32 rollout+distill step (OpenMP) at the workload's own env count
     (the same per-GPU batch as the timed GPU step), for a bounded number of steps."""
@@ -606,7 +640,8 @@ def cpu_baseline(workload, seconds, threads, n):
                        f"OpenMP {threads} threads")
 
 
-def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=100, comm=None, split=False):
+def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=100, comm=None, split=False,
+                teacher=None):
     """North-star check: optimiser steps (one per env step, the reference's lr 1e-4 TF1 Adam)
     until the student's action-MSE vs the teacher, averaged over the last 10 steps and all
     ranks, falls below 1e-3 -- against the reference's budget of 5000 episodes x 50 steps =
@@ -617,7 +652,7 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
     tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
                                       student_dtype=sdt, f32_split=split), device=dev, rank=rank, world_size=world,
-                        comm=comm)
+                        comm=comm, teacher=teacher)
     t0 = time.perf_counter()
     steps, mse, hit = 0, float("nan"), None
     while steps < max_steps:
@@ -647,7 +682,7 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
             "student_mse_final": mse, "opt_steps_run": steps, "seconds": el}
 
 
-def convergence_driver(dev, lr, max_episodes=5000, target=1e-3):
+def convergence_driver(dev, lr, max_episodes=5000, target=1e-3, teacher=None):
     """The env-step reading of the budget on the reference's OWN loop shape: mlp_train.train
     (one env, per env step one Adam step on a 200-row window from the dataset's training pool,
     the 2x64 student, MSE) until an episode's mean window action-MSE is < 1e-3; env steps
@@ -655,7 +690,7 @@ def convergence_driver(dev, lr, max_episodes=5000, target=1e-3):
     from reacherdistilation_amd import mlp_train
     t0 = time.perf_counter()
     tr, ds, losses = mlp_train.train(episodes=max_episodes, loss="mse", lr=lr, log=lambda *a: None, device=dev,
-                                     stop_loss=target)
+                                     stop_loss=target, teacher=teacher)
     el = time.perf_counter() - t0
     hit = bool(losses) and losses[-1] / 50 < target
     env_steps = ds.num_episodes() * 50
@@ -738,15 +773,21 @@ def main():
     # clocks, so the short timed region below (the driver runs 20 steps of ~0.12 ms) measures
     # the kernels rather than the clock ramp.
     conv = conv_small = None
+    fitted, fit_info = fitted_teacher(dev) if ((args.conv_steps > 0 and world == 1) or args.teacher == "fitted") \
+        else (None, None)
+    if args.teacher == "fitted" and fitted is None:
+        raise SystemExit("--teacher fitted needs tests/golden/reacher_fixture.npz")
+    teacher = fitted if args.teacher == "fitted" else None
     if args.conv_steps > 0:
-        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm, split=split)
+        conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm, split=split,
+                           teacher=teacher)
         # the same check at a small per-GPU batch: the env-step reading of the reference's budget
         conv_small = convergence(wl, args.conv_small_envs, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm,
-                                 split=split)
+                                 split=split, teacher=teacher)
 
     cfg = DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=args.lr, student_dtype=sdt,
                         f32_split=split)
-    tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world, comm=comm)
+    tr = DistillTrainer(cfg, device=dev, rank=rank, world_size=world, comm=comm, teacher=teacher)
 
     def one_step(ev=None):
         if ev is None and (world == 1 or comm is not None):
@@ -931,8 +972,23 @@ def main():
         if conv is not None:
             out["convergence"] = conv
             out["convergence_small_batch"] = conv_small
+            out["convergence_teacher"] = args.teacher
             if world == 1:
-                out["convergence_reference_driver"] = convergence_driver(dev, args.lr)
+                out["convergence_reference_driver"] = convergence_driver(dev, args.lr, teacher=teacher)
+        if fit_info is not None and world == 1 and args.conv_steps > 0:
+            # the north star's student action-MSE against a teacher shaped like the
+            # reference's (fitted to its 1,050 teacher records), beside the synthetic teacher's legs
+            ft = {"teacher": fit_info}
+            if args.teacher == "fitted":
+                ft["convergence"], ft["convergence_small_batch"] = conv, conv_small
+                ft["convergence_reference_driver"] = out["convergence_reference_driver"]
+            else:
+                ft["convergence"] = convergence(wl, n, sdt, dev, 0, 1, args.lr, args.conv_steps, split=split,
+                                                teacher=fitted)
+                ft["convergence_small_batch"] = convergence(wl, args.conv_small_envs, sdt, dev, 0, 1, args.lr,
+                                                            args.conv_steps, split=split, teacher=fitted)
+                ft["convergence_reference_driver"] = convergence_driver(dev, args.lr, teacher=fitted)
+            out["convergence_fitted_teacher"] = ft
         out["roofline_env"] = env_roofline(dev)
         ceil = copy_ceiling()
         if ceil is not None:   # the float4 copy measured in this run

@@ -40,7 +40,7 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
           loss: str = "kl", lr: float = 1e-4, seed: int = 0, device="cuda:0", teacher_path: str | None = None,
           warmup_episodes: int = 2 * MLP_BATCH_SIZE, student: str = "policy", keep_prob: float = 1.0,
           log=print, gym_env: bool = False, store_dir: str | None = None, pool: str = "reference",
-          stop_loss: float | None = None):
+          stop_loss: float | None = None, teacher=None):
     """Returns (trainer, dataset, per-episode summed training loss); the trainer is the
     DistillTrainer (student="policy") or the StudentMlpTrainer (student="mlp").  The env I/O
     stays on the device (driver_env.DriverEnv; gym_env=True: through the gym-API env, numpy
@@ -49,12 +49,14 @@ def train(train: bool = True, restore: bool = False, *, episodes: int = MLP_EPIS
     directory (mlp_train.py:105-110); episodes are dumped to it every 5 episodes (:203) and its
     stored pages join the training pool (dataset.py:164-177); ``pool="ring"`` draws windows
     uniformly from the device ring instead.  ``stop_loss``: also stop after the first DAgger
-    episode whose mean window loss falls below it (convergence measurements)."""
+    episode whose mean window loss falls below it (convergence measurements).  ``teacher``: an
+    MlpPolicyParams used instead of the restored / synthetic one (e.g. teacher.fit_teacher)."""
     if student not in ("policy", "mlp"):
         raise ValueError(f"unknown student {student!r}")
     env = DriverEnv(seed, device, gym_api=gym_env)
-    teacher = TeacherAgent(restore=teacher_path is not None, path=teacher_path)   # always restored (ref. :29)
-    tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr), device=device, teacher=teacher.pi)
+    pi = teacher if teacher is not None else \
+        TeacherAgent(restore=teacher_path is not None, path=teacher_path).pi   # always restored (ref. :29)
+    tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss=loss, lr=lr), device=device, teacher=pi)
     sm = StudentMlpTrainer(StudentMlpConfig(loss=loss, lr=lr, keep_prob=keep_prob, seed=seed),
                            device=device) if student == "mlp" else None
     dataset = DeviceDataset(device=device, seed=seed, store=PageStore(store_dir) if store_dir else None, pool=pool)
@@ -160,7 +162,7 @@ def fit_records(ob, t_pdflat, rew=None, *, student: str = "policy", steps: int =
                           "rdd_step_rows")
         tr.set_stream(prev)
         done = 0
-        while done < steps:
+        while done + graph_steps <= steps:
             idx_buf.copy_(_windows(gen, E, None, graph_steps, device=dev))
             g.replay()
             done += graph_steps
@@ -168,6 +170,10 @@ def fit_records(ob, t_pdflat, rew=None, *, student: str = "policy", steps: int =
             if log_every and done % log_every < graph_steps:
                 m = tr.metrics(graph_steps)
                 history.append((done, float((m[:, 2] / (2 * m[:, 3])).mean())))
+        if done < steps:   # the last steps % graph_steps steps eagerly: exactly `steps` Adam steps
+            for i in _windows(gen, E, None, steps - done, device=dev):
+                tr.step_rows(ob_all[i], t_all[i])
+            done = steps
         torch.cuda.synchronize(dev)
         return tr, history
     if student != "mlp":

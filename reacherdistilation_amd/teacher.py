@@ -3,6 +3,8 @@
   TeacherAgent (teacher.py:12-20)  -> policy.TeacherAgent (TF checkpoint or safetensors restore)
   train (:23-37, ppo1 learn)       -> ppo.train
   collect_reward (:39-62)          -> collect_reward below, batched over ``n_envs`` envs
+  (the restored teacher.ckpt)      -> fit_teacher below: the teacher's structure fitted to the
+                                      teacher records the reference ships (its checkpoint does not)
 
 ``collect_reward`` as committed cannot run (``TeaherAgent``, ``ob_ph``, ``t_pdflat``,
 ``reward`` and ``Dataset`` are undefined there).  Its evident intent -- the teacher's mean
@@ -19,9 +21,10 @@ store attached, full pages of MAX_CAPACITY episodes are written as the drivers d
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
-from .config import ACSPACE_SHAPE, EPISODE_STEPS, MAX_CAPACITY
+from .config import ACSPACE_SHAPE, EPISODE_STEPS, MAX_CAPACITY, OBSPACE_SHAPE
 from .dataset import F_OB, F_REW, F_S, F_T, REC, DeviceDataset
 from .distill import DistillConfig, DistillTrainer
 from .env import BatchedReacher
@@ -29,7 +32,46 @@ from .pages import PageStore
 from .policy import MlpPolicyParams, TeacherAgent
 from .ppo import train  # noqa: F401  (teacher.train: PPO on the batched env)
 
-__all__ = ["TeacherAgent", "train", "collect_reward"]
+__all__ = ["TeacherAgent", "train", "collect_reward", "fit_teacher"]
+
+
+def fit_teacher(ob, t_pdflat, *, phases=((30_000, 1e-3), (20_000, 1e-4)), seed: int = 0, device="cuda:0",
+                log_every: int = 0):
+    """A teacher of the reference's structure (teacher.py:14-16: baselines MlpPolicy, observation
+    filter -> 2 x 64 tanh -> linear mean, state-independent logstd) fitted to recorded teacher
+    data: episodes ob [E, 50, 11] with the teacher's pdflat t_pdflat [E, 50, 4] -- the
+    reference's own fixture (tests/golden/reacher_fixture.npz, its 21 teacher-stepped episodes =
+    1,050 records).  The reference restores a trained teacher.ckpt that it does not ship
+    (teacher.py:17-20); this stands in for it where a teacher "shaped like the reference's"
+    matters (the student-MSE north star).
+      filter  baselines RunningMeanStd over the records' observations, as the reference graph's
+              pi/obfilter ops compute it (tf_checkpoint.obfilter: std floored at 0.1);
+      logstd  the records' (constant) teacher logstd;
+      weights the rows-mode trainer (rdd_step_rows: the recorded pdflat as the MSE target,
+              200-row windows drawn as dataset.py:179-194, TF1 Adam) for each (steps, lr) phase,
+              from normc(1.0) / normc(0.01) init (seed).
+    Returns (MlpPolicyParams, history [(phase, step, mean training MSE)])."""
+    from .distill import DistillConfig, DistillTrainer
+    from .mlp_train import fit_records
+    from .tf_checkpoint import obfilter
+    ob = np.asarray(ob, np.float32).reshape(-1, EPISODE_STEPS, OBSPACE_SHAPE)
+    tp = np.asarray(t_pdflat, np.float32).reshape(-1, EPISODE_STEPS, 4)
+    flat = ob.reshape(-1, OBSPACE_SHAPE).astype(np.float64)
+    mean, std = obfilter(flat.sum(0), np.square(flat).sum(0), flat.shape[0])
+    logstd = tuple(float(x) for x in tp.reshape(-1, 4)[:, 2:].mean(0))
+    p = MlpPolicyParams.init(seed, logstd=logstd, out_std=0.01)
+    p.ob_mean, p.ob_std = mean, std
+    hist = []
+    for k, (steps, lr) in enumerate(phases):
+        tr = DistillTrainer(DistillConfig(n_envs=64, seed=seed, loss="mse", lr=lr, metrics_len=100), device=device,
+                            student=p)
+        tr, h = fit_records(ob, tp, steps=int(steps), loss="mse", lr=lr, seed=seed + k, device=device,
+                            log_every=log_every, trainer=tr)
+        hist += [(k, s, m) for s, m in h]
+        p = MlpPolicyParams(tr.student_params().cpu().numpy(), mean, std)
+        tr.close()
+    p.flat[p.flat.size - 2:] = np.asarray(logstd, np.float32)   # (MSE leaves logstd untouched)
+    return p, hist
 
 
 def collect_reward(episodes: int, n_envs: int = 1, *, seed: int = 0, teacher: MlpPolicyParams | None = None,

@@ -192,3 +192,50 @@ def test_fixture_heldout_mse_falls(golden):
     h20, h21 = action_mse(tr, ob[20:21], t[20:21]), action_mse(tr, ob[21:25], t[21:25])
     print(f"fixture held-out: ep20 {h0:.4g} -> {h20:.4g}; eps 21-24 {h21:.4g}; train {hist}")
     assert h20 < 0.2 * h0 and h21 < 0.0212
+
+
+def test_fit_records_takes_exactly_the_requested_steps(golden):
+    """a step count that is no multiple of the graph length (100) runs the remainder
+    eagerly -- exactly `steps` Adam steps, bitwise the eager trajectory on the same batches."""
+    from reacherdistilation_amd.mlp_train import fit_records
+    ob, t, rew = _fixture(golden)
+    E = 20
+    a, _ = fit_records(ob[:E], t[:E], student="policy", steps=230, lr=1e-3, seed=6, device=DEV)
+    b = _trainer(loss="mse", lr=1e-3)
+    ob_all = torch.from_numpy(ob[:E].reshape(-1, 11).astype(np.float32)).to(DEV)
+    t_all = torch.from_numpy(t[:E].reshape(-1, 4).astype(np.float32)).to(DEV)
+    for idx in _batches(6, 230, E):
+        i = torch.from_numpy(idx).to(DEV)
+        b.step_rows(ob_all[i], t_all[i])
+    assert a.counters()[1] == b.counters()[1] == 230
+    assert torch.equal(a.student_params(), b.student_params())
+
+
+def test_fitted_teacher_reproduces_the_fixture_teacher(golden):
+    """teacher.fit_teacher -- the reference teacher's structure (obfilter + 2x64
+    tanh + the records' logstd, teacher.py:14-16) fitted to the fixture's 1,050 teacher records --
+    reproduces the recorded teacher means on those records to <= 1e-4 action-MSE (rdd_forward,
+    the teacher path), carries the records' logstd exactly and the reference graph's obfilter
+    arithmetic, and on the reference LSTM student's episodes 21-24 (teacher-labelled, off the
+    teacher's own state distribution) stays far below that student's 0.0212."""
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    from reacherdistilation_amd.teacher import fit_teacher
+    from reacherdistilation_amd.tf_checkpoint import obfilter
+    ob, t, rew = _fixture(golden)
+    p, hist = fit_teacher(ob[:21], t[:21], seed=0, device=DEV, log_every=10_000)
+    tr = DistillTrainer(DistillConfig(n_envs=64, seed=0), device=DEV, teacher=p)
+
+    def mse(lo, hi):
+        o = torch.from_numpy(ob[lo:hi].reshape(-1, 11).astype(np.float32)).to(DEV)
+        tq, _ = tr.forward(o, student=False)
+        tq = tq.cpu().numpy().astype(np.float64)
+        ref = t[lo:hi].reshape(-1, 4).astype(np.float64)
+        assert np.array_equal(tq[:, 2:].astype(np.float32), ref[:, 2:].astype(np.float32))   # the logstd
+        return float(np.mean((tq[:, :2] - ref[:, :2]) ** 2))
+    train, held = mse(0, 21), mse(21, 25)
+    f = ob[:21].reshape(-1, 11).astype(np.float64)
+    m, s = obfilter(f.sum(0), np.square(f).sum(0), f.shape[0])
+    assert np.array_equal(p.ob_mean, m) and np.array_equal(p.ob_std, s)
+    print(f"fitted teacher: train MSE {train:.3g} (1,050 records), eps 21-24 {held:.3g}; {hist}")
+    assert train <= 1e-4, train
+    assert held < 0.0212
