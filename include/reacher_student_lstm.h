@@ -61,8 +61,8 @@ typedef struct {
 
 /* rdl_config.kernels: by default at most 32 windows run the whole recurrence / BPTT as one
  * persistent launch each and at most 16,384 rows run the heads as one launch each way (when
- * their partial rows fit 256 MB at max_windows); these bits keep
- * the per-step recurrence launches / the per-layer head GEMMs at any size. */
+ * their backward's partial rows fit 512 MB at max_windows: rdl_head_path reports it); these
+ * bits keep the per-step recurrence launches / the per-layer head GEMMs at any size. */
 #define RDL_KERNELS_STEP_RECURRENCE 1
 #define RDL_KERNELS_LAYER_HEAD 2
 
@@ -107,6 +107,10 @@ int rdl_bind_grad_buffer(rdl_trainer* t, float* grad);
 /* optimiser steps taken; RD_EINVAL if a persistent recurrence launch (<= 32 windows) gave up
  * at its grid barrier since the trainer was created (its steps are invalid) */
 int rdl_get_counter(rdl_trainer* t, int64_t* opt_steps);
+/* 1: batches of at most 16,384 rows run the fused head kernels (their backward's partial rows,
+ * T x workgroups x 31,652 floats at max_windows, were allocated: at most 512 MB); 0: the
+ * per-layer head GEMMs at every size (RDL_KERNELS_LAYER_HEAD, or the rows would not fit). */
+int rdl_head_path(const rdl_trainer* t);
 /* [count][4] = loss, sum |mu_s - mu_t|^2, rows (T x B), 0 */
 int rdl_read_metrics(rdl_trainer* t, int64_t count, double* out);
 

@@ -596,7 +596,7 @@ __global__ __launch_bounds__(256) void dense32_grad_kernel(const float* __restri
 // operands, and every layer's output is also stored (A1..A4 for the backward, Y).  Same MFMA
 // k order and epilogue (acc + b, tanhf) as the unsplit rd_gemm launches it replaces.
 constexpr int HF_ROWS = 16, HF_MAX_ROWS = 1 << 18;
-constexpr int64_t HPART_MAX_FLOATS = (int64_t)512 << 20;   // the fused head's partial rows: at most 2 GB
+constexpr int64_t HPART_MAX_FLOATS = (int64_t)128 << 20;   // the fused head's partial rows: at most 512 MB (reacher_student_lstm.h)
 template <int K, int N, bool TANH, int LI, int LO>
 __device__ __forceinline__ void head_layer(const float (*in)[LI], float (*out)[LO], const float* __restrict__ W,
                                            const float* __restrict__ b, float* __restrict__ gout, int ldg,
@@ -1600,6 +1600,11 @@ int rdl_bind_grad_buffer(rdl_trainer* t, float* grad) {
     if (!t) return rd::set_error(RD_EINVAL, "rdl_bind_grad_buffer: null handle");
     t->grad = grad ? grad : t->own_grad;
     return RD_OK;
+}
+
+int rdl_head_path(const rdl_trainer* t) {
+    if (!t) return rd::set_error(RD_EINVAL, "rdl_head_path: null handle");
+    return (t->cfg.kernels & RDL_KERNELS_LAYER_HEAD) || !t->hpart ? 0 : 1;
 }
 
 int rdl_get_counter(rdl_trainer* t, int64_t* opt_steps) {

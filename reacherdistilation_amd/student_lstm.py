@@ -74,6 +74,7 @@ nat.register({
     "rdl_final_state": (INT, [P, I64, P]),
     "rdl_get_slots": (INT, [P, P, P]),
     "rdl_set_slots": (INT, [P, P, P]),
+    "rdl_head_path": (INT, [P]),
 })
 
 
@@ -156,6 +157,14 @@ class StudentLstmTrainer:
         self._sync_stream()
         nat.check(self._lib.rdl_set_params(self._h, nat.ptr(p)), "rdl_set_params")
         torch.cuda.current_stream(self.device).synchronize()
+
+    @property
+    def fused_head(self) -> bool:
+        """True if batches of at most 16,384 rows run the fused head kernels (rdl_head_path)."""
+        r = self._lib.rdl_head_path(self._h)
+        if r < 0:
+            nat.check(r, "rdl_head_path")
+        return r == 1
 
     def params(self) -> torch.Tensor:
         out = torch.empty(self.n_params, dtype=torch.float32, device=self.device)

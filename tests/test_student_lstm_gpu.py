@@ -310,7 +310,7 @@ def test_persistent_recurrence_matches_per_step_launches(T, B, with_state):
     _grad_check(g1, ln.backward(p, fw, d))
 
 
-@pytest.mark.parametrize("T,B", [(10, 20), (3, 130), (1, 5), (10, 4100), (4, 16384)])
+@pytest.mark.parametrize("T,B", [(10, 20), (3, 130), (1, 5), (10, 4100), (4, 16384), (10, 16384)])
 def test_fused_head_matches_the_layer_gemms(T, B):
     """At most 16,384 rows: the heads' forward is one launch (head_fwd_kernel) and its backward
     two (head_bwd_kernel + a fixed-order reduce).  Same MFMA k order and epilogues as the
@@ -318,12 +318,13 @@ def test_fused_head_matches_the_layer_gemms(T, B):
     everything BPTT derives from it (the LSTM's gradients) are bitwise those of
     layer_head=True; the head's weight gradients sum the rows in per-workgroup partials (16
     rows, or 2-8 tiles of 16 rows in registers for large batches: (10, 4100) has a ragged last
-    workgroup and tile, (4, 16384) four tiles per workgroup), so they agree to 1e-5 of their
-    largest entry."""
+    workgroup and tile, (4, 16384) four tiles per workgroup, (10, 16384) eight -- the cap, the
+    benchmarked size), so they agree to 1e-5 of their largest entry."""
     ob, prev, t = _batch(T, B, 21 + B)
     out = {}
     for mode in ("1", "0"):
         tr = _trainer(T, B, "mse", layer_head=mode == "0")
+        assert tr.fused_head == (mode == "1")   # rdl_head_path: the path this trainer takes
         y, _ = tr.forward(_t(ob), _t(prev))
         g = tr.rollout(_t(ob), _t(prev), _t(t)).cpu().numpy()
         out[mode] = (y.cpu().numpy(), g)
