@@ -1014,30 +1014,28 @@ __global__ __launch_bounds__(256) void pack_net_kernel(const float* net, float* 
     for (int p = x; p < P_TOT; p += gridDim.x * 256) pack_param(img, p, net[p], student != 0, kind);
 }
 
-// Both rollout images (contiguous in LDS: teacher then student) with every 16-B load of a
-// thread issued before its first LDS store, so a workgroup keeps ~3.7k loads in flight
-// instead of one round trip per loop iteration.
-// `between` runs while the loads are in flight (the producers' first observations).
-// An LDS-DMA fill (global_load_lds_dwordx4, no staging VGPRs) measured 0.2-0.3 us per step
-// faster but its build's c4 and grid-300 rollouts were not reproducible: the first rollout of a
-// process differed from the later ones in 1-3 dW3 entries owned by lanes 48-63 (6 of 18
-// repeats identical vs 18 of 18 with this copy; profiles/r04i_imgdma_nondeterminism.txt).
+// Both rollout images (contiguous in LDS: teacher then student) by LDS-DMA: every 16-B piece is
+// one global_load_lds_dwordx4 (wave-uniform LDS base + lane x 16 B, per-lane global address), so
+// the copy needs no staging VGPRs and no ds_write pass.  `between` runs while they are in flight
+// (the producers' first observations); every wave then drains its DMA (vmcnt(0)) before the
+// caller's __syncthreads publishes the image.  Round 4 measured it 0.2-0.3 us per step faster
+// than the register-staged copy (profiles/r04c_imgdma_ab.txt) but reverted it: its first rollout
+// in a process differed in lanes-48-63 dW3 entries.  Round 5 found that signature's cause on the
+// compute side -- the SLP-packed dW3 accumulators at the tile loop's latch (PKWAR, DESIGN.md §3;
+// distill.hip is now built without SLP) -- and re-landed the fill; the register-staged form is
+// in profiles/r04_removed_diagnostic_variants.diff.
 template <int V4A, int V4B, int NT, class F>
 __device__ __forceinline__ void copy_images(float* L, const float* ta, const float* sb, F&& between) {
     constexpr int TOT = V4A + V4B, PER = (TOT + NT - 1) / NT;
-    f32x4 r[PER];
+    const int wbase = threadIdx.x & ~63;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const int x = threadIdx.x + u * NT;
-        if (x < V4A) r[u] = reinterpret_cast<const f32x4*>(ta)[x];
-        else if (x < TOT) r[u] = reinterpret_cast<const f32x4*>(sb)[x - V4A];
+        if (x < TOT)
+            __builtin_amdgcn_global_load_lds(x < V4A ? ta + 4 * x : sb + 4 * (x - V4A), L + 4 * (wbase + u * NT), 16, 0, 0);
     }
     between();
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int x = threadIdx.x + u * NT;
-        if (x < TOT) reinterpret_cast<f32x4*>(L)[x] = r[u];
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's image pieces have landed in LDS
 }
 
 // kTanhScale * x as four scalar multiplies: a vector multiply would be a v_pk_mul_f32, and packed-f32
@@ -1416,10 +1414,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     else mlp_forward<CP || KS>(LT, obt, j, g, H1, H2, mt0, mt1);
                     mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
                 } else {
-                    // KS (exact f32): the K-step kernel's schedule puts a W3 load into the SrcC of
-                    // layer 2's last in-flight f32 MFMA (hazards.py LDSRC): fenced (see mfma())
+                    // exact f32: hipcc schedules the A-operand prefetches and the W3 loads into the
+                    // SrcC registers of in-flight f32 MFMAs in this pair forward (hazards.py LDSRC,
+                    // found in the K-step and the LDS-DMA-fill builds): every group fenced (see mfma())
                     if constexpr (SPL) mlp_forward_pair_split(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
-                    else mlp_forward_pair<KS>(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
+                    else mlp_forward_pair<true>(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
                 }
                 STAMP(12);
                 // loss
