@@ -1210,9 +1210,11 @@ static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NETB_S
 constexpr int MD_TEACHER = 0, MD_ROWS = 1, MD_HELPER = 2;
 // KS: a.ksteps env steps in one launch (rdd_step_accum); the K = 1 instances are compiled without
 // the step loop.
-template <bool BS, bool SPL, bool CP, int MD, bool KS = false>
+template <bool BS, bool SPL, bool CP, int MD, bool KS = false, bool TC = false>
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     constexpr bool TGT = MD == MD_ROWS, HLP = MD == MD_HELPER;
+    static_assert(!TC || (BS && MD == MD_TEACHER && !KS), "teacher on the consumer: bf16 student, K = 1");
+    constexpr int P_TM = CP ? P_ACT : P_SACT;   // TC: the consumer's teacher means of one tile [16][2]
     static_assert(!HLP || !BS, "helper pairs: f32 student kernels only");
     constexpr int TN = TGT ? 0 : img_t(SPL), SN = img_s(BS, SPL);
     __shared__ __attribute__((aligned(16))) float lds[TN + SN + PAIRS * PSCR];
@@ -1315,6 +1317,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         const float rtv0 = 1.0f / __expf(2.0f * tl0), rtv1 = 1.0f / __expf(2.0f * tl1);
         uint32_t tiles = 0;
         uint32_t k = 0;
+        uint32_t tct = 0;   // TC: teacher tiles taken from the consumer
         bool ok = true;
         // HLP helper (pair 2 + o): the teacher forward of owner o's first tile (its observations
         // were formed in the prologue, before the barrier), means into this pair's P_ACT, flag [0]
@@ -1371,6 +1374,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             }
             STAMP(11);
             wave_sync();
+            if constexpr (TC) publish(flags + 2, k + 1);   // this group's observation rows are in P_SO
             const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
             for (int t = 0; t < ntile; ++t) {
                 const bool tvalid = base + TILE * t + j < a.n;
@@ -1408,11 +1412,18 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                         else mlp_forward_pair<true>(LT, LS, obt, j, g, H1, H2, mt0, mt1, ms0, ms1);
                     }
                 } else if constexpr (BS) {
+                    if (TC && (t & 1)) {   // the consumer ran this tile's teacher forward
+                        mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
+                        if (!(ok = wait_ge(flags + 3, ++tct, err))) break;
+                        mt0 = PS[P_TM + 2 * j];
+                        mt1 = PS[P_TM + 2 * j + 1];
+                    } else {
                     // CP, KS: in these kernels' schedules the compiler issues loads into the SrcC
                     // registers of the exact teacher's f32 MFMAs: fenced (see mfma())
                     if constexpr (SPL) mlp_forward_split(LT, obt, j, g, mt0, mt1);
-                    else mlp_forward<CP || KS>(LT, obt, j, g, H1, H2, mt0, mt1);
+                    else mlp_forward<CP || KS || TC>(LT, obt, j, g, H1, H2, mt0, mt1);
                     mlp_forward_bf16(LS, obt, j, g, H1, H2, ms0, ms1);
+                    }
                 } else {
                     // exact f32: hipcc schedules the A-operand prefetches and the W3 loads into the
                     // SrcC registers of in-flight f32 MFMAs in this pair forward (hazards.py LDSRC,
@@ -1801,11 +1812,37 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 STAMP(22);
             }
         }
+        uint32_t gi = 0, tcc = 0;   // TC: groups started, teacher tiles published
         for (uint32_t kk = 0;; ++kk) {
-        for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride) {
+        for (uint32_t grp = gfirst; ok && grp < ngroups; grp += gstride, ++gi) {
             const uint32_t base = grp * (uint32_t)gs;
             const int ntile = (int)min((uint32_t)(gs / TILE), (n32 - base + TILE - 1) / TILE);
-            for (int t = 0; ok && t < ntile; ++t) ok = bwd_tile(t);
+            if constexpr (TC) {
+                if (!(ok = wait_ge(flags + 2, gi + 1, err))) break;
+            }
+            for (int t = 0; ok && t < ntile; ++t) {
+                if constexpr (TC) {
+                    // the teacher forward of the next (odd) tile, from the producer's observation rows:
+                    // its means go to P_TM, read by the producer at that tile (one tile in flight: the
+                    // producer takes them before it publishes the tile this wave consumes next)
+                    if (!(t & 1) && t + 1 < ntile) {
+                        const float* obt = PS + P_SO + TILE * (t + 1) * SOS;
+                        float m0, m1;
+                        if constexpr (SPL) {
+                            mlp_forward_split(LT, obt, j, g, m0, m1);
+                        } else {
+                            f32x4 h1[4], h2[4];
+                            mlp_forward<true>(LT, obt, j, g, h1, h2, m0, m1);
+                        }
+                        if (g == 0) {
+                            PS[P_TM + 2 * j] = m0;
+                            PS[P_TM + 2 * j + 1] = m1;
+                        }
+                        publish(flags + 3, ++tcc);
+                    }
+                }
+                ok = bwd_tile(t);
+            }
             if (!ok) break;
             end_group(base, C + kk);
         }
@@ -2092,6 +2129,12 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
         bs ? (spl ? rollout_kernel<true, true, true, MD_TEACHER> : rollout_kernel<true, false, true, MD_TEACHER>)
            : hlp ? (spl ? rollout_kernel<false, true, false, MD_HELPER> : rollout_kernel<false, false, false, MD_HELPER>)
                  : (spl ? rollout_kernel<false, true, false, MD_TEACHER> : rollout_kernel<false, false, false, MD_TEACHER>);
+#ifdef RD_TC
+    if (bs && spl && ksteps == 1) k = rollout_kernel<true, true, true, MD_TEACHER, false, true>;
+#endif
+#ifdef RD_TC_NOCP
+    if (bs && spl && ksteps == 1) k = rollout_kernel<true, true, false, MD_TEACHER, false, true>;
+#endif
     if (ksteps > 1)   // K steps per launch: the producer steps the envs it reads (no CP)
         k = bs ? (spl ? rollout_kernel<true, true, false, MD_TEACHER, true> : rollout_kernel<true, false, false, MD_TEACHER, true>)
                : (spl ? rollout_kernel<false, true, false, MD_TEACHER, true> : rollout_kernel<false, false, false, MD_TEACHER, true>);

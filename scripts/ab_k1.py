@@ -1,6 +1,6 @@
 """Per-step time of the fused step (K = 1) for the BASELINE workloads and of the K = 50 launch at
 the 32,768-env shard, in one process; RD_LIB selects the build (A/B runs alternate processes).
-  python scripts/ab_k1.py [steps]"""
+  python scripts/ab_k1.py [steps] [workload,...]"""
 import json
 import os
 import sys
@@ -18,9 +18,11 @@ WL = {"c2": dict(n_envs=4096), "c3": dict(n_envs=65536, loss="kl"), "c4": dict(n
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+    names = sys.argv[2].split(",") if len(sys.argv) > 2 else list(WL)
     dev = torch.device("cuda", 0)
     out = {"lib": os.environ.get("RD_LIB", "libreacher.so")}
-    for name, kw in WL.items():
+    for name in names:
+        kw = WL[name]
         tr = DistillTrainer(DistillConfig(seed=0, **kw), device=dev)
         K = kw.get("accum_steps", 1)
         fn = tr.step if K == 1 else tr.step_accum
