@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void inputs_kernel(const float* ob, const floa
                                                      float* X, int64_t R, int64_t B, float keep_prob, uint64_t seed,
                                                      int64_t row_base, const uint32_t* ctl, uint32_t* bar) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx == 0) { bar[0] = 0u; bar[1] = 0u; }   // the persistent kernels' grid-barrier counters
+    if (idx == 0) bar[3] += 1u;   // the persistent kernels' granule generation: one per forward call
     if (idx >= R * XLD) return;
     const int64_t r = idx / XLD;
     const int col = (int)(idx % XLD);
@@ -215,10 +215,12 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
 // Workgroup w owns units 16w..16w+15 (13 workgroups): its slice of Wr stays in LDS for the
 // whole launch (the forward's 64 gate columns, BPTT's 16 rows of Wr^T), its cell states c
 // (forward) and dc (BPTT) stay in registers, and between steps the workgroups exchange h
-// (forward) or dz (BPTT) through global memory across a grid barrier: an agent-scope arrival
-// counter with release/acquire fences (the workgroups sit on different XCDs, whose L2s are
-// not coherent), a bounded spin that raises a flag instead of hanging (all 13 workgroups are
-// co-resident: one per CU of 256).  The forward's MFMA sequence and cell arithmetic are
+// (forward) or partial dh (BPTT) through global memory as data-tagged granules (below; the
+// workgroups sit on different XCDs, whose L2s are not coherent): no grid barrier, each
+// consumer re-reads until its granules carry the step's tag, a bounded spin that raises a flag
+// instead of hanging (all 13 workgroups are co-resident: one per CU of 256).  Round 2-4 used the
+// write-through payload + agent-scope arrival counter + barrier poll form (~4 round trips per
+// step; profiles/r05_removed_diagnostic_variants.diff keeps nothing of it: git history does).  The forward's MFMA sequence and cell arithmetic are
 // lstm_rec_fwd_kernel's, so G, c and h are bitwise those of the per-step launches.
 constexpr int PR_ROWS = 32, PR_UNITS = 16, PR_K = 208, PR_GRID = (U + PR_UNITS - 1) / PR_UNITS;
 constexpr int PR_WS = 80;    // forward Wr slice row stride: [k][16 gate + unit], conflict-free B reads
@@ -226,45 +228,24 @@ constexpr int PR_HS = 48;    // A operand row stride: [k][row], conflict-free A 
 constexpr int PR_ZS = 68;    // gate pre-activation exchange [row][64 + pad]
 constexpr uint32_t PR_SPIN_LIMIT = 1u << 22;
 
-// Hand-off between the workgroups of a persistent launch (cdna_hip_programming.md §6 Guideline
-// 16, the write-through form): the exchanged payload (h, dz) is stored with sc1 buffer stores
-// and drained (s_waitcnt vmcnt(0)) before the workgroup's arrival on an agent-scope counter,
-// and EVERY load of it is an sc1 buffer load -- no L2 writeback or L1 invalidate fences (a
-// release/acquire pair per step measured ~3.5 us).  All other data these kernels read was
-// written before the launch.
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t pr_rsrc(const float* base, int64_t floats) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)(floats * 4), 0x00020000);
+// Data-tagged granules (cdna_hip_programming.md §6 Guideline 16, R2 / MI355X_MICROARCH.md
+// "allgather"): each exchanged f32 travels as ONE naturally aligned 8-byte word {tag, value},
+// written by one agent-scope (sc1) store and read by agent-scope loads; a consumer re-reads
+// its granules until every tag is the one it waits for.  No payload drain, no arrival counter,
+// no barrier poll per step: the data is the flag.  Tags = (generation << 8) | phase, the
+// generation advanced on the device once per forward call (inputs_kernel, bar[3]; a replayed
+// graph advances it too), so a granule left by an earlier call never matches.  Two buffers by
+// step parity: a workgroup overwrites parity p only after it read every other workgroup's
+// granules of the step between, which those wrote only after reading parity p themselves.
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+__device__ __forceinline__ void gr_store(unsigned long long* p, uint32_t tag, float v) {
+    __hip_atomic_store((gu64_t*)(p), ((unsigned long long)tag << 32) | __float_as_uint(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ rdg::f32x4 pr_load4(__amdgpu_buffer_rsrc_t r, int64_t idx) {   // sc1
-    return __builtin_bit_cast(rdg::f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
+__device__ __forceinline__ unsigned long long gr_load(const unsigned long long* p) {
+    return __hip_atomic_load((const gu64_t*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void pr_store(__amdgpu_buffer_rsrc_t r, int64_t idx, float x) {   // sc1
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)(idx * 4), 0, 16);
-}
-
-// grid barrier #k of a launch (target = k * gridDim.x arrivals on *bar); false on timeout
-__device__ __forceinline__ bool pr_grid_sync(uint32_t* bar, uint32_t target, uint32_t* err) {
-    __shared__ int ok_s;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 payload stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int ok = 1;
-        for (uint32_t spins = 0; __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
-            if (++spins > PR_SPIN_LIMIT) {
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        ok_s = ok;
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
-    return ok_s != 0;
-}
+__device__ __forceinline__ uint32_t gr_tag(uint32_t gen, uint32_t phase) { return (gen << 8) | phase; }
 
 // rows [32][NB*U] of a [B][ld] matrix -> S[b*PR_K + k][row] (row stride PR_HS); every 16-B load
 // of the thread is issued before its first LDS store.  ld4(row, col) loads 4 floats.
@@ -289,20 +270,23 @@ __device__ __forceinline__ void stage_rows(int B, float (*S)[PR_HS], L&& ld4) {
     }
 }
 
-// bar: [0] forward arrivals [1] BPTT arrivals (zeroed by the preceding inputs / loss kernels)
-// [2] timeout flag.  state0: null (zero state) or [c | h] of [B][U] each; Cs/H rows of step 0
-// are written from it for the backward.
+// bar: [2] timeout flag, [3] granule generation (inputs_kernel).  hx: h granules [2][PR_ROWS][U]
+// (step parity).  state0: null (zero state) or [c | h] of [B][U] each; Cs/H rows of step 0 are
+// written from it for the backward.
+constexpr int GR_SWEEP = (PR_ROWS * U + 255) / 256;   // h granules per thread per step (25 at 32 rows)
 __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ Z,
                                                                const float* __restrict__ state0, float* __restrict__ G,
                                                                float* __restrict__ Cs, float* __restrict__ H, int B,
-                                                               int T, uint32_t* bar) {
+                                                               int T, uint32_t* bar, unsigned long long* hx) {
     __shared__ __attribute__((aligned(16))) float Ws[PR_K][PR_WS];
     __shared__ __attribute__((aligned(16))) float Hs[PR_K][PR_HS];
     __shared__ __attribute__((aligned(16))) float Zl[PR_ROWS][PR_ZS];
+    __shared__ int fail_s;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int u0 = blockIdx.x * PR_UNITS;
     const int rb = wave & 1, ch = wave >> 1;   // rows 16 rb.., gate blocks 2 ch, 2 ch + 1
-    const __amdgpu_buffer_rsrc_t rH = pr_rsrc(H, (int64_t)(T + 1) * B * U);
+    const uint32_t gen = bar[3];
+    if (tid == 0) fail_s = 0;
     {   // Wr slice: rows k of 4 gate blocks x 16 units (four 16-B pieces each), loads batched
         constexpr int PER = (PR_K * 16 + 255) / 256;
         rdg::f32x4 v[PER];
@@ -351,9 +335,31 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
         // A operand: h_s [B][U] -> Hs[k][row] (step 0: the initial state, read directly)
         const float* hs = s == 0 ? (state0 ? state0 + (int64_t)B * U : nullptr) : H + (int64_t)s * B * U;
         {
-            if (s > 0) {   // h_s: written in this launch (sc1)
-                const int64_t base = (int64_t)s * B * U;
-                stage_rows<1>(B, Hs, [&](int row, int c) { return pr_load4(rH, base + (int64_t)row * U + c); });
+            if (s > 0) {   // h_s: the other workgroups' granules of step s, re-read until every tag matches
+                const unsigned long long* src = hx + (int64_t)(s & 1) * PR_ROWS * U;
+                const uint32_t want = gr_tag(gen, (uint32_t)s);
+                const int nb = B * U;
+                for (uint32_t spins = 0;;) {
+                    unsigned long long v[GR_SWEEP];
+#pragma unroll
+                    for (int j = 0; j < GR_SWEEP; ++j) v[j] = gr_load(src + min(tid + 256 * j, nb - 1));
+                    bool ok = true;
+#pragma unroll
+                    for (int j = 0; j < GR_SWEEP; ++j) {
+                        const int idx = tid + 256 * j;
+                        if (idx < nb) {
+                            ok &= (uint32_t)(v[j] >> 32) == want;
+                            Hs[idx % U][idx / U] = __uint_as_float((uint32_t)v[j]);
+                        }
+                    }
+                    if (ok) break;
+                    if (++spins > PR_SPIN_LIMIT) {
+                        __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        fail_s = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
             } else if (hs) {
                 stage_rows<1>(B, Hs, [&](int row, int c) {
                     return *reinterpret_cast<const rdg::f32x4*>(hs + (int64_t)row * U + c);
@@ -363,6 +369,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
             }
         }
         __syncthreads();
+        if (fail_s) return;   // (uniform) a peer's granules never arrived: the timeout flag is raised
         // one accumulation chain per gate block and k order as lstm_rec_fwd_kernel (bitwise);
         // the two blocks' chains interleave
         rdg::f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -397,12 +404,11 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
             float* g = G + row_g * G4;
             g[u] = gi; g[U + u] = gj; g[2 * U + u] = gf; g[3 * U + u] = go;
             Cs[(row_g + B) * U + u] = c;
-            pr_store(rH, (row_g + B) * U + u, go * tanhf(c));
+            const float h = go * tanhf(c);
+            H[(row_g + B) * U + u] = h;   // for the backward (a later launch)
+            if (s + 1 < T) gr_store(hx + (int64_t)((s + 1) & 1) * PR_ROWS * U + (int64_t)row * U + u, gr_tag(gen, (uint32_t)(s + 1)), h);
         }
-        if (s + 1 < T) {
-            load_zx(s + 1);
-            if (!pr_grid_sync(bar, (uint32_t)(s + 1) * gridDim.x, bar + 2)) return;
-        }
+        if (s + 1 < T) load_zx(s + 1);
     }
 }
 
@@ -411,22 +417,25 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
 //  (2) runs the cell backward at its (row, unit) points -> dz_s of its 64 gate columns (to dZ
 //      for the weight gradients, and to LDS),
 //  (3) multiplies those 64 columns by its 64 rows of Wr^T: a partial dh_{s-1} for ALL units,
-//      stored sc1 to its slot of a per-step-parity partial buffer, then the grid barrier.
-// So a step exchanges 13 x 2 KB per workgroup (the units' partials), not all of dz (64 KB).
+//      stored as granules {tag, value} to its slot of a per-step-parity partial buffer.
+// So a step exchanges 13 x 20 rows x 16 units of granules per workgroup (its units' partials),
+// not all of dz (64 KB); (1) re-reads them until every tag matches (no barrier).
 constexpr int PB_N = 208;    // units, padded: 13 column blocks of 16
 constexpr int PB_PART = PB_N * PR_ROWS;   // floats of one workgroup's partial [unit][row]
 __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ dHh,
                                                                 const float* __restrict__ G, const float* __restrict__ Cs,
-                                                                float* __restrict__ dZ, float* __restrict__ part,
+                                                                float* __restrict__ dZ, unsigned long long* __restrict__ part,
                                                                 float* __restrict__ dbl, const float* __restrict__ prev,
                                                                 float* __restrict__ Q, int B, int T, uint32_t* bar) {
     __shared__ __attribute__((aligned(16))) float Wb[64][PB_N];        // [local gate col y*16+c][unit]
     __shared__ __attribute__((aligned(16))) float As[64][PR_HS];       // dz_s of the local columns: [col][row]
+    __shared__ int fail_s;
     static_assert(PR_HS >= 40, "As also holds the 5 x 8 row-group sums at the end");
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int u0 = blockIdx.x * PR_UNITS;
     const int rb = wave & 1, cb0 = (wave >> 1) * 7, ncb = (wave >> 1) ? 6 : 7;   // rows 16 rb.., column blocks
-    const __amdgpu_buffer_rsrc_t rP = pr_rsrc(part, (int64_t)2 * PR_GRID * PB_PART);
+    const uint32_t gen = bar[3];
+    if (tid == 0) fail_s = 0;
     {   // Wb[y*16 + c][n] = Wr[n][y*U + u0 + c]: rows n of Wr, 16 consecutive gate columns each
         constexpr int PER = (PB_N * 16 + 255) / 256;
         rdg::f32x4 v[PER];
@@ -471,19 +480,44 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
         }
     };
     load_cell(T - 1);
-    uint32_t nsync = 0;
     for (int s = T - 1; s >= 0; --s) {
         float dhn[4] = {0.f, 0.f, 0.f, 0.f};
-        if (s < T - 1 && act) {   // (1) dh_next: the 13 partials of step s+1, fixed order
-            const int64_t pb = (int64_t)((s + 1) & 1) * PR_GRID * PB_PART + (int64_t)u * PR_ROWS + 4 * r4;
-            rdg::f32x4 v[PR_GRID];
+        if (s < T - 1) {   // (1) dh_next: the 13 partials of step s+1 (granules), summed in a fixed order
+            if (act) {
+                const unsigned long long* pb = part + (int64_t)((s + 1) & 1) * PR_GRID * PB_PART + (int64_t)u * PR_ROWS + 4 * r4;
+                const uint32_t want = gr_tag(gen, 128u + (uint32_t)(s + 1));
+                const bool rowok[4] = {4 * r4 < B, 4 * r4 + 1 < B, 4 * r4 + 2 < B, 4 * r4 + 3 < B};
+                for (uint32_t spins = 0;;) {
+                    unsigned long long v[PR_GRID][4];
 #pragma unroll
-            for (int w = 0; w < PR_GRID; ++w) v[w] = pr_load4(rP, pb + (int64_t)w * PB_PART);
-            rdg::f32x4 acc = v[0];
+                    for (int w = 0; w < PR_GRID; ++w)
 #pragma unroll
-            for (int w = 1; w < PR_GRID; ++w) acc += v[w];
+                        for (int r = 0; r < 4; ++r) v[w][r] = gr_load(pb + (int64_t)w * PB_PART + r);
+                    bool ok = true;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dhn[r] = acc[r];
+                    for (int w = 0; w < PR_GRID; ++w)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) ok &= !rowok[r] || (uint32_t)(v[w][r] >> 32) == want;
+                    if (ok) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float a = __uint_as_float((uint32_t)v[0][r]);
+#pragma unroll
+                            for (int w = 1; w < PR_GRID; ++w) a += __uint_as_float((uint32_t)v[w][r]);
+                            dhn[r] = rowok[r] ? a : 0.0f;
+                        }
+                        break;
+                    }
+                    if (++spins > PR_SPIN_LIMIT) {
+                        __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        fail_s = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            if (fail_s) return;   // (uniform) a peer's granules never arrived: the timeout flag is raised
         }
         // (2) TF1 LSTMCell backward (cell_bwd_kernel's arithmetic)
         const int64_t rs = (int64_t)s * B;
@@ -530,15 +564,16 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
             }
         }
         const int64_t po = (int64_t)(s & 1) * PR_GRID * PB_PART + (int64_t)blockIdx.x * PB_PART;
+        const uint32_t tag = gr_tag(gen, 128u + (uint32_t)s);
 #pragma unroll
         for (int q = 0; q < 7; ++q) {   // lane (i, gq): rows 16 rb + 4 gq .. +3 of unit 16 (cb0 + q) + i
-            if (q < ncb)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[q]), rP,
-                                                       (int)((po + (int64_t)(16 * (cb0 + q) + i) * PR_ROWS + 16 * rb + 4 * gq) * 4),
-                                                       0, 16);
+            if (q < ncb) {
+                unsigned long long* d = part + po + (int64_t)(16 * (cb0 + q) + i) * PR_ROWS + 16 * rb + 4 * gq;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gr_store(d + r, tag, acc[q][r]);
+            }
         }
         __syncthreads();   // As is rewritten by the next step's cell
-        if (!pr_grid_sync(bar + 1, ++nsync * gridDim.x, bar + 2)) return;
     }
     // dbl (the gate bias gradient) and Q = prev^T dz of the local columns: the 8 row groups'
     // sums, in order (As[col][8 j + r4] holds sum j of row group r4)
@@ -1125,7 +1160,8 @@ struct rdl_trainer {
     int64_t colws_floats = 0;
     uint32_t* ctl = nullptr;
     uint32_t* bar = nullptr;   // persistent kernels: [0] forward / [1] BPTT barrier arrivals, [2] timeout flag
-    float* bpart = nullptr;    // persistent BPTT: per-step-parity partial dh of every workgroup
+    unsigned long long* bpart = nullptr;   // persistent BPTT: per-step-parity partial dh granules of every workgroup
+    unsigned long long* hx = nullptr;      // persistent forward: per-step-parity h granules
     float* qbuf = nullptr;     // persistent BPTT: Q = prev^T dz [4][800]
     int64_t last_B = 0;   // windows of the last forward pass (rdl_final_state)
 };
@@ -1220,7 +1256,7 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     if (persistent(t, B)) {   // Zx, then all T recurrent steps in one launch (it writes the step-0 state rows)
         RDL_CK(mm(t, (int)R, G4, XI, t->X, XLD, 0, P + OFF_WL, G4, 0, t->Z, G4, P + OFF_BL), "rdl gemm Zx");
         hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
-                           (const float*)t->Z, state0, t->G, t->Cs, t->H, (int)B, T, t->bar);
+                           (const float*)t->Z, state0, t->G, t->Cs, t->H, (int)B, T, t->bar, t->hx);
         RDL_CK(hipGetLastError(), "rdl lstm_fwd_persist_kernel");
     } else {
     if (state0) {
@@ -1451,7 +1487,10 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     alloc(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
     if (e == hipSuccess) e = hipMalloc((void**)&t->ctl, sizeof(uint32_t) * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&t->bar, sizeof(uint32_t) * 4);
-    alloc(&t->bpart, (int64_t)2 * PR_GRID * PB_PART);
+    if (e == hipSuccess) e = hipMalloc((void**)&t->bpart, sizeof(unsigned long long) * 2 * PR_GRID * PB_PART);
+    if (e == hipSuccess) e = hipMemsetAsync(t->bpart, 0, sizeof(unsigned long long) * 2 * PR_GRID * PB_PART, t->stream);
+    if (e == hipSuccess) e = hipMalloc((void**)&t->hx, sizeof(unsigned long long) * 2 * PR_ROWS * U);
+    if (e == hipSuccess) e = hipMemsetAsync(t->hx, 0, sizeof(unsigned long long) * 2 * PR_ROWS * U, t->stream);
     alloc(&t->qbuf, 4 * G4);
     if (e == hipSuccess) e = hipMemsetAsync(t->bar, 0, sizeof(uint32_t) * 4, t->stream);
     t->grad = t->own_grad;
@@ -1483,9 +1522,11 @@ int rdl_destroy(rdl_trainer* t) {
     rd::DeviceGuard dg(t->device);
     float* bufs[] = {t->params, t->m, t->v, t->own_grad, t->X, t->H, t->Cs, t->Z, t->G, t->A1, t->A2, t->A3, t->A4,
                      t->Y, t->dY, t->D32, t->D64a, t->D128, t->D64b, t->dHh, t->dP, t->dhn, t->dc, t->split,
-                     t->colws, t->lpart, t->hist, t->bpart, t->qbuf, t->hpart};
+                     t->colws, t->lpart, t->hist, t->qbuf, t->hpart};
     for (float* p : bufs)
         if (p) (void)hipFree(p);
+    if (t->bpart) (void)hipFree(t->bpart);
+    if (t->hx) (void)hipFree(t->hx);
     if (t->ctl) (void)hipFree(t->ctl);
     if (t->bar) (void)hipFree(t->bar);
     delete t;

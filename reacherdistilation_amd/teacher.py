@@ -58,7 +58,7 @@ def fit_teacher(ob, t_pdflat, *, phases=((30_000, 1e-3), (20_000, 1e-4)), seed: 
     tp = np.asarray(t_pdflat, np.float32).reshape(-1, EPISODE_STEPS, 4)
     flat = ob.reshape(-1, OBSPACE_SHAPE).astype(np.float64)
     mean, std = obfilter(flat.sum(0), np.square(flat).sum(0), flat.shape[0])
-    logstd = tuple(float(x) for x in tp.reshape(-1, 4)[:, 2:].mean(0))
+    logstd = tuple(float(x) for x in tp.reshape(-1, 4)[:, 2:].astype(np.float64).mean(0))   # (f64: exact when constant)
     p = MlpPolicyParams.init(seed, logstd=logstd, out_std=0.01)
     p.ob_mean, p.ob_std = mean, std
     hist = []

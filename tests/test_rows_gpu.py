@@ -233,7 +233,7 @@ def test_fitted_teacher_reproduces_the_fixture_teacher(golden):
         assert np.array_equal(tq[:, 2:].astype(np.float32), ref[:, 2:].astype(np.float32))   # the logstd
         return float(np.mean((tq[:, :2] - ref[:, :2]) ** 2))
     train, held = mse(0, 21), mse(21, 25)
-    f = ob[:21].reshape(-1, 11).astype(np.float64)
+    f = ob[:21].reshape(-1, 11).astype(np.float32).astype(np.float64)   # the f32 records fit_teacher sees
     m, s = obfilter(f.sum(0), np.square(f).sum(0), f.shape[0])
     assert np.array_equal(p.ob_mean, m) and np.array_equal(p.ob_std, s)
     print(f"fitted teacher: train MSE {train:.3g} (1,050 records), eps 21-24 {held:.3g}; {hist}")
