@@ -1210,6 +1210,10 @@ static_assert((NETX + NETX_S + PAIRS * PSCR) * 4 <= 160 * 1024 && (NETX + NETB_S
 constexpr int MD_TEACHER = 0, MD_ROWS = 1, MD_HELPER = 2;
 // KS: a.ksteps env steps in one launch (rdd_step_accum); the K = 1 instances are compiled without
 // the step loop.
+// TC (bf16 student with the split teacher, config 5): the consumer wave runs the teacher forward
+// of each group's odd tiles from the producer's observation rows and hands the means back
+// (P_TM, flag [3]); the producer publishes each group's observations (flag [2]) and runs the
+// teacher of the even tiles beside the student forwards (c5 -0.5 us per step).
 template <bool BS, bool SPL, bool CP, int MD, bool KS = false, bool TC = false>
 __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
     constexpr bool TGT = MD == MD_ROWS, HLP = MD == MD_HELPER;
@@ -2126,15 +2130,10 @@ int launch_rollout(rdd_trainer* t, const float* obs_in = nullptr, int64_t n_obs 
     if (hlp) grid = (int)((ngroups + 1) / 2);
     t->last_grid = grid;
     void (*k)(RolloutArgs) =
-        bs ? (spl ? rollout_kernel<true, true, true, MD_TEACHER> : rollout_kernel<true, false, true, MD_TEACHER>)
+        bs ? (spl ? rollout_kernel<true, true, true, MD_TEACHER, false, true>   // TC: DESIGN.md §3 "c5"
+                  : rollout_kernel<true, false, true, MD_TEACHER>)
            : hlp ? (spl ? rollout_kernel<false, true, false, MD_HELPER> : rollout_kernel<false, false, false, MD_HELPER>)
                  : (spl ? rollout_kernel<false, true, false, MD_TEACHER> : rollout_kernel<false, false, false, MD_TEACHER>);
-#ifdef RD_TC
-    if (bs && spl && ksteps == 1) k = rollout_kernel<true, true, true, MD_TEACHER, false, true>;
-#endif
-#ifdef RD_TC_NOCP
-    if (bs && spl && ksteps == 1) k = rollout_kernel<true, true, false, MD_TEACHER, false, true>;
-#endif
     if (ksteps > 1)   // K steps per launch: the producer steps the envs it reads (no CP)
         k = bs ? (spl ? rollout_kernel<true, true, false, MD_TEACHER, true> : rollout_kernel<true, false, false, MD_TEACHER, true>)
                : (spl ? rollout_kernel<false, true, false, MD_TEACHER, true> : rollout_kernel<false, false, false, MD_TEACHER, true>);

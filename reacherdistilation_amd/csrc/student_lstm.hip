@@ -81,7 +81,10 @@ __global__ __launch_bounds__(256) void inputs_kernel(const float* ob, const floa
                                                      float* X, int64_t R, int64_t B, float keep_prob, uint64_t seed,
                                                      int64_t row_base, const uint32_t* ctl, uint32_t* bar) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx == 0) bar[3] += 1u;   // the persistent kernels' granule generation: one per forward call
+    if (idx == 0) {
+        bar[1] = 0u;    // the persistent BPTT's grid-barrier counter
+        bar[3] += 1u;   // the persistent forward's granule generation: one per forward call
+    }
     if (idx >= R * XLD) return;
     const int64_t r = idx / XLD;
     const int col = (int)(idx % XLD);
@@ -215,18 +218,59 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
 // Workgroup w owns units 16w..16w+15 (13 workgroups): its slice of Wr stays in LDS for the
 // whole launch (the forward's 64 gate columns, BPTT's 16 rows of Wr^T), its cell states c
 // (forward) and dc (BPTT) stay in registers, and between steps the workgroups exchange h
-// (forward) or partial dh (BPTT) through global memory as data-tagged granules (below; the
-// workgroups sit on different XCDs, whose L2s are not coherent): no grid barrier, each
-// consumer re-reads until its granules carry the step's tag, a bounded spin that raises a flag
-// instead of hanging (all 13 workgroups are co-resident: one per CU of 256).  Round 2-4 used the
-// write-through payload + agent-scope arrival counter + barrier poll form (~4 round trips per
-// step; profiles/r05_removed_diagnostic_variants.diff keeps nothing of it: git history does).  The forward's MFMA sequence and cell arithmetic are
+// (forward) or partial dh (BPTT) through global memory (the workgroups sit on different XCDs,
+// whose L2s are not coherent), with bounded spins that raise a flag instead of hanging (all 13
+// workgroups are co-resident: one per CU of 256).  The forward's h travels as data-tagged
+// granules, no grid barrier (round 5: 81 -> 68 us for T = 10 at 20 windows); BPTT keeps the
+// write-through payload + agent-scope arrival counter form, since its granule form (52
+// 8-byte granules per thread and step instead of 13 16-byte loads) measured slower (76 -> 103 us,
+// profiles/r05i_*).  The forward's MFMA sequence and cell arithmetic are
 // lstm_rec_fwd_kernel's, so G, c and h are bitwise those of the per-step launches.
 constexpr int PR_ROWS = 32, PR_UNITS = 16, PR_K = 208, PR_GRID = (U + PR_UNITS - 1) / PR_UNITS;
 constexpr int PR_WS = 80;    // forward Wr slice row stride: [k][16 gate + unit], conflict-free B reads
 constexpr int PR_HS = 48;    // A operand row stride: [k][row], conflict-free A reads
 constexpr int PR_ZS = 68;    // gate pre-activation exchange [row][64 + pad]
 constexpr uint32_t PR_SPIN_LIMIT = 1u << 22;
+
+// BPTT's hand-off between the workgroups of a persistent launch (cdna_hip_programming.md §6
+// Guideline 16, the write-through form): the exchanged payload (h, dz) is stored with sc1 buffer stores
+// and drained (s_waitcnt vmcnt(0)) before the workgroup's arrival on an agent-scope counter,
+// and EVERY load of it is an sc1 buffer load -- no L2 writeback or L1 invalidate fences (a
+// release/acquire pair per step measured ~3.5 us).  All other data these kernels read was
+// written before the launch.
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pr_rsrc(const float* base, int64_t floats) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)(floats * 4), 0x00020000);
+}
+__device__ __forceinline__ rdg::f32x4 pr_load4(__amdgpu_buffer_rsrc_t r, int64_t idx) {   // sc1
+    return __builtin_bit_cast(rdg::f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
+}
+__device__ __forceinline__ void pr_store(__amdgpu_buffer_rsrc_t r, int64_t idx, float x) {   // sc1
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)(idx * 4), 0, 16);
+}
+
+// grid barrier #k of a launch (target = k * gridDim.x arrivals on *bar); false on timeout
+__device__ __forceinline__ bool pr_grid_sync(uint32_t* bar, uint32_t target, uint32_t* err) {
+    __shared__ int ok_s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 payload stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int ok = 1;
+        for (uint32_t spins = 0; __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+            if (++spins > PR_SPIN_LIMIT) {
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        ok_s = ok;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
+    return ok_s != 0;
+}
 
 // Data-tagged granules (cdna_hip_programming.md §6 Guideline 16, R2 / MI355X_MICROARCH.md
 // "allgather"): each exchanged f32 travels as ONE naturally aligned 8-byte word {tag, value},
@@ -417,25 +461,22 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
 //  (2) runs the cell backward at its (row, unit) points -> dz_s of its 64 gate columns (to dZ
 //      for the weight gradients, and to LDS),
 //  (3) multiplies those 64 columns by its 64 rows of Wr^T: a partial dh_{s-1} for ALL units,
-//      stored as granules {tag, value} to its slot of a per-step-parity partial buffer.
-// So a step exchanges 13 x 20 rows x 16 units of granules per workgroup (its units' partials),
-// not all of dz (64 KB); (1) re-reads them until every tag matches (no barrier).
+//      stored sc1 to its slot of a per-step-parity partial buffer, then the grid barrier.
+// So a step exchanges 13 x 2 KB per workgroup (the units' partials), not all of dz (64 KB).
 constexpr int PB_N = 208;    // units, padded: 13 column blocks of 16
 constexpr int PB_PART = PB_N * PR_ROWS;   // floats of one workgroup's partial [unit][row]
 __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ dHh,
                                                                 const float* __restrict__ G, const float* __restrict__ Cs,
-                                                                float* __restrict__ dZ, unsigned long long* __restrict__ part,
+                                                                float* __restrict__ dZ, float* __restrict__ part,
                                                                 float* __restrict__ dbl, const float* __restrict__ prev,
                                                                 float* __restrict__ Q, int B, int T, uint32_t* bar) {
     __shared__ __attribute__((aligned(16))) float Wb[64][PB_N];        // [local gate col y*16+c][unit]
     __shared__ __attribute__((aligned(16))) float As[64][PR_HS];       // dz_s of the local columns: [col][row]
-    __shared__ int fail_s;
     static_assert(PR_HS >= 40, "As also holds the 5 x 8 row-group sums at the end");
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int u0 = blockIdx.x * PR_UNITS;
     const int rb = wave & 1, cb0 = (wave >> 1) * 7, ncb = (wave >> 1) ? 6 : 7;   // rows 16 rb.., column blocks
-    const uint32_t gen = bar[3];
-    if (tid == 0) fail_s = 0;
+    const __amdgpu_buffer_rsrc_t rP = pr_rsrc(part, (int64_t)2 * PR_GRID * PB_PART);
     {   // Wb[y*16 + c][n] = Wr[n][y*U + u0 + c]: rows n of Wr, 16 consecutive gate columns each
         constexpr int PER = (PB_N * 16 + 255) / 256;
         rdg::f32x4 v[PER];
@@ -480,44 +521,19 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
         }
     };
     load_cell(T - 1);
+    uint32_t nsync = 0;
     for (int s = T - 1; s >= 0; --s) {
         float dhn[4] = {0.f, 0.f, 0.f, 0.f};
-        if (s < T - 1) {   // (1) dh_next: the 13 partials of step s+1 (granules), summed in a fixed order
-            if (act) {
-                const unsigned long long* pb = part + (int64_t)((s + 1) & 1) * PR_GRID * PB_PART + (int64_t)u * PR_ROWS + 4 * r4;
-                const uint32_t want = gr_tag(gen, 128u + (uint32_t)(s + 1));
-                const bool rowok[4] = {4 * r4 < B, 4 * r4 + 1 < B, 4 * r4 + 2 < B, 4 * r4 + 3 < B};
-                for (uint32_t spins = 0;;) {
-                    unsigned long long v[PR_GRID][4];
+        if (s < T - 1 && act) {   // (1) dh_next: the 13 partials of step s+1, fixed order
+            const int64_t pb = (int64_t)((s + 1) & 1) * PR_GRID * PB_PART + (int64_t)u * PR_ROWS + 4 * r4;
+            rdg::f32x4 v[PR_GRID];
 #pragma unroll
-                    for (int w = 0; w < PR_GRID; ++w)
+            for (int w = 0; w < PR_GRID; ++w) v[w] = pr_load4(rP, pb + (int64_t)w * PB_PART);
+            rdg::f32x4 acc = v[0];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) v[w][r] = gr_load(pb + (int64_t)w * PB_PART + r);
-                    bool ok = true;
+            for (int w = 1; w < PR_GRID; ++w) acc += v[w];
 #pragma unroll
-                    for (int w = 0; w < PR_GRID; ++w)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) ok &= !rowok[r] || (uint32_t)(v[w][r] >> 32) == want;
-                    if (ok) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float a = __uint_as_float((uint32_t)v[0][r]);
-#pragma unroll
-                            for (int w = 1; w < PR_GRID; ++w) a += __uint_as_float((uint32_t)v[w][r]);
-                            dhn[r] = rowok[r] ? a : 0.0f;
-                        }
-                        break;
-                    }
-                    if (++spins > PR_SPIN_LIMIT) {
-                        __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        fail_s = 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            __syncthreads();
-            if (fail_s) return;   // (uniform) a peer's granules never arrived: the timeout flag is raised
+            for (int r = 0; r < 4; ++r) dhn[r] = acc[r];
         }
         // (2) TF1 LSTMCell backward (cell_bwd_kernel's arithmetic)
         const int64_t rs = (int64_t)s * B;
@@ -564,16 +580,15 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
             }
         }
         const int64_t po = (int64_t)(s & 1) * PR_GRID * PB_PART + (int64_t)blockIdx.x * PB_PART;
-        const uint32_t tag = gr_tag(gen, 128u + (uint32_t)s);
 #pragma unroll
         for (int q = 0; q < 7; ++q) {   // lane (i, gq): rows 16 rb + 4 gq .. +3 of unit 16 (cb0 + q) + i
-            if (q < ncb) {
-                unsigned long long* d = part + po + (int64_t)(16 * (cb0 + q) + i) * PR_ROWS + 16 * rb + 4 * gq;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) gr_store(d + r, tag, acc[q][r]);
-            }
+            if (q < ncb)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[q]), rP,
+                                                       (int)((po + (int64_t)(16 * (cb0 + q) + i) * PR_ROWS + 16 * rb + 4 * gq) * 4),
+                                                       0, 16);
         }
         __syncthreads();   // As is rewritten by the next step's cell
+        if (!pr_grid_sync(bar + 1, ++nsync * gridDim.x, bar + 2)) return;
     }
     // dbl (the gate bias gradient) and Q = prev^T dz of the local columns: the 8 row groups'
     // sums, in order (As[col][8 j + r4] holds sum j of row group r4)
@@ -1160,7 +1175,7 @@ struct rdl_trainer {
     int64_t colws_floats = 0;
     uint32_t* ctl = nullptr;
     uint32_t* bar = nullptr;   // persistent kernels: [0] forward / [1] BPTT barrier arrivals, [2] timeout flag
-    unsigned long long* bpart = nullptr;   // persistent BPTT: per-step-parity partial dh granules of every workgroup
+    float* bpart = nullptr;                // persistent BPTT: per-step-parity partial dh of every workgroup
     unsigned long long* hx = nullptr;      // persistent forward: per-step-parity h granules
     float* qbuf = nullptr;     // persistent BPTT: Q = prev^T dz [4][800]
     int64_t last_B = 0;   // windows of the last forward pass (rdl_final_state)
@@ -1487,8 +1502,7 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     alloc(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
     if (e == hipSuccess) e = hipMalloc((void**)&t->ctl, sizeof(uint32_t) * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&t->bar, sizeof(uint32_t) * 4);
-    if (e == hipSuccess) e = hipMalloc((void**)&t->bpart, sizeof(unsigned long long) * 2 * PR_GRID * PB_PART);
-    if (e == hipSuccess) e = hipMemsetAsync(t->bpart, 0, sizeof(unsigned long long) * 2 * PR_GRID * PB_PART, t->stream);
+    alloc(&t->bpart, (int64_t)2 * PR_GRID * PB_PART);
     if (e == hipSuccess) e = hipMalloc((void**)&t->hx, sizeof(unsigned long long) * 2 * PR_ROWS * U);
     if (e == hipSuccess) e = hipMemsetAsync(t->hx, 0, sizeof(unsigned long long) * 2 * PR_ROWS * U, t->stream);
     alloc(&t->qbuf, 4 * G4);
@@ -1522,10 +1536,9 @@ int rdl_destroy(rdl_trainer* t) {
     rd::DeviceGuard dg(t->device);
     float* bufs[] = {t->params, t->m, t->v, t->own_grad, t->X, t->H, t->Cs, t->Z, t->G, t->A1, t->A2, t->A3, t->A4,
                      t->Y, t->dY, t->D32, t->D64a, t->D128, t->D64b, t->dHh, t->dP, t->dhn, t->dc, t->split,
-                     t->colws, t->lpart, t->hist, t->qbuf, t->hpart};
+                     t->colws, t->lpart, t->hist, t->bpart, t->qbuf, t->hpart};
     for (float* p : bufs)
         if (p) (void)hipFree(p);
-    if (t->bpart) (void)hipFree(t->bpart);
     if (t->hx) (void)hipFree(t->hx);
     if (t->ctl) (void)hipFree(t->ctl);
     if (t->bar) (void)hipFree(t->bar);
