@@ -8,6 +8,7 @@ OUT=gpurun_out/r05f; mkdir -p $OUT; export TMPDIR=/tmp
 BARGS="--steps 100 --warmup 200 --no-cpu-baseline --no-exact-leg --accum 0 --conv-steps 0 --fixture-steps 0 --no-strong-projection"
 PARGS="--steps 20 --warmup 3 --no-cpu-baseline --no-exact-leg --accum 0 --conv-steps 0 --fixture-steps 0 --no-strong-projection"
 for WL in c3 c5 c4; do
+  mkdir -p $OUT/$WL
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$WL/prof -o run -- python3 bench.py --workload $WL $BARGS > $OUT/$WL/bench.json 2> $OUT/$WL/prof.err || { tail $OUT/$WL/prof.err; exit 1; }
   for c in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA"; do
     t=$(echo $c | cut -d' ' -f1)
@@ -25,6 +26,6 @@ for cfg in "65536 kl" "32768 mse"; do
     t=$(echo $c | cut -d' ' -f1)
     timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $D/pmc_$t -o run -- python3 scripts/accum_probe.py $PA > $D/pmc_$t.log 2>&1 || { tail $D/pmc_$t.log; exit 1; }
   done
-  python3 scripts/pmc_traffic.py $D/pmc_rollout_k.json "0, true>" $D/pmc_*/ > /dev/null
+  python3 scripts/pmc_traffic.py $D/pmc_rollout_k.json "0, true, false>(" $D/pmc_*/ > /dev/null
   echo "k50 $N done"
 done
