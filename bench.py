@@ -640,7 +640,7 @@ def cpu_baseline(workload, seconds, threads, n):
                        f"OpenMP {threads} threads")
 
 
-def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=100, comm=None, split=False,
+def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=None, comm=None, split=False,
                 teacher=None):
     """North-star check: optimiser steps (one per env step, the reference's lr 1e-4 TF1 Adam)
     until the student's action-MSE vs the teacher, averaged over the last 10 steps and all
@@ -655,6 +655,8 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
                         comm=comm, teacher=teacher)
     t0 = time.perf_counter()
     steps, mse, hit = 0, float("nan"), None
+    if chunk is None:   # small batches: checked every 10 steps, as scripts/conv_sweep.py measures them
+        chunk = 10 if n * world <= 256 else 100
     while steps < max_steps:
         for _ in range(chunk):
             tr.step()

@@ -4,7 +4,9 @@ reference's 250,000 (mlp_train.py:143-204: 5,000 episodes x 50 steps).
   (a) the batched trainer at small batches and a few learning rates (bench.convergence);
   (b) the reference-shaped single-env driver (mlp_train.train: one env step + one Adam step on
       a 200-row dataset window per step, the reference's own loop), MSE loss.
-usage: python scripts/conv_sweep.py [out.jsonl]"""
+usage: python scripts/conv_sweep.py [out.jsonl] [--teacher fitted] [--quick]
+  --teacher fitted: the reference teacher's structure fitted to the fixture's 1,050 teacher records
+  (teacher.fit_teacher) instead of the synthetic teacher."""
 import json
 import os
 import sys
@@ -19,21 +21,28 @@ import bench  # noqa: E402
 
 
 def main():
-    out = open(sys.argv[1], "w") if len(sys.argv) > 1 else sys.stdout
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    out = open(args[0], "w") if args else sys.stdout
     dev = torch.device("cuda", 0)
     wl = bench.WORKLOADS["c2"]
-    for n in (16, 32, 64, 128, 256):
+    teacher = None
+    if "--teacher" in sys.argv and sys.argv[sys.argv.index("--teacher") + 1] == "fitted":
+        teacher, info = bench.fitted_teacher(dev)
+        out.write(json.dumps({"teacher": info}) + "\n")
+    sizes = (8, 16, 32, 64) if "--quick" in sys.argv else (16, 32, 64, 128, 256)
+    for n in sizes:
         for lr in (1e-4, 3e-4, 1e-3):
-            r = bench.convergence(wl, n, "f32", dev, 0, 1, lr, max_steps=min(20000, 2_000_000 // n), chunk=10,
-                                  split=True)
+            r = bench.convergence(wl, n, "f32", dev, 0, 1, lr, max_steps=min(40000, 2_000_000 // n), chunk=10,
+                                  split=True, teacher=teacher)
             r["leg"] = "batched"
+            r["teacher"] = "fitted" if teacher is not None else "synthetic"
             out.write(json.dumps(r) + "\n")
             out.flush()
     from reacherdistilation_amd import mlp_train
     for lr in (1e-4, 3e-4, 1e-3):
         t0 = time.perf_counter()
         tr, ds, losses = mlp_train.train(episodes=5000, warmup_episodes=40, loss="mse", lr=lr, log=lambda *a: None,
-                                         stop_loss=1e-3)
+                                         stop_loss=1e-3, teacher=teacher)
         el = time.perf_counter() - t0
         hit = len(losses) if losses and losses[-1] / 50 < 1e-3 else None
         env_steps = ds.num_episodes() * 50
