@@ -1,8 +1,9 @@
 // CRC32C (Castagnoli) on the host for the TF checkpoint reader / writer (tf_checkpoint.py):
 // the masked CRC of every table block and the crc32c of every tensor's bytes.  Slicing-by-8
-// (eight 256-entry tables, one 8-byte word per step): ~1-2 GB/s on one core, where the
-// per-byte Python loop it replaces ran at ~2 MB/s.  Reflected polynomial
-// 0x82F63B78, init/final xor ~0: check value crc32c("123456789") = 0xE3069283.
+// (eight 256-entry tables, one 8-byte word per step) everywhere, and the SSE4.2 crc32
+// instruction (which computes exactly this polynomial) where the host CPU has it; the per-byte
+// Python loop it replaces ran at ~2 MB/s.  Reflected polynomial 0x82F63B78,
+// init/final xor ~0: check value crc32c("123456789") = 0xE3069283.
 #include <stdint.h>
 #include <string.h>
 
@@ -28,12 +29,32 @@ const Tables& tables() {
     return tb;
 }
 
+// c is the running (pre-inverted) register on entry and exit
+__attribute__((target("sse4.2"))) uint32_t crc_hw(const uint8_t* data, int64_t n, uint32_t c) {
+    uint64_t c64 = c;
+    int64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, data + i, 8);
+        c64 = __builtin_ia32_crc32di(c64, w);
+    }
+    uint32_t c32 = (uint32_t)c64;
+    for (; i < n; ++i) c32 = __builtin_ia32_crc32qi(c32, data[i]);
+    return c32;
+}
+
+bool have_hw() {
+    static const bool hw = __builtin_cpu_supports("sse4.2");
+    return hw;
+}
+
 }  // namespace
 
 extern "C" uint32_t rd_crc32c(const uint8_t* data, int64_t n, uint32_t crc) {
-    const Tables& tb = tables();
     uint32_t c = ~crc;
     if (!data || n <= 0) return ~c;
+    if (have_hw()) return ~crc_hw(data, n, c);
+    const Tables& tb = tables();
     int64_t i = 0;
     for (; i + 8 <= n; i += 8) {   // little-endian host (x86-64)
         uint32_t lo, hi;

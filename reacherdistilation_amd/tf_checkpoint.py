@@ -52,16 +52,16 @@ def crc32c_py(data: bytes, crc: int = 0) -> int:
 
 
 def crc32c(data: bytes, crc: int = 0) -> int:
-    """CRC32C of `data`, continuing from `crc`: the native slicing-by-8 form (rd_crc32c in
-    libreacher.so; ~1 GB/s, where the per-byte loop runs at ~2 MB/s), else crc32c_py."""
+    """CRC32C of `data`, continuing from `crc`: the native form (rd_crc32c in libreacher.so:
+    the SSE4.2 crc32 instruction, else slicing-by-8), else crc32c_py (~2 MB/s)."""
     try:
         from . import _native
         lib = _native.load()
     except Exception:   # noqa: BLE001  (host utility: the library is the fast path, not a requirement)
         return crc32c_py(data, crc)
     import ctypes
-    b = bytes(data)
-    buf = ctypes.create_string_buffer(b, len(b)) if b else None
+    b = data if isinstance(data, bytes) else bytes(data)
+    buf = ctypes.c_char_p(b) if b else None   # points into the bytes object: no copy
     return int(lib.rd_crc32c(buf, len(b), crc & 0xFFFFFFFF))
 
 

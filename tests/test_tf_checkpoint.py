@@ -5,6 +5,7 @@ format only (round trips, the table/footer/CRC invariants, the CRC32C check valu
 unpinned); the teacher's VARIABLES -- names, shapes, dtypes, the Saver's key set -- and the
 observation filter's restore arithmetic are pinned to the reference's own logged GraphDef
 (its save/SaveV2 node and pi/obfilter ops)."""
+import os
 import struct
 
 import numpy as np
@@ -22,8 +23,9 @@ def test_crc32c_check_value():
 
 
 def test_native_crc32c_matches_the_table_definition():
-    """rd_crc32c (libreacher.so, slicing-by-8) = the per-byte table form on every length 0..70
-    (all tail cases of the 8-byte loop), on a 1 MB buffer, and when continued in pieces."""
+    """rd_crc32c (libreacher.so: SSE4.2 crc32 where the CPU has it) = the per-byte table form on
+    every length 0..70 (all tail cases of the 8-byte loop), on a 1 MB buffer, and when continued
+    in pieces."""
     rs = np.random.RandomState(0)
     data = rs.randint(0, 256, 1 << 20).astype(np.uint8).tobytes()
     for n in range(71):
@@ -32,6 +34,29 @@ def test_native_crc32c_matches_the_table_definition():
     assert big == tc.crc32c_py(data)
     assert tc.crc32c(data[600_001:], tc.crc32c(data[:600_001])) == big
 
+
+def test_native_crc32c_table_form_matches(tmp_path):
+    """The slicing-by-8 form (what a CPU without SSE4.2 runs) gives the same CRCs: the same source
+    built on the host with the CPU probe answering "no", called on every tail length and a
+    200 KB buffer, continued in pieces."""
+    import ctypes
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not found")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = str(tmp_path / "libcrc_tables.so")
+    src = tmp_path / "crc_tables.cpp"
+    src.write_text('#define __builtin_cpu_supports(feature) 0\n#include "%s"\n'
+                   % os.path.join(root, "reacherdistilation_amd", "csrc", "rd_crc32c.cpp"))
+    subprocess.run([gxx, "-O2", "-shared", "-fPIC", "-o", so, str(src)], check=True)
+    fn = ctypes.CDLL(so).rd_crc32c
+    fn.restype, fn.argtypes = ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_int64, ctypes.c_uint32]
+    d = np.random.RandomState(1).randint(0, 256, 200_000).astype(np.uint8).tobytes()
+    for n in list(range(71)) + [len(d)]:
+        assert fn(d[:n], n, 0) == tc.crc32c_py(d[:n]) == tc.crc32c(d[:n]), n
+    assert fn(d[77:], len(d) - 77, fn(d[:77], 77, 0)) == tc.crc32c(d)
 
 def test_lstm_checkpoint_round_trip_is_fast(tmp_path):
     """a T = 10 LSTM checkpoint with its Adam slots (6.1 MB) is written and read back
