@@ -76,15 +76,12 @@ constexpr int COLSUM_CHUNK = 512;         // rows per first-level column-sum blo
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-// X[r] = [dropout(ob[r]) (11) | prev[r] . Wp + bp (32) | 0]; r = t B + b
+// X[r] = [dropout(ob[r]) (11) | prev[r] . Wp + bp (32) | 0]; r = t B + b (the persistent forward
+// forms its steps' rows itself with the same arithmetic)
 __global__ __launch_bounds__(256) void inputs_kernel(const float* ob, const float* prev, const float* params,
                                                      float* X, int64_t R, int64_t B, float keep_prob, uint64_t seed,
-                                                     int64_t row_base, const uint32_t* ctl, uint32_t* bar) {
+                                                     int64_t row_base, const uint32_t* ctl) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx == 0) {
-        bar[1] = 0u;    // the persistent BPTT's grid-barrier counter
-        bar[3] += 1u;   // the persistent forward's granule generation: one per forward call
-    }
     if (idx >= R * XLD) return;
     const int64_t r = idx / XLD;
     const int col = (int)(idx % XLD);
@@ -129,10 +126,12 @@ __global__ __launch_bounds__(256) void cell_fwd_kernel(const float* Z, const flo
 // GEMM accumulating into Z + cell_fwd_kernel): a workgroup owns 64 rows x 16 units, i.e. the
 // 64 gate columns {i, j, f, o} x those units of Wr, so at the end of the K loop every lane
 // holds all four gate pre-activations of its (row, unit) outputs.  4 waves, wave w = rows
-// 16w..16w+15 x the 4 gate blocks (one A and four B operands per k-step, 4 MFMAs).  The k
-// order and the epilogue's z = (acc + 0) + Zx are the unfused path's, so G, c and h are
-// bitwise those of the two-launch form.  Z_s keeps the input half (the backward reuses Z).
+// 16w..16w+15 x the 4 gate blocks (one A and four B operands per k-step, 4 MFMAs).  The K sum
+// runs as two chains, k < 112 and k >= 112, and the epilogue's z = ((lo + hi) + 0) + Zx: the
+// persistent kernel's order (its waves split K there), so both give bitwise the same G, c and
+// h.  Z_s keeps the input half (the backward reuses Z).
 constexpr int RF_ROWS = 64, RF_UNITS = 16, RF_TK = 16, RF_LS = 64 + 16;
+constexpr int LSTM_KH = 112;   // the recurrent K sum as two chains, k < 112 and k >= 112, added (lo + hi)
 __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restrict__ Hp, const float* __restrict__ Wr,
                                                            const float* __restrict__ Zx,
                                                            const float* __restrict__ cprev, float* __restrict__ Gs,
@@ -158,17 +157,10 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
         for (int e = 0; e < 4; ++e) As[buf][ak + e][tid >> 2] = a[e];
         *reinterpret_cast<rdg::f32x4*>(&Bs[buf][bk][16 * by + 4 * (bq & 3)]) = b;
     };
-    rdg::f32x4 acc[4];
+    rdg::f32x4 lo[4], hi[4];   // the two K chains (the persistent kernel's waves kh = 0, 1)
 #pragma unroll
-    for (int y = 0; y < 4; ++y) acc[y] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
-    // load pipeline of rd_gemm.h: tile t+2's loads issue right after tile t+1 is staged, so
-    // they stay in flight across the barrier and the next MFMA phase
-    constexpr int NT = (U + RF_TK - 1) / RF_TK;
-    stage(0, load_a(0), load_b(0));
-    rdg::f32x4 na = load_a(RF_TK), nb = load_b(RF_TK);
-    __syncthreads();
-    for (int kt = 0; kt < NT; ++kt) {
-        const int buf = kt & 1;
+    for (int y = 0; y < 4; ++y) lo[y] = hi[y] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+    auto tile = [&](int buf, rdg::f32x4 (&acc)[4]) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int kk = 4 * s + gq;
@@ -177,6 +169,18 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
             for (int y = 0; y < 4; ++y)
                 acc[y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[buf][kk][16 * y + i], acc[y], 0, 0, 0);
         }
+    };
+    // load pipeline of rd_gemm.h: tile t+2's loads issue right after tile t+1 is staged, so
+    // they stay in flight across the barrier and the next MFMA phase
+    constexpr int NT = (U + RF_TK - 1) / RF_TK;
+    static_assert(LSTM_KH % RF_TK == 0, "the K split falls on a tile boundary");
+    stage(0, load_a(0), load_b(0));
+    rdg::f32x4 na = load_a(RF_TK), nb = load_b(RF_TK);
+    __syncthreads();
+    for (int kt = 0; kt < NT; ++kt) {
+        const int buf = kt & 1;
+        if (kt < LSTM_KH / RF_TK) tile(buf, lo);
+        else tile(buf, hi);
         if (kt + 1 < NT) {
             stage(buf ^ 1, na, nb);
             if (kt + 2 < NT) {
@@ -201,8 +205,8 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
     for (int r = 0; r < 4; ++r) {
         const int64_t row = m0 + 16 * wave + 4 * gq + r;
         if (row >= B || u >= U) continue;
-        const float gi = sigm((acc[0][r] + 0.0f) + zx[0][r]), gj = tanhf((acc[1][r] + 0.0f) + zx[1][r]);
-        const float gf = sigm((acc[2][r] + 0.0f) + zx[2][r] + 1.0f), go = sigm((acc[3][r] + 0.0f) + zx[3][r]);
+        const float gi = sigm(((lo[0][r] + hi[0][r]) + 0.0f) + zx[0][r]), gj = tanhf(((lo[1][r] + hi[1][r]) + 0.0f) + zx[1][r]);
+        const float gf = sigm(((lo[2][r] + hi[2][r]) + 0.0f) + zx[2][r] + 1.0f), go = sigm(((lo[3][r] + hi[3][r]) + 0.0f) + zx[3][r]);
         const float c = fmaf(gf, cpv[r], gi * gj);
         float* g = Gs + row * G4;
         g[u] = gi; g[U + u] = gj; g[2 * U + u] = gf; g[3 * U + u] = go;
@@ -212,31 +216,32 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------- persistent recurrence
-// Small batches (B <= PR_ROWS windows, e.g. the reference's 20) are launch-latency bound:
-// ~10 us per recurrent step whatever the work.  lstm_fwd_persist_kernel runs ALL T steps of
-// the forward recurrence in one launch and lstm_bptt_persist_kernel all T steps of BPTT.
-// Workgroup w owns units 16w..16w+15 (13 workgroups): its slice of Wr stays in LDS for the
-// whole launch (the forward's 64 gate columns, BPTT's 16 rows of Wr^T), its cell states c
-// (forward) and dc (BPTT) stay in registers, and between steps the workgroups exchange h
-// (forward) or partial dh (BPTT) through global memory (the workgroups sit on different XCDs,
-// whose L2s are not coherent), with bounded spins that raise a flag instead of hanging (all 13
-// workgroups are co-resident: one per CU of 256).  The forward's h travels as data-tagged
-// granules, no grid barrier (round 5: 81 -> 68 us for T = 10 at 20 windows); BPTT keeps the
-// write-through payload + agent-scope arrival counter form, since its granule form (52
-// 8-byte granules per thread and step instead of 13 16-byte loads) measured slower (76 -> 103 us,
-// profiles/r05i_*).  The forward's MFMA sequence and cell arithmetic are
-// lstm_rec_fwd_kernel's, so G, c and h are bitwise those of the per-step launches.
-constexpr int PR_ROWS = 32, PR_UNITS = 16, PR_K = 208, PR_GRID = (U + PR_UNITS - 1) / PR_UNITS;
-constexpr int PR_WS = 80;    // forward Wr slice row stride: [k][16 gate + unit], conflict-free B reads
-constexpr int PR_HS = 48;    // A operand row stride: [k][row], conflict-free A reads
-constexpr int PR_ZS = 68;    // gate pre-activation exchange [row][64 + pad]
+// Small batches (B <= PR_ROWS windows, e.g. the reference's 20) are latency bound: ~10 us per
+// recurrent step as separate launches whatever the work.  lstm_fwd_persist_kernel runs ALL T
+// steps of the forward recurrence in one launch and lstm_bptt_persist_kernel all T steps of BPTT.
+// Workgroup w owns units 4w..4w+3 (50 workgroups, round 5; 13 of 16 units before): its 16 gate
+// columns c = 4 y + j (gate y, unit j), its slice of Wr held in REGISTERS as the MFMA B operands
+// for the whole launch, its cell points (row, unit) one per thread.  Per step the critical path
+// is the h hand-off, one short MFMA chain per wave and one cell evaluation per thread: at 13
+// workgroups each SIMD issued 104 f32 MFMAs per step with LDS-fed operands (2.9 us) and a thread
+// ran two cells (2.2 us), stamped in profiles/r05l_lstm_stamps.jsonl.  The forward's h travels
+// as data-tagged granules, no grid barrier; BPTT keeps the write-through payload + agent-scope
+// arrival counter form (its granule form measured slower at 13 workgroups, profiles/r05i_*).
+// The forward's K sum is two chains, k < PR_KH and k >= PR_KH, added (lo + hi) -- the per-step
+// kernel's order -- so G, c and h are bitwise those of the per-step launches.
+constexpr int PR_ROWS = 32, PR_UNITS = 4, PR_GRID = U / PR_UNITS;   // 50 workgroups
+constexpr int PR_COLS = 4 * PR_UNITS;   // 16 gate columns per workgroup: c = 4 y + j
+constexpr int PR_KH = LSTM_KH;          // K split of the forward's gate sums (lstm_rec_fwd_kernel's)
+constexpr int PR_AS = 212;              // h staging row pitch [row][k]: conflict-free A reads (212 = 20 mod 64)
+constexpr int PR_KQ = PR_KH / 4, PR_KQ1 = (U - PR_KH) / 4;   // k steps of the two halves (28, 22: pad k >= U skipped)
 constexpr uint32_t PR_SPIN_LIMIT = 1u << 22;
+static_assert(U % PR_UNITS == 0 && PR_KH % RF_TK == 0 && PR_KQ1 <= PR_KQ, "persistent LSTM tiling");
 
 // BPTT's hand-off between the workgroups of a persistent launch (cdna_hip_programming.md §6
-// Guideline 16, the write-through form): the exchanged payload (h, dz) is stored with sc1 buffer stores
-// and drained (s_waitcnt vmcnt(0)) before the workgroup's arrival on an agent-scope counter,
-// and EVERY load of it is an sc1 buffer load -- no L2 writeback or L1 invalidate fences (a
-// release/acquire pair per step measured ~3.5 us).  All other data these kernels read was
+// Guideline 16, the write-through form): the exchanged payload (partial dh) is stored with sc1
+// buffer stores and drained (s_waitcnt vmcnt(0)) before the workgroup's arrival on an agent-scope
+// counter, and EVERY load of it is an sc1 buffer load -- no L2 writeback or L1 invalidate fences
+// (a release/acquire pair per step measured ~3.5 us).  All other data these kernels read was
 // written before the launch.
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pr_rsrc(const float* base, int64_t floats) {
@@ -245,40 +250,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pr_rsrc(const float* base, int
 __device__ __forceinline__ rdg::f32x4 pr_load4(__amdgpu_buffer_rsrc_t r, int64_t idx) {   // sc1
     return __builtin_bit_cast(rdg::f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
 }
-__device__ __forceinline__ void pr_store(__amdgpu_buffer_rsrc_t r, int64_t idx, float x) {   // sc1
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)(idx * 4), 0, 16);
-}
-
-// grid barrier #k of a launch (target = k * gridDim.x arrivals on *bar); false on timeout
-__device__ __forceinline__ bool pr_grid_sync(uint32_t* bar, uint32_t target, uint32_t* err) {
-    __shared__ int ok_s;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 payload stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int ok = 1;
-        for (uint32_t spins = 0; __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
-            if (++spins > PR_SPIN_LIMIT) {
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        ok_s = ok;
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
-    return ok_s != 0;
-}
 
 // Data-tagged granules (cdna_hip_programming.md §6 Guideline 16, R2 / MI355X_MICROARCH.md
 // "allgather"): each exchanged f32 travels as ONE naturally aligned 8-byte word {tag, value},
 // written by one agent-scope (sc1) store and read by agent-scope loads; a consumer re-reads
 // its granules until every tag is the one it waits for.  No payload drain, no arrival counter,
 // no barrier poll per step: the data is the flag.  Tags = (generation << 8) | phase, the
-// generation advanced on the device once per forward call (inputs_kernel, bar[3]; a replayed
-// graph advances it too), so a granule left by an earlier call never matches.  Two buffers by
+// generation advanced on the device once per forward call (the forward's last workgroup, bar[3];
+// a replayed graph advances it too), so a granule left by an earlier call never matches.  Two buffers by
 // step parity: a workgroup overwrites parity p only after it read every other workgroup's
 // granules of the step between, which those wrote only after reading parity p themselves.
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -291,326 +270,444 @@ __device__ __forceinline__ unsigned long long gr_load(const unsigned long long* 
 }
 __device__ __forceinline__ uint32_t gr_tag(uint32_t gen, uint32_t phase) { return (gen << 8) | phase; }
 
-// rows [32][NB*U] of a [B][ld] matrix -> S[b*PR_K + k][row] (row stride PR_HS); every 16-B load
-// of the thread is issued before its first LDS store.  ld4(row, col) loads 4 floats.
-template <int NB, class L>
-__device__ __forceinline__ void stage_rows(int B, float (*S)[PR_HS], L&& ld4) {
-    constexpr int F4 = U / 4, PER = (NB * PR_ROWS * F4 + 255) / 256;
-    rdg::f32x4 v[PER];
+// SrcC fence around MFMA chains (student_mlp.hip's fence_begin / fence_end): every operand is
+// in registers before the chains start, the accumulators pass through an empty asm
+// (memory clobber) before and after them and are read by a VALU before the closing one, so no
+// load issues while one of these f32 MFMAs is in flight -- hipcc otherwise renames a chain's
+// accumulators and loads the next operands into registers an in-flight MFMA still reads as SrcC
+// (scripts/isa/hazards.py class LDSRC; found in the sixteen-wave head backward, round 5).  Used by
+// the head's data gradients and the persistent BPTT's weight-gradient chains.
+template <int Q>
+__device__ __forceinline__ void fence_begin(rdg::f32x4 (&G)[Q]) {
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int f = threadIdx.x + 256 * j, b = f / (PR_ROWS * F4), r = f - b * (PR_ROWS * F4);
-        const int row = r / F4, k4 = r - row * F4;
-        v[j] = (b < NB && row < B) ? ld4(row, b * U + 4 * k4) : rdg::f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int f = threadIdx.x + 256 * j, b = f / (PR_ROWS * F4), r = f - b * (PR_ROWS * F4);
-        const int row = r / F4, k4 = r - row * F4;
-        if (b < NB) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) S[b * PR_K + 4 * k4 + e][row] = v[j][e];
-        }
-    }
+    for (int t = 0; t < Q; ++t) asm volatile("" : "+v"(G[t])::"memory");
 }
-
-// bar: [2] timeout flag, [3] granule generation (inputs_kernel).  hx: h granules [2][PR_ROWS][U]
-// (step parity).  state0: null (zero state) or [c | h] of [B][U] each; Cs/H rows of step 0 are
-// written from it for the backward.
-constexpr int GR_SWEEP = (PR_ROWS * U + 255) / 256;   // h granules per thread per step (25 at 32 rows)
-__global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ Z,
+template <int Q>
+__device__ __forceinline__ void fence_end(rdg::f32x4 (&G)[Q]) {
+#pragma unroll
+    for (int t = 0; t < Q; ++t) G[t][3] = __builtin_amdgcn_fmed3f(G[t][3], G[t][3], G[t][3]);
+#pragma unroll
+    for (int t = 0; t < Q; ++t) asm volatile("" : "+v"(G[t])::"memory");
+}
+// bar: [0] the forward's finished-workgroup count, [1] the BPTT's barrier counter, [2] timeout
+// flag, [3] granule generation.  The last forward workgroup to finish (every one has read the
+// generation by then) resets [0] and [1] and advances [3], so the next call's tags are new.
+// hx: h granules [2][PR_ROWS][U] (step parity).  state0: null (zero state) or [c | h] of
+// [B][U] each; Cs/H rows of step 0 are written from it for the backward.  Wave (rb, kh): rows
+// 16 rb.. x the 16 local columns over K half kh; thread t < 4 B: the cell point (row t / 4,
+// unit u0 + t % 4).  The launch also forms the inputs (round 5: no inputs_kernel, no Zx GEMM
+// launch): per step s the rows X_s = [dropout(ob) | prev . Wp + bp] (x_value: inputs_kernel's
+// arithmetic; workgroup 0 stores them for the weight gradient) and the input half of the gates
+// Zx_s = X_s Wl[0:43] + bl of the local columns (the Zx GEMM's MFMA k order and epilogue), so
+// G, c and h stay bitwise those of the per-step path.  Zx of step s+1 is formed right after step
+// s publishes h, while the granules travel.
+constexpr int GR_SWEEP = (PR_ROWS * U + 255) / 256;   // h granules per thread per step (at most 25)
+constexpr int PR_XQ = (XI + 3) / 4;                    // Zx k steps (11; k = 43 is the zero column)
+__global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ P, const float* __restrict__ ob,
+                                                               const float* __restrict__ prev, float* __restrict__ X,
                                                                const float* __restrict__ state0, float* __restrict__ G,
                                                                float* __restrict__ Cs, float* __restrict__ H, int B,
-                                                               int T, uint32_t* bar, unsigned long long* hx) {
-    __shared__ __attribute__((aligned(16))) float Ws[PR_K][PR_WS];
-    __shared__ __attribute__((aligned(16))) float Hs[PR_K][PR_HS];
-    __shared__ __attribute__((aligned(16))) float Zl[PR_ROWS][PR_ZS];
+                                                               int T, float keep_prob, uint64_t seed, int64_t row_base,
+                                                               const uint32_t* __restrict__ ctl, uint32_t* bar,
+                                                               unsigned long long* hx) {
+    __shared__ __attribute__((aligned(16))) float As[PR_ROWS][PR_AS];          // h_s [row][k]; zero past B, U
+    __shared__ __attribute__((aligned(16))) float Zp[2][PR_ROWS][PR_COLS + 1];   // the K halves' sums [row][c]
+    __shared__ __attribute__((aligned(16))) float Xs[PR_ROWS][XLD];             // X_s rows; zero past B
+    __shared__ __attribute__((aligned(16))) float Zx[PR_ROWS][PR_COLS + 1];     // Zx_s of the local columns
     __shared__ int fail_s;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int u0 = blockIdx.x * PR_UNITS;
-    const int rb = wave & 1, ch = wave >> 1;   // rows 16 rb.., gate blocks 2 ch, 2 ch + 1
-    const uint32_t gen = bar[3];
+    const int rb = wave & 1, kh = wave >> 1;
+    const int kq0 = kh ? PR_KQ : 0;
+    const uint32_t gen = bar[3], step = ctl[0];
+    const float* Wr = P + OFF_WL + XI * G4;
     if (tid == 0) fail_s = 0;
-    {   // Wr slice: rows k of 4 gate blocks x 16 units (four 16-B pieces each), loads batched
-        constexpr int PER = (PR_K * 16 + 255) / 256;
-        rdg::f32x4 v[PER];
+    // this lane's B operands over the launch: Wr[k][y U + u0 + j] of column i = 4 y + j, and
+    // (waves 0, 1) Wl[k][..] of the input half, k < 43; the lane's bias bl[column i]
+    const int64_t col = (int64_t)(i >> 2) * U + u0 + (i & 3);
+    float bw[PR_KQ], bx[PR_XQ];
 #pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int f = tid + 256 * j, k = f >> 4, y = (f >> 2) & 3, c4 = f & 3, u = u0 + 4 * c4;
-            v[j] = (k < U && u < U) ? *reinterpret_cast<const rdg::f32x4*>(Wr + (int64_t)k * G4 + y * U + u)
-                                    : rdg::f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int f = tid + 256 * j, k = f >> 4, y = (f >> 2) & 3, c4 = f & 3;
-            if (k < PR_K) *reinterpret_cast<rdg::f32x4*>(&Ws[k][16 * y + 4 * c4]) = v[j];
-        }
+    for (int q = 0; q < PR_KQ; ++q) {
+        const int k = 4 * (kq0 + q) + gq;
+        bw[q] = (q < PR_KQ1 || kh == 0) ? Wr[(int64_t)k * G4 + col] : 0.0f;
     }
-    for (int x = tid; x < (PR_K - U) * PR_HS; x += 256) Hs[U + x / PR_HS][x % PR_HS] = 0.0f;   // k >= U: never written
-    // this thread's (row, unit) points of the cell: p = tid, tid + 256 over B x 16
-    float cst[2];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int pt = tid + 256 * q, row = pt >> 4, u = u0 + (pt & 15);
-        cst[q] = 0.0f;
-        if (row < B && u < U) {
-            const int64_t idx = (int64_t)row * U + u;
-            const float c0 = state0 ? state0[idx] : 0.0f, h0 = state0 ? state0[(int64_t)B * U + idx] : 0.0f;
-            cst[q] = c0;
-            Cs[idx] = c0;   // rows of step 0, read by the backward
-            H[idx] = h0;
-        }
+    for (int q = 0; q < PR_XQ; ++q) {
+        const int k = 4 * q + gq;
+        bx[q] = (kh == 0 && k < XI) ? P[OFF_WL + (int64_t)k * G4 + col] : 0.0f;
     }
-    // the input half of a step's gate pre-activations (written by the Zx GEMM before this
-    // launch): loaded one step ahead, before the grid barrier, so that only h crosses it
-    float zx[2][4];
-    auto load_zx = [&](int s) {
-        const float* Zs = Z + (int64_t)s * B * G4;
+    const float bias = P[OFF_BL + col];
+    // this thread's column of the dense32 part of X (c = 11 + tid % 32 for every row it forms)
+    const int dc = tid & 31;
+    float wp[4];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int pt = tid + 256 * q, row = pt >> 4, u = u0 + (pt & 15);
-            const bool ok = row < B && u < U;
+    for (int a = 0; a < 4; ++a) wp[a] = P[OFF_WP + a * 32 + dc];
+    const float bpc = P[OFF_BP + dc];
+    for (int x = tid; x < PR_ROWS * PR_AS; x += 256) (&As[0][0])[x] = 0.0f;
+    for (int x = tid; x < PR_ROWS * XLD; x += 256) (&Xs[0][0])[x] = 0.0f;
+    const bool pt = tid < 4 * B;
+    const int pr = tid >> 2, pu = u0 + (tid & 3);
+    float cst = 0.0f;
+    if (pt) {
+        const int64_t idx = (int64_t)pr * U + pu;
+        const float c0 = state0 ? state0[idx] : 0.0f, h0 = state0 ? state0[(int64_t)B * U + idx] : 0.0f;
+        cst = c0;
+        Cs[idx] = c0;   // rows of step 0, read by the backward
+        H[idx] = h0;
+    }
+    // X_s -> Xs (and X, workgroup 0): x_value's arithmetic with one Philox draw per (row, 4
+    // columns) of the dropout part and the dense32 part's weights held in registers; then
+    // Zx_s = Xs Wl[0:43] + bl on waves 0, 1 -> Zx
+    auto inputs = [&](int s) {
+        for (int x = tid; x < 3 * B; x += 256) {   // dropout(ob) (student_nn.py:24): columns 4 q .. 4 q + 3 < 11
+            const int r = x / 3, q = x - 3 * r;
+            const int64_t rg = (int64_t)s * B + r;
+            uint32_t o[4] = {0u, 0u, 0u, 0u};
+            if (keep_prob < 1.0f) {
+                const uint64_t w = (uint64_t)(row_base + r);
+                rd::philox((uint32_t)w, (uint32_t)(w >> 32), step, (uint32_t)(4 * s + q), (uint32_t)seed,
+                           (uint32_t)(seed >> 32), o);
+            }
 #pragma unroll
-            for (int y = 0; y < 4; ++y) zx[q][y] = ok ? Zs[(int64_t)row * G4 + y * U + u] : 0.0f;
+            for (int e = 0; e < 4; ++e) {
+                const int c = 4 * q + e;
+                if (c < 11) {
+                    float v = ob[rg * 11 + c];
+                    if (keep_prob < 1.0f) v = rd::u01(o[e]) < keep_prob ? v / keep_prob : 0.0f;
+                    Xs[r][c] = v;
+                    if (blockIdx.x == 0) X[rg * XLD + c] = v;
+                }
+            }
+        }
+        for (int x = tid; x < 32 * B; x += 256) {   // prev . Wp + bp (student_nn.py:26)
+            const int r = x >> 5;
+            const int64_t rg = (int64_t)s * B + r;
+            const float* pv = prev + rg * 4;
+            float v = bpc;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) v = fmaf(pv[a], wp[a], v);
+            Xs[r][11 + dc] = v;
+            if (blockIdx.x == 0) X[rg * XLD + 11 + dc] = v;
+        }
+        if (blockIdx.x == 0)
+            for (int r = tid; r < B; r += 256) X[((int64_t)s * B + r) * XLD + XI] = 0.0f;
+        __syncthreads();   // Xs complete; the previous step's cell has read Zx
+        if (kh == 0) {
+            float av[PR_XQ];
+#pragma unroll
+            for (int q = 0; q < PR_XQ; ++q) av[q] = Xs[16 * rb + i][4 * q + gq];
+            rdg::f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
+            fence_begin(acc);
+#pragma unroll
+            for (int q = 0; q < PR_XQ; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bx[q], acc[0], 0, 0, 0);
+            fence_end(acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Zx[16 * rb + 4 * gq + r][i] = acc[0][r] + bias;
         }
     };
-    load_zx(0);
+    __syncthreads();   // As and Xs zeroed before the staging writes
+    inputs(0);
+    const int nb = B * U;
     for (int s = 0; s < T; ++s) {
-        // A operand: h_s [B][U] -> Hs[k][row] (step 0: the initial state, read directly)
-        const float* hs = s == 0 ? (state0 ? state0 + (int64_t)B * U : nullptr) : H + (int64_t)s * B * U;
-        {
-            if (s > 0) {   // h_s: the other workgroups' granules of step s, re-read until every tag matches
-                const unsigned long long* src = hx + (int64_t)(s & 1) * PR_ROWS * U;
-                const uint32_t want = gr_tag(gen, (uint32_t)s);
-                const int nb = B * U;
-                for (uint32_t spins = 0;;) {
-                    unsigned long long v[GR_SWEEP];
+        if (s > 0) {   // h_s: every workgroup's granules of step s, re-read until every tag matches
+            const unsigned long long* src = hx + (int64_t)(s & 1) * PR_ROWS * U;
+            const uint32_t want = gr_tag(gen, (uint32_t)s);
+            for (uint32_t spins = 0;;) {
+                unsigned long long v[GR_SWEEP];
 #pragma unroll
-                    for (int j = 0; j < GR_SWEEP; ++j) v[j] = gr_load(src + min(tid + 256 * j, nb - 1));
-                    bool ok = true;
+                for (int j = 0; j < GR_SWEEP; ++j)
+                    v[j] = 256 * j < nb ? gr_load(src + min(tid + 256 * j, nb - 1)) : (unsigned long long)want << 32;
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < GR_SWEEP; ++j) ok &= (uint32_t)(v[j] >> 32) == want;
+                if (ok) {
 #pragma unroll
                     for (int j = 0; j < GR_SWEEP; ++j) {
                         const int idx = tid + 256 * j;
-                        if (idx < nb) {
-                            ok &= (uint32_t)(v[j] >> 32) == want;
-                            Hs[idx % U][idx / U] = __uint_as_float((uint32_t)v[j]);
-                        }
+                        if (idx < nb) As[idx / U][idx % U] = __uint_as_float((uint32_t)v[j]);
                     }
-                    if (ok) break;
-                    if (++spins > PR_SPIN_LIMIT) {
-                        __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        fail_s = 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
+                    break;
                 }
-            } else if (hs) {
-                stage_rows<1>(B, Hs, [&](int row, int c) {
-                    return *reinterpret_cast<const rdg::f32x4*>(hs + (int64_t)row * U + c);
-                });
-            } else {
-                for (int x = tid; x < PR_ROWS * U; x += 256) Hs[x % U][x / U] = 0.0f;
+                if (++spins > PR_SPIN_LIMIT) {
+                    __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    fail_s = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
+        } else if (state0) {
+            const float* hs = state0 + (int64_t)B * U;
+            for (int idx = tid; idx < nb; idx += 256) As[idx / U][idx % U] = hs[idx];
         }
         __syncthreads();
-        if (fail_s) return;   // (uniform) a peer's granules never arrived: the timeout flag is raised
-        // one accumulation chain per gate block and k order as lstm_rec_fwd_kernel (bitwise);
-        // the two blocks' chains interleave
-        rdg::f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        if (fail_s) break;   // (uniform) a peer's granules never arrived: the timeout flag is raised
+        // this wave's K half: one accumulation chain in k order (the per-step kernel's lo / hi)
+        rdg::f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
         {
-            for (int kt = 0; kt < PR_K / 16; ++kt) {
+            const float* arow = &As[16 * rb + i][4 * kq0 + gq];
+            float av[PR_KQ];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int kk = 16 * kt + 4 * q + gq;
-                    const float a = Hs[kk][16 * rb + i];
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Ws[kk][16 * (2 * ch) + i], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Ws[kk][16 * (2 * ch + 1) + i], acc1, 0, 0, 0);
-                }
+            for (int q = 0; q < PR_KQ1; ++q) av[q] = arow[4 * q];
+            if (kh == 0) {
+#pragma unroll
+                for (int q = PR_KQ1; q < PR_KQ; ++q) av[q] = arow[4 * q];
             }
+            fence_begin(acc);
+#pragma unroll
+            for (int q = 0; q < PR_KQ1; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[q], acc[0], 0, 0, 0);
+            if (kh == 0) {
+#pragma unroll
+                for (int q = PR_KQ1; q < PR_KQ; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[q], acc[0], 0, 0, 0);
+            }
+            fence_end(acc);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {   // C layout: lane (i, gq) holds rows 4 gq + r, column i
-            Zl[16 * rb + 4 * gq + r][16 * (2 * ch) + i] = acc0[r];
-            Zl[16 * rb + 4 * gq + r][16 * (2 * ch + 1) + i] = acc1[r];
-        }
+        for (int r = 0; r < 4; ++r) Zp[kh][16 * rb + 4 * gq + r][i] = acc[0][r];   // C: rows 4 gq + r, column i
         __syncthreads();
-        // TF1 LSTMCell (lstm_rec_fwd_kernel's arithmetic)
+        // TF1 LSTMCell (lstm_rec_fwd_kernel's arithmetic) at this thread's point
+        if (pt) {
+            const int c0 = tid & 3;
+            float z[4];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int pt = tid + 256 * q, row = pt >> 4, ul = pt & 15, u = u0 + ul;
-            if (row >= B || u >= U) continue;
-            const float* zr = Zl[row];
-            const float gi = sigm((zr[ul] + 0.0f) + zx[q][0]), gj = tanhf((zr[16 + ul] + 0.0f) + zx[q][1]);
-            const float gf = sigm((zr[32 + ul] + 0.0f) + zx[q][2] + 1.0f), go = sigm((zr[48 + ul] + 0.0f) + zx[q][3]);
-            const float c = fmaf(gf, cst[q], gi * gj);
-            cst[q] = c;
-            const int64_t row_g = (int64_t)s * B + row;
-            float* g = G + row_g * G4;
-            g[u] = gi; g[U + u] = gj; g[2 * U + u] = gf; g[3 * U + u] = go;
-            Cs[(row_g + B) * U + u] = c;
+            for (int y = 0; y < 4; ++y) z[y] = ((Zp[0][pr][4 * y + c0] + Zp[1][pr][4 * y + c0]) + 0.0f) + Zx[pr][4 * y + c0];
+            const float gi = sigm(z[0]), gj = tanhf(z[1]), gf = sigm(z[2] + 1.0f), go = sigm(z[3]);
+            const float c = fmaf(gf, cst, gi * gj);
+            cst = c;
             const float h = go * tanhf(c);
-            H[(row_g + B) * U + u] = h;   // for the backward (a later launch)
-            if (s + 1 < T) gr_store(hx + (int64_t)((s + 1) & 1) * PR_ROWS * U + (int64_t)row * U + u, gr_tag(gen, (uint32_t)(s + 1)), h);
+            if (s + 1 < T) gr_store(hx + (int64_t)((s + 1) & 1) * PR_ROWS * U + (int64_t)pr * U + pu, gr_tag(gen, (uint32_t)(s + 1)), h);
+            const int64_t row_g = (int64_t)s * B + pr;
+            float* g = G + row_g * G4 + pu;
+            g[0] = gi; g[U] = gj; g[2 * U] = gf; g[3 * U] = go;
+            Cs[(row_g + B) * U + pu] = c;
+            H[(row_g + B) * U + pu] = h;   // for the backward (a later launch)
         }
-        if (s + 1 < T) load_zx(s + 1);
+        if (s + 1 < T) inputs(s + 1);
+    }
+    // the last workgroup to finish advances the generation (every workgroup read it at entry)
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t done = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done + 1 == gridDim.x) {
+            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bar + 3, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
 // BPTT of all T steps, split-K over the workgroups: per step s (T-1 .. 0) workgroup w
-//  (1) sums dh_next for its 16 units from the 13 partials of step s+1 (fixed order, sc1 loads),
-//  (2) runs the cell backward at its (row, unit) points -> dz_s of its 64 gate columns (to dZ
-//      for the weight gradients, and to LDS),
-//  (3) multiplies those 64 columns by its 64 rows of Wr^T: a partial dh_{s-1} for ALL units,
-//      stored sc1 to its slot of a per-step-parity partial buffer, then the grid barrier.
-// So a step exchanges 13 x 2 KB per workgroup (the units' partials), not all of dz (64 KB).
+//  (1) sums dh_next at its points from the 50 partials of step s+1 (fixed order, sc1 loads),
+//  (2) runs the cell backward at its points -> dz_s of its 16 gate columns (to LDS),
+//  (3) multiplies those 16 columns by its 16 rows of Wr^T: a partial dh_{s-1} for ALL units,
+//      stored sc1 to its slot of a per-step-parity partial buffer, arrives at the grid barrier,
+//  (4) while the other workgroups arrive: its 16 columns of dWl += [x_s | h_{s-1}]^T dz_s (the
+//      LSTM kernel's weight gradient, 243 x 16 per workgroup, accumulated in registers over the
+//      steps: no dz round trip through HBM and no weight-gradient launch, round 5).
 constexpr int PB_N = 208;    // units, padded: 13 column blocks of 16
 constexpr int PB_PART = PB_N * PR_ROWS;   // floats of one workgroup's partial [unit][row]
+constexpr int PB_RED = 4 + 16;            // per point: the dbl sums (4 gates) and Q = prev^T dz (4 x 4)
 __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __restrict__ Wr, const float* __restrict__ dHh,
                                                                 const float* __restrict__ G, const float* __restrict__ Cs,
-                                                                float* __restrict__ dZ, float* __restrict__ part,
+                                                                const float* __restrict__ X, const float* __restrict__ Hp,
+                                                                float* __restrict__ dWl, float* __restrict__ part,
                                                                 float* __restrict__ dbl, const float* __restrict__ prev,
                                                                 float* __restrict__ Q, int B, int T, uint32_t* bar) {
-    __shared__ __attribute__((aligned(16))) float Wb[64][PB_N];        // [local gate col y*16+c][unit]
-    __shared__ __attribute__((aligned(16))) float As[64][PR_HS];       // dz_s of the local columns: [col][row]
-    static_assert(PR_HS >= 40, "As also holds the 5 x 8 row-group sums at the end");
+    __shared__ __attribute__((aligned(16))) float Dz[PR_ROWS][PR_COLS + 1];          // dz_s [row][c]; zero past B
+    __shared__ __attribute__((aligned(16))) float Dh[PR_GRID][PR_UNITS][PR_ROWS];    // dh_next partials [w][j][row]
+    __shared__ float red[PR_ROWS][PR_UNITS][PB_RED];
+    __shared__ int ok_s;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     const int u0 = blockIdx.x * PR_UNITS;
-    const int rb = wave & 1, cb0 = (wave >> 1) * 7, ncb = (wave >> 1) ? 6 : 7;   // rows 16 rb.., column blocks
-    const __amdgpu_buffer_rsrc_t rP = pr_rsrc(part, (int64_t)2 * PR_GRID * PB_PART);
-    {   // Wb[y*16 + c][n] = Wr[n][y*U + u0 + c]: rows n of Wr, 16 consecutive gate columns each
-        constexpr int PER = (PB_N * 16 + 255) / 256;
-        rdg::f32x4 v[PER];
+    // (4)'s operands and sums: wave w owns dWl rows 16 (w + 4 q) .. +15 (q < 4) x the 16 local
+    // columns; xa[q][rq] = A^T[k = 16 (w + 4 q) + i][r = 4 rq + gq], A = [x_s | h_{s-1}] rows of step s
+    rdg::f32x4 accw[4];
 #pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int f = tid + 256 * j, n = f >> 4, y = (f >> 2) & 3, c4 = f & 3, u = u0 + 4 * c4;
-            v[j] = (n < U && u < U) ? *reinterpret_cast<const rdg::f32x4*>(Wr + (int64_t)n * G4 + y * U + u)
-                                    : rdg::f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+    for (int q = 0; q < 4; ++q) accw[q] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+    float xa[4][PR_ROWS / 4];
+    auto load_a = [&](int s) {
 #pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int f = tid + 256 * j, n = f >> 4, y = (f >> 2) & 3, c4 = f & 3;
-            if (n < PB_N) {
+        for (int q = 0; q < 4; ++q) {
+            const int k = 16 * (wave + 4 * q) + i;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) Wb[16 * y + 4 * c4 + e][n] = v[j][e];
+            for (int rq = 0; rq < PR_ROWS / 4; ++rq) {
+                const int r = 4 * rq + gq;
+                const int64_t row = (int64_t)s * B + r;
+                xa[q][rq] = (r >= B || k >= XI + U) ? 0.0f : k < XI ? X[row * XLD + k] : Hp[row * U + (k - XI)];
             }
-        }
-    }
-    for (int x = tid; x < 64 * PR_HS; x += 256) As[x / PR_HS][x % PR_HS] = 0.0f;   // rows >= B stay 0
-    // this thread's points: unit c = tid & 15, rows 4 r4 .. 4 r4 + 3 (threads < 128)
-    const int c = tid & 15, r4 = tid >> 4, u = u0 + c;
-    const bool act = tid < 128 && u < U;
-    float dcs[4] = {0.f, 0.f, 0.f, 0.f};
-    float bsum[4] = {0.f, 0.f, 0.f, 0.f};   // dbl: this thread's rows, all steps, per gate
-    float qsum[4][4] = {};                    // Q = prev^T dz: [prev component][gate]
-    float cg[4][4], cct[4], ccp[4], cdh[4], cpv[4][4];
-    auto load_cell = [&](int s) {   // gates, c_t, c_{t-1}, dh from the head: written before the launch
-        const int64_t rs = (int64_t)s * B;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 4 * r4 + r;
-            const bool ok = act && row < B;
-            const int64_t idx = (rs + row) * U + u;
-            const float* g = G + (rs + row) * G4;
-#pragma unroll
-            for (int y = 0; y < 4; ++y) cg[r][y] = ok ? g[y * U + u] : 0.0f;
-            cct[r] = ok ? Cs[idx + (int64_t)B * U] : 0.0f;
-            ccp[r] = ok ? Cs[idx] : 0.0f;
-            cdh[r] = ok ? dHh[idx] : 0.0f;
-#pragma unroll
-            for (int a = 0; a < 4; ++a) cpv[r][a] = ok ? prev[(rs + row) * 4 + a] : 0.0f;
         }
     };
+    auto dwl_step = [&]() {   // dz_s is in Dz (rows >= B zero)
+        float dv[PR_ROWS / 4];
+#pragma unroll
+        for (int rq = 0; rq < PR_ROWS / 4; ++rq) dv[rq] = Dz[4 * rq + gq][i];
+        const int nrq = (B + 3) >> 2;
+        fence_begin(accw);
+#pragma unroll
+        for (int rq = 0; rq < PR_ROWS / 4; ++rq) {
+            if (rq < nrq) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) accw[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[q][rq], dv[rq], accw[q], 0, 0, 0);
+            }
+        }
+        fence_end(accw);
+    };
+    const int rb = wave & 1, cbo = wave >> 1;   // rows 16 rb.., unit blocks cbo, cbo + 2, .. (7 or 6 of 13)
+    const __amdgpu_buffer_rsrc_t rP = pr_rsrc(part, (int64_t)2 * PR_GRID * PB_PART);
+    // this lane's B operands over the launch: B[k][n] = Wr[n][y U + u0 + j] at k = 4 y + j = 4 q4 + gq
+    float bw[7][4];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        const int n = 16 * (cbo + 2 * q) + i;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) bw[q][q4] = n < U ? Wr[(int64_t)n * G4 + q4 * U + u0 + gq] : 0.0f;
+    }
+    for (int x = tid; x < PR_ROWS * (PR_COLS + 1); x += 256) (&Dz[0][0])[x] = 0.0f;
+    const bool pt = tid < 4 * B;
+    const int pr = tid >> 2, pj = tid & 3, pu = u0 + pj;
+    float dcs = 0.f;
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};   // dbl: this point's row, all steps, per gate
+    float qsum[4][4] = {};                    // Q = prev^T dz: [prev component][gate]
+    float cg[4], cct, ccp, cdh, cpv[4];
+    auto load_cell = [&](int s) {   // gates, c_t, c_{t-1}, dh from the head: written before the launch
+        const int64_t rs = (int64_t)s * B + (pt ? pr : 0);
+        const float* g = G + rs * G4 + pu;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) cg[y] = pt ? g[y * U] : 0.0f;
+        cct = pt ? Cs[(rs + B) * U + pu] : 0.0f;
+        ccp = pt ? Cs[rs * U + pu] : 0.0f;
+        cdh = pt ? dHh[rs * U + pu] : 0.0f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) cpv[a] = pt ? prev[rs * 4 + a] : 0.0f;
+    };
     load_cell(T - 1);
+    load_a(T - 1);
+    __syncthreads();   // Dz zeroed
+    const int nrg = (B + 3) >> 2, nl = PR_GRID * PR_UNITS * nrg;   // 16-B partial loads per step (4 rows each)
+    constexpr int NLD = (PR_GRID * PR_UNITS * (PR_ROWS / 4) + 255) / 256;
     uint32_t nsync = 0;
     for (int s = T - 1; s >= 0; --s) {
-        float dhn[4] = {0.f, 0.f, 0.f, 0.f};
-        if (s < T - 1 && act) {   // (1) dh_next: the 13 partials of step s+1, fixed order
-            const int64_t pb = (int64_t)((s + 1) & 1) * PR_GRID * PB_PART + (int64_t)u * PR_ROWS + 4 * r4;
-            rdg::f32x4 v[PR_GRID];
+        float dhn = 0.f;
+        if (s < T - 1) {   // (1) dh_next: the 50 partials of step s+1 for the local units, summed in workgroup order
+            const int64_t pb = (int64_t)((s + 1) & 1) * PR_GRID * PB_PART;
+            rdg::f32x4 v[NLD];
 #pragma unroll
-            for (int w = 0; w < PR_GRID; ++w) v[w] = pr_load4(rP, pb + (int64_t)w * PB_PART);
-            rdg::f32x4 acc = v[0];
+            for (int j = 0; j < NLD; ++j) {
+                const int x = min(tid + 256 * j, nl - 1), w = x / (PR_UNITS * nrg), rem = x - w * (PR_UNITS * nrg);
+                const int jj = rem / nrg, rg = rem - jj * nrg;
+                v[j] = 256 * j < nl ? pr_load4(rP, pb + (int64_t)w * PB_PART + (int64_t)(u0 + jj) * PR_ROWS + 4 * rg)
+                                    : rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+            }
 #pragma unroll
-            for (int w = 1; w < PR_GRID; ++w) acc += v[w];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dhn[r] = acc[r];
+            for (int j = 0; j < NLD; ++j) {
+                const int x = tid + 256 * j;
+                if (x < nl) {
+                    const int w = x / (PR_UNITS * nrg), rem = x - w * (PR_UNITS * nrg), jj = rem / nrg, rg = rem - jj * nrg;
+                    *reinterpret_cast<rdg::f32x4*>(&Dh[w][jj][4 * rg]) = v[j];
+                }
+            }
+            __syncthreads();
+            if (pt) {
+                float a = Dh[0][pj][pr];
+#pragma unroll 10
+                for (int w = 1; w < PR_GRID; ++w) a += Dh[w][pj][pr];
+                dhn = a;
+            }
         }
         // (2) TF1 LSTMCell backward (cell_bwd_kernel's arithmetic)
-        const int64_t rs = (int64_t)s * B;
-        if (act) {
+        if (pt) {
+            const float gi = cg[0], gj = cg[1], gf = cg[2], go = cg[3];
+            const float dh = s < T - 1 ? cdh + dhn : cdh;
+            const float tc = tanhf(cct);
+            const float dcv = fmaf(dh * go, fmaf(-tc, tc, 1.0f), dcs);
+            const float z0 = dcv * gj * gi * (1.0f - gi), z1 = dcv * gi * fmaf(-gj, gj, 1.0f);
+            const float z2 = dcv * ccp * gf * (1.0f - gf), z3 = dh * tc * go * (1.0f - go);
+            Dz[pr][pj] = z0; Dz[pr][4 + pj] = z1; Dz[pr][8 + pj] = z2; Dz[pr][12 + pj] = z3;
+            bsum[0] += z0; bsum[1] += z1; bsum[2] += z2; bsum[3] += z3;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 4 * r4 + r;
-                if (row >= B) continue;
-                const float gi = cg[r][0], gj = cg[r][1], gf = cg[r][2], go = cg[r][3];
-                const float dh = s < T - 1 ? cdh[r] + dhn[r] : cdh[r];
-                const float tc = tanhf(cct[r]);
-                const float dcv = fmaf(dh * go, fmaf(-tc, tc, 1.0f), dcs[r]);
-                const float z0 = dcv * gj * gi * (1.0f - gi), z1 = dcv * gi * fmaf(-gj, gj, 1.0f);
-                const float z2 = dcv * ccp[r] * gf * (1.0f - gf), z3 = dh * tc * go * (1.0f - go);
-                float* dz = dZ + (rs + row) * G4;
-                dz[u] = z0; dz[U + u] = z1; dz[2 * U + u] = z2; dz[3 * U + u] = z3;
-                As[c][row] = z0; As[16 + c][row] = z1; As[32 + c][row] = z2; As[48 + c][row] = z3;
-                bsum[0] += z0; bsum[1] += z1; bsum[2] += z2; bsum[3] += z3;
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    qsum[a][0] = fmaf(cpv[r][a], z0, qsum[a][0]);
-                    qsum[a][1] = fmaf(cpv[r][a], z1, qsum[a][1]);
-                    qsum[a][2] = fmaf(cpv[r][a], z2, qsum[a][2]);
-                    qsum[a][3] = fmaf(cpv[r][a], z3, qsum[a][3]);
-                }
-                dcs[r] = dcv * gf;
+            for (int a = 0; a < 4; ++a) {
+                qsum[a][0] = fmaf(cpv[a], z0, qsum[a][0]);
+                qsum[a][1] = fmaf(cpv[a], z1, qsum[a][1]);
+                qsum[a][2] = fmaf(cpv[a], z2, qsum[a][2]);
+                qsum[a][3] = fmaf(cpv[a], z3, qsum[a][3]);
             }
+            dcs = dcv * gf;
         }
         if (s == 0) break;
         load_cell(s - 1);
         __syncthreads();
-        // (3) partial dh_{s-1}[row][n] over the local columns, for every unit n
+        // (3) partial dh_{s-1}[row][n] over the 16 local columns, for every unit n
         rdg::f32x4 acc[7];
 #pragma unroll
         for (int q = 0; q < 7; ++q) acc[q] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
         {
+            float av[4];
 #pragma unroll
-            for (int kq = 0; kq < 16; ++kq) {
-                const int kk = 4 * kq + gq;
-                const float a = As[kk][16 * rb + i];
+            for (int q4 = 0; q4 < 4; ++q4) av[q4] = Dz[16 * rb + i][4 * q4 + gq];
 #pragma unroll
-                for (int q = 0; q < 7; ++q)
-                    if (q < ncb) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Wb[kk][16 * (cb0 + q) + i], acc[q], 0, 0, 0);
+            for (int q4 = 0; q4 < 4; ++q4) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q4], bw[q][q4], acc[q], 0, 0, 0);
+                if (cbo == 0) acc[6] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q4], bw[6][q4], acc[6], 0, 0, 0);
             }
         }
         const int64_t po = (int64_t)(s & 1) * PR_GRID * PB_PART + (int64_t)blockIdx.x * PB_PART;
 #pragma unroll
-        for (int q = 0; q < 7; ++q) {   // lane (i, gq): rows 16 rb + 4 gq .. +3 of unit 16 (cb0 + q) + i
-            if (q < ncb)
+        for (int q = 0; q < 7; ++q) {   // lane (i, gq): rows 16 rb + 4 gq .. +3 of unit 16 (cbo + 2 q) + i
+            if (q < 6 || cbo == 0)
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[q]), rP,
-                                                       (int)((po + (int64_t)(16 * (cb0 + q) + i) * PR_ROWS + 16 * rb + 4 * gq) * 4),
+                                                       (int)((po + (int64_t)(16 * (cbo + 2 * q) + i) * PR_ROWS + 16 * rb + 4 * gq) * 4),
                                                        0, 16);
         }
-        __syncthreads();   // As is rewritten by the next step's cell
-        if (!pr_grid_sync(bar + 1, ++nsync * gridDim.x, bar + 2)) return;
+        // arrive (every wave's sc1 partial stores drained first), then (4) while the others arrive
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dwl_step();
+        load_a(s - 1);
+        if (tid == 0) {
+            const uint32_t target = ++nsync * gridDim.x;
+            int ok = 1;
+            for (uint32_t spins = 0; __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+                if (++spins > PR_SPIN_LIMIT) {
+                    __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            ok_s = ok;
+        }
+        __syncthreads();   // Dz and Dh are rewritten by the next step
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
+        if (!ok_s) return;
     }
-    // dbl (the gate bias gradient) and Q = prev^T dz of the local columns: the 8 row groups'
-    // sums, in order (As[col][8 j + r4] holds sum j of row group r4)
+    __syncthreads();   // dz_0 in Dz
+    dwl_step();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // C: rows k = 16 (w + 4 q) + 4 gq + r, local column i
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = 16 * (wave + 4 * q) + 4 * gq + r;
+            if (k < XI + U) dWl[(int64_t)k * G4 + (i >> 2) * U + u0 + (i & 3)] = accw[q][r];
+        }
+    }
+    // dbl (the gate bias gradient) and Q = prev^T dz of the local columns: the points' sums, in row order
     __syncthreads();
-    if (tid < 128) {
+    if (pt) {
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
-            As[16 * y + c][r4] = bsum[y];
+            red[pr][pj][y] = bsum[y];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) As[16 * y + c][8 * (a + 1) + r4] = qsum[a][y];
+            for (int a = 0; a < 4; ++a) red[pr][pj][4 + 4 * a + y] = qsum[a][y];
         }
     }
     __syncthreads();
-    for (int o = tid; o < 64 * 5; o += 256) {
-        const int col = o & 63, j = o >> 6, y = col >> 4, uu = u0 + (col & 15);
+    for (int o = tid; o < PR_UNITS * PB_RED; o += 256) {
+        const int jj = o / PB_RED, e = o - jj * PB_RED, uu = u0 + jj;
         float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v += As[col][8 * j + k];
-        if (uu < U) {
-            if (j == 0) dbl[y * U + uu] = v;
-            else Q[(j - 1) * G4 + y * U + uu] = v;
-        }
+        for (int r = 0; r < B; ++r) v += red[r][jj][e];
+        if (e < 4) dbl[e * U + uu] = v;
+        else Q[((e - 4) >> 2) * G4 + ((e - 4) & 3) * U + uu] = v;
     }
 }
 
@@ -699,10 +796,30 @@ __device__ __forceinline__ void head_stage(const float* __restrict__ src, int ld
     }
 }
 
-// workgroup (t, rb) of the grid T x nb: rows t B + 16 rb .. of step t, with step t's head
+// workgroup (t, rb) of the grid T x nb: rows t B + 16 rb .. of step t, with step t's head.
+// WL (grids of at most HB_WIDE_GRID workgroups, e.g. the reference's 20 windows): the head's
+// 31,652 parameters are copied into LDS first (LDS-DMA, one issue burst beside the row
+// staging), so the five layers read their B operands from LDS instead of paying an L2/HBM
+// round trip each (round 5); same values, same MFMA order.  Larger grids stream them from L2
+// (124 KB of LDS would leave one workgroup per CU).
+constexpr int HB_WIDE_GRID = 256;   // at most this many one-tile workgroups: the latency-bound forms
+static_assert(HSZ % 4 == 0 && (OFF_H % 4) == 0, "16-B pieces of a head's parameters");
+// step t's head -> W (16-B LDS-DMA pieces, lane l of a wave's burst to base + 16 l); the caller
+// waits (vmcnt) before its barrier
+__device__ __forceinline__ void head_params_to_lds(const float* __restrict__ P, float* W) {
+    constexpr int V4 = HSZ / 4, PER = (V4 + 255) / 256;
+    const int wbase = threadIdx.x & ~63;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int x = threadIdx.x + 256 * u;
+        if (x < V4) __builtin_amdgcn_global_load_lds(P + 4 * x, W + 4 * (wbase + 256 * u), 16, 0, 0);
+    }
+}
+template <bool WL>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
                                                        float* A1, float* A2, float* A3, float* A4, float* Y, int64_t B,
                                                        int nb) {
+    __shared__ __attribute__((aligned(16))) float Wl[WL ? HSZ : 4];
     __shared__ __attribute__((aligned(16))) float X0[HF_ROWS][U + 4];
     __shared__ __attribute__((aligned(16))) float X1[HF_ROWS][L1];
     __shared__ __attribute__((aligned(16))) float X2[HF_ROWS][L2];
@@ -711,14 +828,17 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
     __shared__ __attribute__((aligned(16))) float X5[HF_ROWS][8];
     const int ts = blockIdx.x / nb, rb = blockIdx.x - ts * nb;
     const int64_t row0 = (int64_t)ts * B + (int64_t)rb * HF_ROWS, R = (int64_t)(ts + 1) * B;
-    const float* P = P0 + OFF_H + (int64_t)ts * HSZ;   // step ts's head
+    const float* P = P0 + OFF_H + (int64_t)ts * HSZ;
+    if constexpr (WL) head_params_to_lds(P, Wl);
     head_stage<U, U + 4>(Hc, U, row0, R, X0, threadIdx.x);
+    if constexpr (WL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of Wl have landed
     __syncthreads();
-    head_layer<U, H1, true>(X0, X1, P + OFF_W1, P + OFF_B1, A1, L1, row0, R);
-    head_layer<H1, H2, true>(X1, X2, P + OFF_W2, P + OFF_B2, A2, L2, row0, R);
-    head_layer<H2, H3, true>(X2, X3, P + OFF_W3, P + OFF_B3, A3, L3, row0, R);
-    head_layer<H3, H4, true>(X3, X4, P + OFF_W4, P + OFF_B4, A4, L4, row0, R);
-    head_layer<H4, 4, false>(X4, X5, P + OFF_W5, P + OFF_B5, Y, 4, row0, R);
+    const float* W = WL ? (const float*)Wl : P;
+    head_layer<U, H1, true>(X0, X1, W + OFF_W1, W + OFF_B1, A1, L1, row0, R);
+    head_layer<H1, H2, true>(X1, X2, W + OFF_W2, W + OFF_B2, A2, L2, row0, R);
+    head_layer<H2, H3, true>(X2, X3, W + OFF_W3, W + OFF_B3, A3, L3, row0, R);
+    head_layer<H3, H4, true>(X3, X4, W + OFF_W4, W + OFF_B4, A4, L4, row0, R);
+    head_layer<H4, 4, false>(X4, X5, W + OFF_W5, W + OFF_B5, Y, 4, row0, R);
 }
 
 // Head backward for the same small batches: per 16-row workgroup the data gradients down the
@@ -734,23 +854,40 @@ template <int KO, int NI, bool DT, int NW, int LD, int LI, int LA, class WF>
 __device__ __forceinline__ void head_dgrad_f(const float (*dout)[LD], float (*din)[LI], const float (*act)[LA], WF wf,
                                              float* gout, int ldg, int64_t row0, int64_t R, int tid) {
     const int wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
-    constexpr int NB = (NI + 15) / 16;
+    constexpr int NB = (NI + 15) / 16, IT = (NB + NW - 1) / NW;
+    // the chains' operands: dout's (shared by every column block) and this lane's weights, all
+    // loads issued before the first MFMA; the chains interleave (one accumulator per block)
+    float av[KO / 4], bv[IT][KO / 4];
 #pragma unroll
-    for (int it = 0; it < (NB + NW - 1) / NW; ++it) {   // unrolled: every weight load of the layer in flight at once
+    for (int kq = 0; kq < KO / 4; ++kq) av[kq] = dout[i][4 * kq + gq];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int col = 16 * (wave + NW * it) + i;
+        const bool cv = wave + NW * it < NB && col < NI;
+#pragma unroll
+        for (int kq = 0; kq < KO / 4; ++kq) bv[it][kq] = wf(it, kq, cv, col, 4 * kq + gq);
+    }
+    rdg::f32x4 acc[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) acc[it] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
+    fence_begin(acc);
+#pragma unroll
+    for (int kq = 0; kq < KO / 4; ++kq) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+            if (wave + NW * it < NB) acc[it] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kq], bv[it][kq], acc[it], 0, 0, 0);
+    }
+    fence_end(acc);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
         const int cb = wave + NW * it;
         if (cb >= NB) break;
         const int col = 16 * cb + i;
         const bool cv = col < NI;
-        rdg::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kq = 0; kq < KO / 4; ++kq) {
-            const int k = 4 * kq + gq;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dout[i][k], wf(it, kq, cv, col, k), acc, 0, 0, 0);
-        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = 4 * gq + r;
-            float v = acc[r];
+            float v = acc[it][r];
             if (DT) {
                 const float a = act[row][col < NI ? col : 0];
                 v *= fmaf(-a, a, 1.0f);
@@ -789,11 +926,11 @@ struct HeadW {
 };
 // part[m][n] = sum over the 16 rows of act[row][m] d[row][n], m < M (the last input row is the
 // ones column: the bias gradient), n < N (one tile of rows: head_bwd_kernel<false>)
-template <int M, int N, int LA, int LD>
+template <int M, int N, int NW, int LA, int LD>
 __device__ __forceinline__ void head_wgrad(const float (*act)[LA], const float (*d)[LD], float* __restrict__ part) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     constexpr int MB = (M + 15) / 16, NB = (N + 15) / 16;
-    for (int t = wave; t < MB * NB; t += 4) {
+    for (int t = wave; t < MB * NB; t += NW) {
         const int m0 = 16 * (t / NB), n0 = 16 * (t % NB);
         const int mc = m0 + i < M ? m0 + i : M - 1, nc = n0 + i < N ? n0 + i : N - 1;
         rdg::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -852,9 +989,11 @@ __device__ __forceinline__ void head_wgrad_store(const rdg::f32x4 (&acc)[wq<M, N
 }
 
 // MT: tpb tiles per workgroup with the weight-gradient accumulators in registers over all of them
-// (eight waves share them), for large batches; else one tile, four waves, 64 VGPRs
-template <bool MT>
-__global__ __launch_bounds__(MT ? 512 : 256) void head_bwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
+// (eight waves share them), for large batches; else one tile per workgroup, NWV waves: sixteen
+// when the whole grid is one wave of workgroups (e.g. the reference's 20 windows: 20
+// workgroups on 256 CUs, latency bound -- round 5), else four
+template <bool MT, int NWV>
+__global__ __launch_bounds__(64 * NWV) void head_bwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
                                                        const float* __restrict__ A1, const float* __restrict__ A2,
                                                        const float* __restrict__ A3, const float* __restrict__ A4,
                                                        const float* __restrict__ dY, float* __restrict__ dHh,
@@ -875,7 +1014,8 @@ __global__ __launch_bounds__(MT ? 512 : 256) void head_bwd_kernel(const float* _
     const int64_t R = (int64_t)(ts + 1) * B;
     const float* P = P0 + OFF_H + (int64_t)ts * HSZ;
     float* pw = part + (int64_t)blockIdx.x * HB_PART;
-    constexpr int NW = MT ? 8 : 4, NT = 64 * NW;   // MT: eight waves share the accumulators
+    constexpr int NW = NWV, NT = 64 * NW;   // MT: eight waves share the accumulators
+    static_assert(!MT || NW == 8, "the MT form runs eight waves");
     rdg::f32x4 a1[wq<U + 1, H1, NW>()], a2[wq<H1 + 1, H2, NW>()], a3[wq<H2 + 1, H3, NW>()],
         a4[wq<H3 + 1, H4, NW>()], a5[wq<H4 + 1, 4, NW>()];
 #define RDL_ZERO(a) _Pragma("unroll") for (auto& x : a) x = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
@@ -941,11 +1081,11 @@ __global__ __launch_bounds__(MT ? 512 : 256) void head_bwd_kernel(const float* _
             head_wgrad_acc<H4 + 1, 4, NW>(X4, D5, a5, tid);
             __syncthreads();   // the next tile restages the LDS rows
         } else {              // one tile: each layer's partial stored at once
-            head_wgrad<U + 1, H1>(X0, D1, pw);
-            head_wgrad<H1 + 1, H2>(X1, D2, pw + (OFF_W2 - OFF_W1));
-            head_wgrad<H2 + 1, H3>(X2, D3, pw + (OFF_W3 - OFF_W1));
-            head_wgrad<H3 + 1, H4>(X3, D4, pw + (OFF_W4 - OFF_W1));
-            head_wgrad<H4 + 1, 4>(X4, D5, pw + (OFF_W5 - OFF_W1));
+            head_wgrad<U + 1, H1, NW>(X0, D1, pw);
+            head_wgrad<H1 + 1, H2, NW>(X1, D2, pw + (OFF_W2 - OFF_W1));
+            head_wgrad<H2 + 1, H3, NW>(X2, D3, pw + (OFF_W3 - OFF_W1));
+            head_wgrad<H3 + 1, H4, NW>(X3, D4, pw + (OFF_W4 - OFF_W1));
+            head_wgrad<H4 + 1, 4, NW>(X4, D5, pw + (OFF_W5 - OFF_W1));
         }
     }
     if constexpr (MT) {
@@ -1264,16 +1404,16 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     const int64_t R = (int64_t)T * B;
     const float* P = t->params;
     t->last_B = B;
-    hipLaunchKernelGGL(inputs_kernel, dim3((unsigned)((R * XLD + 255) / 256)), dim3(256), 0, t->stream, ob, prev, P,
-                       t->X, R, B, train ? t->cfg.keep_prob : 1.0f, t->cfg.seed, t->cfg.row_base,
-                       (const uint32_t*)t->ctl, t->bar);
-    RDL_CK(hipGetLastError(), "rdl inputs_kernel");
-    if (persistent(t, B)) {   // Zx, then all T recurrent steps in one launch (it writes the step-0 state rows)
-        RDL_CK(mm(t, (int)R, G4, XI, t->X, XLD, 0, P + OFF_WL, G4, 0, t->Z, G4, P + OFF_BL), "rdl gemm Zx");
-        hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
-                           (const float*)t->Z, state0, t->G, t->Cs, t->H, (int)B, T, t->bar, t->hx);
+    const float kp = train ? t->cfg.keep_prob : 1.0f;
+    if (persistent(t, B)) {   // X, Zx and all T recurrent steps in one launch (it writes the step-0 state rows)
+        hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P, ob, prev, t->X, state0,
+                           t->G, t->Cs, t->H, (int)B, T, kp, t->cfg.seed, t->cfg.row_base, (const uint32_t*)t->ctl,
+                           t->bar, t->hx);
         RDL_CK(hipGetLastError(), "rdl lstm_fwd_persist_kernel");
     } else {
+    hipLaunchKernelGGL(inputs_kernel, dim3((unsigned)((R * XLD + 255) / 256)), dim3(256), 0, t->stream, ob, prev, P,
+                       t->X, R, B, kp, t->cfg.seed, t->cfg.row_base, (const uint32_t*)t->ctl);
+    RDL_CK(hipGetLastError(), "rdl inputs_kernel");
     if (state0) {
         RDL_CK(hipMemcpyAsync(t->Cs, state0, sizeof(float) * B * U, hipMemcpyDeviceToDevice, t->stream), "rdl state");
         RDL_CK(hipMemcpyAsync(t->H, state0 + B * U, sizeof(float) * B * U, hipMemcpyDeviceToDevice, t->stream),
@@ -1297,7 +1437,8 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     const float* Hc = t->H + B * U;
     if (fused_head(t, R)) {
         const int nb = (int)((B + HF_ROWS - 1) / HF_ROWS);
-        hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)(T * nb)), dim3(256), 0, t->stream, Hc, P, t->A1, t->A2,
+        auto* kern = (int64_t)T * nb <= HB_WIDE_GRID ? head_fwd_kernel<true> : head_fwd_kernel<false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(T * nb)), dim3(256), 0, t->stream, Hc, P, t->A1, t->A2,
                            t->A3, t->A4, out_pdflat, B, nb);
         RDL_CK(hipGetLastError(), "rdl head_fwd_kernel");
         return RD_OK;
@@ -1340,8 +1481,9 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     const float* Hc = t->H + B * U;
     if (fused_head(t, R)) {   // the heads' backward as two launches (head_bwd_kernel + fixed-order reduce)
         const int nb = head_nb(T, B), tpb = head_tpb(T, B);
-        hipLaunchKernelGGL(tpb > 1 ? head_bwd_kernel<true> : head_bwd_kernel<false>, dim3((unsigned)(T * nb)),
-                           dim3(tpb > 1 ? 512 : 256), 0, t->stream, Hc, P,
+        const bool wide = tpb == 1 && (int64_t)T * nb <= HB_WIDE_GRID;
+        auto* kern = tpb > 1 ? head_bwd_kernel<true, 8> : wide ? head_bwd_kernel<false, 16> : head_bwd_kernel<false, 4>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(T * nb)), dim3(tpb > 1 ? 512 : wide ? 1024 : 256), 0, t->stream, Hc, P,
                            (const float*)t->A1, (const float*)t->A2, (const float*)t->A3, (const float*)t->A4,
                            (const float*)t->dY, t->dHh, t->hpart, B, nb, tpb);
         RDL_CK(hipGetLastError(), "rdl head_bwd_kernel");
@@ -1382,7 +1524,8 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     float* dZl = t->Z;
     if (persistent(t, B)) {
         hipLaunchKernelGGL(lstm_bptt_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P + OFF_WL + XI * G4,
-                           (const float*)t->dHh, (const float*)t->G, (const float*)t->Cs, dZl, t->bpart, g + OFF_BL,
+                           (const float*)t->dHh, (const float*)t->G, (const float*)t->Cs, (const float*)t->X,
+                           (const float*)t->H, g + OFF_WL, t->bpart, g + OFF_BL,
                            prev, t->qbuf, (int)B, T, t->bar);
         RDL_CK(hipGetLastError(), "rdl lstm_bptt_persist_kernel");
     } else {
@@ -1411,10 +1554,12 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
         RDL_CK(rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus), "rdl gemm dh + cell");
     }
     }
-    // LSTM weights: dWl = [x | h_prev]^T dz over all rows; dbl; then dp -> dWp, dbp
-    RDL_CK(mm2(t, ga(XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4),
-               ga(U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4)),
-           "rdl dWl x | h");
+    // LSTM weights: dWl = [x | h_prev]^T dz over all rows (in the persistent BPTT for small
+    // batches); dbl; then dp -> dWp, dbp
+    if (!persistent(t, B))
+        RDL_CK(mm2(t, ga(XI, G4, Ri, t->X, XLD, 1, dZl, G4, 0, g + OFF_WL, G4),
+                   ga(U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4)),
+               "rdl dWl x | h");
     if (!persistent(t, B)) RDL_CK(colsum(t, dZl, R, G4, G4, g + OFF_BL), "rdl dbl");   // else summed in BPTT
     if (persistent(t, B)) {   // from the BPTT kernel's dbl and Q = prev^T dz: one launch
         hipLaunchKernelGGL(dense32_grad_kernel, dim3(160), dim3(256), 0, t->stream, P, (const float*)t->qbuf, g);
