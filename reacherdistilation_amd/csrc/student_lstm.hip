@@ -711,31 +711,6 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
     }
 }
 
-// dWp = Q . Wl[11:43]^T and dbp = Wl[11:43] . dbl: the input-side dense32 layer's gradients
-// (student_nn.py:26) from the BPTT kernel's gate sums, without materialising dP = dZ . Wl^T
-// (the same sums in another order: sum over the rows first, then over the 800 gate columns)
-__global__ __launch_bounds__(256) void dense32_grad_kernel(const float* __restrict__ P, const float* __restrict__ Q,
-                                                           float* __restrict__ g) {
-    // block o: 0..127 dWp[a][c] (a = o / 32), 128..159 dbp[c]; a fixed-order tree over 256 threads
-    __shared__ float red[256];
-    const int o = blockIdx.x, c = o & 31;
-    const float* w = P + OFF_WL + (int64_t)(11 + c) * G4;
-    const float* q = o < 128 ? Q + (o >> 5) * G4 : g + OFF_BL;
-    float v = 0.f;
-#pragma unroll
-    for (int j = 0; j < (G4 + 255) / 256; ++j) {
-        const int k = threadIdx.x + 256 * j;
-        if (k < G4) v = fmaf(w[k], q[k], v);
-    }
-    red[threadIdx.x] = v;
-    __syncthreads();
-    for (int h = 128; h > 0; h >>= 1) {
-        if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) g[(o < 128 ? OFF_WP : OFF_BP - 128) + o] = red[0];
-}
-
 // ---------------------------------------------------------------- fused head (small batches)
 // The head 200-64-128-64-32-4 (student_nn.py:42-46) over a few hundred rows is five launches of
 // ~10 us each, none of them busy.  head_fwd_kernel runs all five layers for 16 rows per
@@ -815,10 +790,41 @@ __device__ __forceinline__ void head_params_to_lds(const float* __restrict__ P, 
         if (x < V4) __builtin_amdgcn_global_load_lds(P + 4 * x, W + 4 * (wbase + 256 * u), 16, 0, 0);
     }
 }
+// The loss of a training forward (small batches; loss_kernel's per-row arithmetic) at the end
+// of head_fwd_kernel: dY of the workgroup's rows and its loss / squared-error sums; the metrics
+// (their sum in workgroup order) are formed by grad_finish_kernel after BPTT.
+struct HeadLoss {
+    const float* tgt;   // null: no loss (inference forward)
+    float* dY;
+    float* part;        // [grid][2] partial sums
+    float inv_n;
+    int loss;
+};
+__device__ __forceinline__ float2 row_loss(const float* o, const float* t, int loss, float inv_n, float* d) {
+    const float e0 = o[0] - t[0], e1 = o[1] - t[1];
+    const float sq = fmaf(e0, e0, e1 * e1);
+    float lv, d0, d1, d2 = 0.f, d3 = 0.f;
+    if (loss == RDL_LOSS_MSE) {
+        d0 = e0 * inv_n;
+        d1 = e1 * inv_n;
+        lv = 0.5f * inv_n * sq;
+    } else {
+        const float ivt0 = expf(-2.0f * t[2]), ivt1 = expf(-2.0f * t[3]);
+        const float vs0 = expf(2.0f * o[2]), vs1 = expf(2.0f * o[3]);
+        lv = ((t[2] - o[2]) + 0.5f * (vs0 + e0 * e0) * ivt0 - 0.5f) +
+             ((t[3] - o[3]) + 0.5f * (vs1 + e1 * e1) * ivt1 - 0.5f);
+        d0 = e0 * ivt0;
+        d1 = e1 * ivt1;
+        d2 = fmaf(vs0, ivt0, -1.0f);
+        d3 = fmaf(vs1, ivt1, -1.0f);
+    }
+    d[0] = d0; d[1] = d1; d[2] = d2; d[3] = d3;
+    return make_float2(lv, sq);
+}
 template <bool WL>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ Hc, const float* __restrict__ P0,
                                                        float* A1, float* A2, float* A3, float* A4, float* Y, int64_t B,
-                                                       int nb) {
+                                                       int nb, HeadLoss hl) {
     __shared__ __attribute__((aligned(16))) float Wl[WL ? HSZ : 4];
     __shared__ __attribute__((aligned(16))) float X0[HF_ROWS][U + 4];
     __shared__ __attribute__((aligned(16))) float X1[HF_ROWS][L1];
@@ -839,6 +845,27 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
     head_layer<H2, H3, true>(X2, X3, W + OFF_W3, W + OFF_B3, A3, L3, row0, R);
     head_layer<H3, H4, true>(X3, X4, W + OFF_W4, W + OFF_B4, A4, L4, row0, R);
     head_layer<H4, 4, false>(X4, X5, W + OFF_W5, W + OFF_B5, Y, 4, row0, R);
+    if (!hl.tgt) return;   // (uniform) inference forward
+    __shared__ float ls[HF_ROWS][2];
+    const int tid = threadIdx.x;
+    if (tid < HF_ROWS) {   // X5 holds the layer's output rows (head_layer ends with a barrier)
+        float2 v = make_float2(0.f, 0.f);
+        if (row0 + tid < R) {
+            float o[4] = {X5[tid][0], X5[tid][1], X5[tid][2], X5[tid][3]};
+            float d[4];
+            v = row_loss(o, hl.tgt + (row0 + tid) * 4, hl.loss, hl.inv_n, d);
+            *reinterpret_cast<rdg::f32x4*>(hl.dY + (row0 + tid) * 4) = rdg::f32x4{d[0], d[1], d[2], d[3]};
+        }
+        ls[tid][0] = v.x;
+        ls[tid][1] = v.y;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float a = 0.f, b = 0.f;
+        for (int r = 0; r < HF_ROWS; ++r) { a += ls[r][0]; b += ls[r][1]; }
+        hl.part[2 * blockIdx.x] = a;
+        hl.part[2 * blockIdx.x + 1] = b;
+    }
 }
 
 // Head backward for the same small batches: per 16-row workgroup the data gradients down the
@@ -1097,13 +1124,12 @@ __global__ __launch_bounds__(64 * NWV) void head_bwd_kernel(const float* __restr
     }
 }
 
-// head t's gradient (blockIdx.y = t): grad[OFF_H + t HSZ + p] = sum over step t's nb
-// workgroups' partial rows, in row order
-__global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part, int nb,
-                                                                float* __restrict__ g) {
-    const int p = blockIdx.x * 256 + threadIdx.x;
+// One launch for the gradient's last pieces (small batches, after BPTT): blocks < T HB_BLK run
+// head_wgrad_reduce_kernel's sums, the next 160 (dense) dense32_grad_kernel's dot products.
+constexpr int HB_BLK = (HB_PART + 255) / 256;
+__device__ __forceinline__ void head_part_sum(const float* __restrict__ part, int nb, float* __restrict__ g, int t, int p) {
     if (p >= HB_PART) return;
-    const float* q = part + (int64_t)blockIdx.y * nb * HB_PART + p;
+    const float* q = part + (int64_t)t * nb * HB_PART + p;
     float a = 0.f, b = 0.f;
     int w = 0;
     for (; w + 1 < nb; w += 2) {
@@ -1111,7 +1137,69 @@ __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __r
         b += q[(int64_t)(w + 1) * HB_PART];
     }
     if (w < nb) a += q[(int64_t)w * HB_PART];
-    g[OFF_H + (int64_t)blockIdx.y * HSZ + p] = a + b;
+    g[OFF_H + (int64_t)t * HSZ + p] = a + b;
+}
+// dWp = Q . Wl[11:43]^T and dbp = Wl[11:43] . dbl: the input-side dense32 layer's gradients
+// (student_nn.py:26) from the BPTT kernel's gate sums, without materialising dP = dZ . Wl^T
+// (the same sums in another order: sum over the rows first, then over the 800 gate columns)
+__device__ __forceinline__ void dense32_dot(const float* __restrict__ P, const float* __restrict__ Q, float* __restrict__ g,
+                                            int o) {
+    // o: 0..127 dWp[a][c] (a = o / 32), 128..159 dbp[c]; a fixed-order tree over 256 threads
+    __shared__ float red[256];
+    const int c = o & 31;
+    const float* w = P + OFF_WL + (int64_t)(11 + c) * G4;
+    const float* q = o < 128 ? Q + (o >> 5) * G4 : g + OFF_BL;
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < (G4 + 255) / 256; ++j) {
+        const int k = threadIdx.x + 256 * j;
+        if (k < G4) v = fmaf(w[k], q[k], v);
+    }
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) g[(o < 128 ? OFF_WP : OFF_BP - 128) + o] = red[0];
+}
+// The last block: the metrics of the step from head_fwd_kernel's loss partials (lpart, nl
+// workgroups, summed in workgroup order) into the ring slot, and the step words' snapshot for
+// the Adam kernel (loss_kernel's job on the other paths).
+__global__ __launch_bounds__(256) void grad_finish_kernel(const float* __restrict__ part, int nb, int T,
+                                                          const float* __restrict__ P, const float* __restrict__ Q,
+                                                          float* __restrict__ g, const float* __restrict__ lpart, int nl,
+                                                          float rows, uint32_t* ctl, float* hist, int hist_len) {
+    const int b = blockIdx.x;
+    if (b < T * HB_BLK) {
+        head_part_sum(part, nb, g, b / HB_BLK, (b % HB_BLK) * 256 + threadIdx.x);
+    } else if (b < T * HB_BLK + 160) {
+        dense32_dot(P, Q, g, b - T * HB_BLK);   // (uniform per block)
+    } else if (threadIdx.x == 0) {
+        float a = 0.f, c = 0.f;
+        for (int w = 0; w < nl; ++w) {
+            a += lpart[2 * w];
+            c += lpart[2 * w + 1];
+        }
+        float* h = hist + (int64_t)(ctl[0] % (uint32_t)hist_len) * N_MET;
+        h[0] = a;
+        h[1] = c;
+        h[2] = rows;
+        h[3] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ctl[4 + k] = ctl[k];
+    }
+}
+
+// head t's gradient (blockIdx.y = t): grad[OFF_H + t HSZ + p] = sum over step t's nb
+// workgroups' partial rows, in row order
+__global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part, int nb,
+                                                                float* __restrict__ g) {
+    head_part_sum(part, nb, g, blockIdx.y, blockIdx.x * 256 + threadIdx.x);
+}
+__global__ __launch_bounds__(256) void dense32_grad_kernel(const float* __restrict__ P, const float* __restrict__ Q,
+                                                           float* __restrict__ g) {
+    dense32_dot(P, Q, g, blockIdx.x);
 }
 
 // BPTT through one cell (dh = dh_head + dh_next; dc carried in place).  The fused backward
@@ -1314,7 +1402,9 @@ struct rdl_trainer {
     float* hpart = nullptr;    // fused head backward: one partial row of HB_PART per workgroup (head_nb)
     int64_t colws_floats = 0;
     uint32_t* ctl = nullptr;
-    uint32_t* bar = nullptr;   // persistent kernels: [0] forward / [1] BPTT barrier arrivals, [2] timeout flag
+    bool loss_in_head = false;   // the last forward computed the loss (head_fwd_kernel<true>)
+    uint32_t* bar = nullptr;   // persistent kernels: [0] forward / [1] BPTT barrier arrivals, [2] timeout flag,
+                               // [3] granule generation
     float* bpart = nullptr;                // persistent BPTT: per-step-parity partial dh of every workgroup
     unsigned long long* hx = nullptr;      // persistent forward: per-step-parity h granules
     float* qbuf = nullptr;     // persistent BPTT: Q = prev^T dz [4][800]
@@ -1398,12 +1488,15 @@ bool persistent(const rdl_trainer* t, int64_t B) {
 
 // forward over all T steps of B windows.  out_pdflat: where the head's output goes (the
 // internal Y when training).
+// tgt (training): the loss rides in the head forward where that runs as one wide-grid launch
+// (t->loss_in_head tells run_backward)
 int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float* state0, int64_t B, float* out_pdflat,
-                bool train) {
+                bool train, const float* tgt = nullptr, int64_t B_global = 0) {
     const int T = t->T;
     const int64_t R = (int64_t)T * B;
     const float* P = t->params;
     t->last_B = B;
+    t->loss_in_head = false;
     const float kp = train ? t->cfg.keep_prob : 1.0f;
     if (persistent(t, B)) {   // X, Zx and all T recurrent steps in one launch (it writes the step-0 state rows)
         hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P, ob, prev, t->X, state0,
@@ -1437,9 +1530,15 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     const float* Hc = t->H + B * U;
     if (fused_head(t, R)) {
         const int nb = (int)((B + HF_ROWS - 1) / HF_ROWS);
-        auto* kern = (int64_t)T * nb <= HB_WIDE_GRID ? head_fwd_kernel<true> : head_fwd_kernel<false>;
+        const bool wl = (int64_t)T * nb <= HB_WIDE_GRID;
+        HeadLoss hl{};
+        if (wl && tgt && persistent(t, B)) {   // grad_finish_kernel forms the metrics
+            hl = HeadLoss{tgt, t->dY, t->lpart, 1.0f / ((float)T * (float)B_global), t->cfg.loss};
+            t->loss_in_head = true;
+        }
+        auto* kern = wl ? head_fwd_kernel<true> : head_fwd_kernel<false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)(T * nb)), dim3(256), 0, t->stream, Hc, P, t->A1, t->A2,
-                           t->A3, t->A4, out_pdflat, B, nb);
+                           t->A3, t->A4, out_pdflat, B, nb, hl);
         RDL_CK(hipGetLastError(), "rdl head_fwd_kernel");
         return RD_OK;
     }
@@ -1469,6 +1568,7 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
     float* g = t->grad;
     const int lblk = (int)((R + LOSS_BLOCK - 1) / LOSS_BLOCK);
     const bool fold = lblk == 1;   // a single loss block writes the metrics itself
+    if (!t->loss_in_head) {   // else the head forward formed dY and the metrics
     hipLaunchKernelGGL(loss_kernel, dim3(lblk), dim3(LOSS_BLOCK), 0, t->stream, (const float*)t->Y, tgt, t->dY, R,
                        t->cfg.loss, 1.0f / ((float)T * (float)B_global), t->lpart, t->ctl, fold ? t->hist : nullptr,
                        t->cfg.metrics_len);
@@ -1478,7 +1578,10 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
                            t->ctl, t->hist, t->cfg.metrics_len);
         RDL_CK(hipGetLastError(), "rdl metrics_kernel");
     }
+    }
     const float* Hc = t->H + B * U;
+    // small batches: the head rows' sums, the dense32 gradient and the metrics as one launch after BPTT
+    const bool finish = t->loss_in_head;
     if (fused_head(t, R)) {   // the heads' backward as two launches (head_bwd_kernel + fixed-order reduce)
         const int nb = head_nb(T, B), tpb = head_tpb(T, B);
         const bool wide = tpb == 1 && (int64_t)T * nb <= HB_WIDE_GRID;
@@ -1487,9 +1590,11 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
                            (const float*)t->A1, (const float*)t->A2, (const float*)t->A3, (const float*)t->A4,
                            (const float*)t->dY, t->dHh, t->hpart, B, nb, tpb);
         RDL_CK(hipGetLastError(), "rdl head_bwd_kernel");
-        hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((HB_PART + 255) / 256, (unsigned)T), dim3(256), 0, t->stream,
-                           (const float*)t->hpart, nb, g);
-        RDL_CK(hipGetLastError(), "rdl head_wgrad_reduce_kernel");
+        if (!finish) {
+            hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((HB_PART + 255) / 256, (unsigned)T), dim3(256), 0,
+                               t->stream, (const float*)t->hpart, nb, g);
+            RDL_CK(hipGetLastError(), "rdl head_wgrad_reduce_kernel");
+        }
     } else {
     // step s's head backward over its B rows (weight gradients; data gradients with the tanh
     // derivative fused): per layer, [dW; db] (weight gradient, ones column) beside the data
@@ -1561,7 +1666,13 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
                    ga(U, G4, Ri, t->H, U, 1, dZl, G4, 0, g + OFF_WL + XI * G4, G4)),
                "rdl dWl x | h");
     if (!persistent(t, B)) RDL_CK(colsum(t, dZl, R, G4, G4, g + OFF_BL), "rdl dbl");   // else summed in BPTT
-    if (persistent(t, B)) {   // from the BPTT kernel's dbl and Q = prev^T dz: one launch
+    if (finish) {   // the heads' row sums + dWp, dbp from the BPTT kernel's dbl and Q = prev^T dz
+        hipLaunchKernelGGL(grad_finish_kernel, dim3((unsigned)(T * HB_BLK + 161)), dim3(256), 0, t->stream,
+                           (const float*)t->hpart, head_nb(T, B), T, P, (const float*)t->qbuf, g,
+                           (const float*)t->lpart, (int)(T * ((B + HF_ROWS - 1) / HF_ROWS)), (float)R, t->ctl, t->hist,
+                           t->cfg.metrics_len);
+        RDL_CK(hipGetLastError(), "rdl grad_finish_kernel");
+    } else if (persistent(t, B)) {   // from the BPTT kernel's dbl and Q = prev^T dz: one launch
         hipLaunchKernelGGL(dense32_grad_kernel, dim3(160), dim3(256), 0, t->stream, P, (const float*)t->qbuf, g);
         RDL_CK(hipGetLastError(), "rdl dense32_grad_kernel");
     } else {
@@ -1643,7 +1754,7 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     const int64_t hp = (int64_t)t->T * nbmax * HB_PART;
     if (hp <= HPART_MAX_FLOATS) alloc(&t->hpart, hp);
     alloc(&t->colws, t->colws_floats);
-    alloc(&t->lpart, 2 * ((R + LOSS_BLOCK - 1) / LOSS_BLOCK));
+    alloc(&t->lpart, std::max<int64_t>(2 * ((R + LOSS_BLOCK - 1) / LOSS_BLOCK), 2 * HB_WIDE_GRID));
     alloc(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
     if (e == hipSuccess) e = hipMalloc((void**)&t->ctl, sizeof(uint32_t) * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&t->bar, sizeof(uint32_t) * 4);
@@ -1776,7 +1887,7 @@ int rdl_rollout(rdl_trainer* t, const float* ob, const float* prev_pdflat, const
         return rd::set_error(RD_EINVAL, "rdl_rollout: bad argument");
     rd::DeviceGuard dg(t->device);
     RD_HIP(dg.err, "rdl_rollout");
-    if (int rc = run_forward(t, ob, prev_pdflat, state0, windows, t->Y, true)) return rc;
+    if (int rc = run_forward(t, ob, prev_pdflat, state0, windows, t->Y, true, t_pdflat, windows_global)) return rc;
     return run_backward(t, prev_pdflat, t_pdflat, windows, windows_global);
 }
 

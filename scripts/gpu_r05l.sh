@@ -2,7 +2,7 @@
 # Round-5 LSTM redesign check: LSTM GPU tests, the 20/32/1024-window bench, kernel stats at 20 windows
 set -o pipefail
 OUT=gpurun_out/r05l; mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_student_lstm_gpu.py > $OUT/pytest_lstm.log 2>&1 || { tail -30 $OUT/pytest_lstm.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_student_lstm_gpu.py tests/test_c1_gpu.py > $OUT/pytest_lstm.log 2>&1 || { tail -30 $OUT/pytest_lstm.log; exit 1; }
 tail -2 $OUT/pytest_lstm.log
 timeout -k 10 300 python -u scripts/bench_student_lstm.py 20 32 1024 16384 > $OUT/bench.jsonl 2> $OUT/bench.err || { cat $OUT/bench.err | tail; exit 1; }
 cat $OUT/bench.jsonl

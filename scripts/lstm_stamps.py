@@ -1,7 +1,7 @@
 """Phase stamps of the LSTM student's 20-window training step (diagnostic build
-libreacher_lstmst.so: profiles/r05l_lstm_stamps.diff applied, -DRDL_STAMPS).  Workgroup 0's
-s_memrealtime (100 MHz) at the phases of lstm_fwd_persist_kernel (0), lstm_bptt_persist_kernel
-(1), head_bwd_kernel (2) and head_fwd_kernel (3) of the last of N steps; prints one JSON line.
+libreacher_lstmst.so: profiles/r05l_lstm_stamps_50wg.diff applied, -DRDL_STAMPS).  Workgroup 0's
+s_memrealtime (100 MHz) at the phases of lstm_fwd_persist_kernel (0) and lstm_bptt_persist_kernel
+(1) of the last of N steps; prints one JSON line.
 
   RD_LIB=libreacher_lstmst.so python scripts/lstm_stamps.py [windows] [steps]
 """
@@ -37,34 +37,20 @@ def main():
     st = np.zeros((8, 64), dtype=np.uint64)
     assert rd(st.ctypes.data) == 0
     us = lambda a, b: round(float(int(b) - int(a)) / 100.0, 3)   # 100 MHz ticks -> us
-    f, bp, hb, hf = st[0], st[1], st[2], st[3]
-    t0 = int(f[0])
+    f, bp = st[0], st[1]
     out = {"windows": B, "T": T, "steps": n,
-           "fwd": {"prologue": us(f[0], f[1]),
-                   "steps": [{"wait_h": us(f[1] if s == 0 else f[4 + 3 * (s - 1)], f[2 + 3 * s]),
-                              "mfma": us(f[2 + 3 * s], f[3 + 3 * s]), "cell": us(f[3 + 3 * s], f[4 + 3 * s])}
-                             for s in range(T)],
-                   "total": us(f[0], f[4 + 3 * (T - 1)]),
-                   "shader_clock_ghz": round((int(st[4][1]) - int(st[4][0])) / (float(int(f[4 + 3 * (T - 1)]) - int(f[0])) * 10.0), 3)},
-           "head_fwd": {"start_after_fwd_start": us(t0, hf[0]), "stage": us(hf[0], hf[1]),
-                        "layers": [us(hf[k], hf[k + 1]) for k in range(1, 6)], "total": us(hf[0], hf[6])},
-           "head_bwd": {"start_after_fwd_start": us(t0, hb[0]), "stage": us(hb[0], hb[1]),
-                        "dgrad": [us(hb[k], hb[k + 1]) for k in range(1, 6)], "wgrad_issue": us(hb[6], hb[7]),
-                        "wgrad_drain": us(hb[7], hb[8]), "total": us(hb[0], hb[8])},
-           "bptt": {"start_after_fwd_start": us(t0, bp[0]), "prologue": us(bp[0], bp[1]),
-                    "steps": [{"dh_in": us(bp[1] if j == 0 else bp[4 + 4 * (j - 1)], bp[2 + 4 * j]),
-                               "cell": us(bp[2 + 4 * j], bp[3 + 4 * j]), "mfma_store": us(bp[3 + 4 * j], bp[4 + 4 * j])}
-                              for j in range(T - 1)],
-                    "last_cell_and_sums": us(bp[4 + 4 * (T - 2)], bp[60]),
-                    "total_to_sums": us(bp[0], bp[60])}}
-    if int(st[5][0]):   # the cell-split build (profiles/r05l_lstm_stamps.diff, second part)
-        c5 = st[5]
-        out["fwd_cell_split"] = [{"z_to_h": us(c5[6 * s], c5[6 * s + 1]), "stores": us(c5[6 * s + 1], c5[6 * s + 2]),
-                                  "q1_z_to_h": us(c5[6 * s + 3], c5[6 * s + 4]) if int(c5[6 * s + 3]) else None,
-                                  "q1_stores": us(c5[6 * s + 4], c5[6 * s + 5]) if int(c5[6 * s + 3]) else None,
-                                  "after_mfma_to_z": us(f[3 + 3 * s], c5[6 * s]),
-                                  "tail": us(c5[6 * s + 5] if int(c5[6 * s + 3]) else c5[6 * s + 2], f[4 + 3 * s])}
-                                 for s in range(T)]
+           "fwd": {"prologue_and_inputs0": us(f[0], f[1]),
+                   "steps": [{"wait_h": us(f[1] if s == 0 else f[5 + 4 * (s - 1)], f[2 + 4 * s]),
+                              "mfma": us(f[2 + 4 * s], f[3 + 4 * s]), "cell": us(f[3 + 4 * s], f[4 + 4 * s]),
+                              "inputs_next": us(f[4 + 4 * s], f[5 + 4 * s])} for s in range(T)],
+                   "total": us(f[0], f[5 + 4 * (T - 1)])},
+           "bptt": {"start_after_fwd_start": us(f[0], bp[0]), "prologue": us(bp[0], bp[1]),
+                    "steps": [{"dh_in": us(bp[1] if j == 0 else bp[6 + 5 * (j - 1)], bp[2 + 5 * j]),
+                               "cell_and_loads": us(bp[2 + 5 * j], bp[3 + 5 * j]),
+                               "mfma_store": us(bp[3 + 5 * j], bp[4 + 5 * j]),
+                               "arrive_dwl": us(bp[4 + 5 * j], bp[5 + 5 * j]),
+                               "wait": us(bp[5 + 5 * j], bp[6 + 5 * j])} for j in range(T - 1)],
+                    "last_cell": us(bp[6 + 5 * (T - 2)], bp[60])}}
     print(json.dumps(out), flush=True)
     tr.close()
 
