@@ -658,11 +658,11 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
                                                        (int)((po + (int64_t)(16 * (cbo + 2 * q) + i) * PR_ROWS + 16 * rb + 4 * gq) * 4),
                                                        0, 16);
         }
-        // arrive (every wave's sc1 partial stores drained first), then (4) while the others arrive
+        // (4) while the sc1 partial stores drain, then arrive (every wave's stores landed first)
+        dwl_step();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        dwl_step();
         load_a(s - 1);
         if (tid == 0) {
             const uint32_t target = ++nsync * gridDim.x;
