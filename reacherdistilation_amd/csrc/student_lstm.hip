@@ -779,6 +779,41 @@ __device__ __forceinline__ void head_stage(const float* __restrict__ src, int ld
 // (124 KB of LDS would leave one workgroup per CU).
 constexpr int HB_WIDE_GRID = 256;   // at most this many one-tile workgroups: the latency-bound forms
 static_assert(HSZ % 4 == 0 && (OFF_H % 4) == 0, "16-B pieces of a head's parameters");
+// A head's weights in the head backward's MFMA operand order ("packed"), kept beside the
+// parameters (t->wpack, [T][HWP]): written by the Adam kernel with every update and by
+// pack_heads_kernel when the parameters are set.  Per layer (W5, W4, W3, W2, W1 of [NI][KO]),
+// per column block cb < ceil(NI / 16) and k step kq < KO / 4, 64 floats, lane (i, gq) ->
+// W[16 cb + i][4 kq + gq] (zero past NI).  A wave of head_bwd_kernel<false, 16> loads each of its
+// B operands with one coalesced 256-B access instead of sixteen 16-B pieces of sixteen lines
+// (the [NI][KO] layout read per lane cost the backward 15 us of a 24 us launch at 20 windows,
+// profiles/r05p_*).
+__host__ __device__ constexpr int hw_size(int KO, int NI) { return ((NI + 15) / 16) * 16 * KO; }
+constexpr int HWP_5 = 0, HWP_4 = HWP_5 + hw_size(4, H4), HWP_3 = HWP_4 + hw_size(H4, H3),
+              HWP_2 = HWP_3 + hw_size(H3, H2), HWP_1 = HWP_2 + hw_size(H2, H1), HWP = HWP_1 + hw_size(H1, U);
+// packed index of head offset o (within one head's HSZ), or -1 for the biases (KO is a power of
+// two in every layer: shifts and masks, no divisions)
+template <int KO>
+__device__ __forceinline__ int hw_at(int base, int rel) {
+    const int col = rel / KO, k = rel & (KO - 1);
+    return base + (((col >> 4) * (KO / 4) + (k >> 2)) << 6) + ((k & 3) << 4) + (col & 15);
+}
+__device__ __forceinline__ int hw_index(int o) {
+    static_assert((H1 & (H1 - 1)) == 0 && (H2 & (H2 - 1)) == 0 && (H3 & (H3 - 1)) == 0 && (H4 & (H4 - 1)) == 0,
+                  "power-of-two layer widths");
+    if (o < OFF_B1) return hw_at<H1>(HWP_1, o - OFF_W1);
+    if (o >= OFF_W2 && o < OFF_B2) return hw_at<H2>(HWP_2, o - OFF_W2);
+    if (o >= OFF_W3 && o < OFF_B3) return hw_at<H3>(HWP_3, o - OFF_W3);
+    if (o >= OFF_W4 && o < OFF_B4) return hw_at<H4>(HWP_4, o - OFF_W4);
+    if (o >= OFF_W5 && o < OFF_B5) return hw_at<4>(HWP_5, o - OFF_W5);
+    return -1;
+}
+__global__ __launch_bounds__(256) void pack_heads_kernel(const float* __restrict__ P, float* __restrict__ wpack, int T) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= (int64_t)T * HSZ) return;
+    const int ts = (int)(q / HSZ), o = (int)(q - (int64_t)ts * HSZ);
+    const int w = hw_index(o);
+    if (w >= 0) wpack[(int64_t)ts * HWP + w] = P[OFF_H + q];
+}
 // step t's head -> W (16-B LDS-DMA pieces, lane l of a wave's burst to base + 16 l); the caller
 // waits (vmcnt) before its barrier
 __device__ __forceinline__ void head_params_to_lds(const float* __restrict__ P, float* W) {
@@ -949,6 +984,16 @@ struct HeadW {
             for (int kq = 0; kq < KO / 4; ++kq) w[it][kq] = cv ? W[col * KO + 4 * kq + gq] : 0.0f;
         }
     }
+    // from the packed layout (pack_layer): one coalesced load per operand
+    __device__ __forceinline__ void load_packed(const float* __restrict__ Wp, int tid) {
+        const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int cb = wave + NW * it;
+#pragma unroll
+            for (int kq = 0; kq < KO / 4; ++kq) w[it][kq] = cb < NB ? Wp[(cb * (KO / 4) + kq) * 64 + lane] : 0.0f;
+        }
+    }
     __device__ __forceinline__ float operator()(int it, int kq, bool, int, int) const { return w[it][kq]; }
 };
 // part[m][n] = sum over the 16 rows of act[row][m] d[row][n], m < M (the last input row is the
@@ -1024,7 +1069,8 @@ __global__ __launch_bounds__(64 * NWV) void head_bwd_kernel(const float* __restr
                                                        const float* __restrict__ A1, const float* __restrict__ A2,
                                                        const float* __restrict__ A3, const float* __restrict__ A4,
                                                        const float* __restrict__ dY, float* __restrict__ dHh,
-                                                       float* __restrict__ part, int64_t B, int nb, int tpb) {
+                                                       float* __restrict__ part, int64_t B, int nb, int tpb,
+                                                       const float* __restrict__ wpack) {
     __shared__ __attribute__((aligned(16))) float X0[HF_ROWS][U + 4];   // Hc, ones column U
     __shared__ __attribute__((aligned(16))) float X1[HF_ROWS][L1];
     __shared__ __attribute__((aligned(16))) float X2[HF_ROWS][L2];
@@ -1054,7 +1100,18 @@ __global__ __launch_bounds__(64 * NWV) void head_bwd_kernel(const float* __restr
     HeadW<H3, H2, NW> w3;
     HeadW<H2, H1, NW> w2;
     HeadW<H1, U, NW> w1;
-    if constexpr (MT) {
+    // RW: the weights held in registers -- MT (read once per workgroup over its tiles) and the
+    // sixteen-wave form (one column block per wave: every layer's weights in one round trip at
+    // entry, beside the row staging, instead of one round trip per layer)
+    constexpr bool RW = MT || NW == 16;
+    if (RW && wpack) {   // (uniform) the packed copy of this step's head weights
+        const float* d = wpack + (int64_t)ts * HWP;
+        w5.load_packed(d + HWP_5, threadIdx.x);
+        w4.load_packed(d + HWP_4, threadIdx.x);
+        w3.load_packed(d + HWP_3, threadIdx.x);
+        w2.load_packed(d + HWP_2, threadIdx.x);
+        w1.load_packed(d + HWP_1, threadIdx.x);
+    } else if constexpr (RW) {
         w5.load(P + OFF_W5, threadIdx.x);
         w4.load(P + OFF_W4, threadIdx.x);
         w3.load(P + OFF_W3, threadIdx.x);
@@ -1069,7 +1126,7 @@ __global__ __launch_bounds__(64 * NWV) void head_bwd_kernel(const float* __restr
         // at once and spill)
         const float* Pk = P;
         int tid = threadIdx.x;
-        asm volatile("" : "+s"(Pk), "+v"(tid));
+        if constexpr (MT) asm volatile("" : "+s"(Pk), "+v"(tid));
         // rows past R (the step's last row) are zero (activations and gradients): they add nothing
         head_stage<U, U + 4, NT>(Hc, U, row0, R, X0, tid);
         head_stage<H1 + 1, L1, NT>(A1, L1, row0, R, X1, tid);   // with the ones column
@@ -1079,7 +1136,7 @@ __global__ __launch_bounds__(64 * NWV) void head_bwd_kernel(const float* __restr
         head_stage<4, 8, NT>(dY, 4, row0, R, D5, tid);
         if (tid < HF_ROWS) X0[tid][U] = row0 + tid < R ? 1.0f : 0.0f;
         __syncthreads();
-        if constexpr (MT) {
+        if constexpr (RW) {
             head_dgrad_f<4, H4, true, NW>(D5, D4, X4, w5, nullptr, 0, row0, R, tid);
             __syncthreads();
             head_dgrad_f<H4, H3, true, NW>(D4, D3, X3, w4, nullptr, 0, row0, R, tid);
@@ -1341,6 +1398,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* src, int64_t M
 struct AdamArgs {
     const float* grad;
     float* params;
+    float* wpack;   // the heads' weights in the head backward's operand order (hw_index)
     float* m;
     float* v;
     uint32_t* ctl;
@@ -1360,7 +1418,12 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
         v += (g * g - v) * (1.0f - a.b2);
         a.m[p] = m;
         a.v[p] = v;
-        a.params[p] -= (m * alpha) / (sqrtf(v) + a.eps);
+        const float w = a.params[p] - (m * alpha) / (sqrtf(v) + a.eps);
+        a.params[p] = w;
+        if (p >= OFF_H) {
+            const int q = p - OFF_H, ts = q / HSZ, x = hw_index(q - ts * HSZ);
+            if (x >= 0) a.wpack[(int64_t)ts * HWP + x] = w;
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctl[0] = S + 1u;
@@ -1400,6 +1463,7 @@ struct rdl_trainer {
     float *dhn = nullptr, *dc = nullptr;
     float *split = nullptr, *colws = nullptr, *lpart = nullptr, *hist = nullptr;
     float* hpart = nullptr;    // fused head backward: one partial row of HB_PART per workgroup (head_nb)
+    float* wpack = nullptr;    // [T][HWP]: the heads' weights packed by the training forward (small batches)
     int64_t colws_floats = 0;
     uint32_t* ctl = nullptr;
     bool loss_in_head = false;   // the last forward computed the loss (head_fwd_kernel<true>)
@@ -1588,7 +1652,8 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
         auto* kern = tpb > 1 ? head_bwd_kernel<true, 8> : wide ? head_bwd_kernel<false, 16> : head_bwd_kernel<false, 4>;
         hipLaunchKernelGGL(kern, dim3((unsigned)(T * nb)), dim3(tpb > 1 ? 512 : wide ? 1024 : 256), 0, t->stream, Hc, P,
                            (const float*)t->A1, (const float*)t->A2, (const float*)t->A3, (const float*)t->A4,
-                           (const float*)t->dY, t->dHh, t->hpart, B, nb, tpb);
+                           (const float*)t->dY, t->dHh, t->hpart, B, nb, tpb,
+                           wide ? (const float*)t->wpack : nullptr);
         RDL_CK(hipGetLastError(), "rdl head_bwd_kernel");
         if (!finish) {
             hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((HB_PART + 255) / 256, (unsigned)T), dim3(256), 0,
@@ -1684,7 +1749,7 @@ int run_backward(rdl_trainer* t, const float* prev, const float* tgt, int64_t B,
 }
 
 int launch_adam(rdl_trainer* t) {
-    AdamArgs a{t->grad, t->params, t->m, t->v, t->ctl, t->cfg.lr, t->cfg.beta1, t->cfg.beta2, t->cfg.eps, t->np};
+    AdamArgs a{t->grad, t->params, t->wpack, t->m, t->v, t->ctl, t->cfg.lr, t->cfg.beta1, t->cfg.beta2, t->cfg.eps, t->np};
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((t->np + 255) / 256)), dim3(256), 0, t->stream, a);
     RD_HIP(hipGetLastError(), "rdl adam_kernel");
     return RD_OK;
@@ -1753,6 +1818,7 @@ int rdl_create(rdl_trainer** out, const rdl_config* cfg, int device, void* hip_s
     for (int64_t b = HF_ROWS; b < t->Bmax + HF_ROWS; b += HF_ROWS) nbmax = std::max<int64_t>(nbmax, head_nb(t->T, b));
     const int64_t hp = (int64_t)t->T * nbmax * HB_PART;
     if (hp <= HPART_MAX_FLOATS) alloc(&t->hpart, hp);
+    alloc(&t->wpack, (int64_t)t->T * HWP);
     alloc(&t->colws, t->colws_floats);
     alloc(&t->lpart, std::max<int64_t>(2 * ((R + LOSS_BLOCK - 1) / LOSS_BLOCK), 2 * HB_WIDE_GRID));
     alloc(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
@@ -1792,7 +1858,7 @@ int rdl_destroy(rdl_trainer* t) {
     rd::DeviceGuard dg(t->device);
     float* bufs[] = {t->params, t->m, t->v, t->own_grad, t->X, t->H, t->Cs, t->Z, t->G, t->A1, t->A2, t->A3, t->A4,
                      t->Y, t->dY, t->D32, t->D64a, t->D128, t->D64b, t->dHh, t->dP, t->dhn, t->dc, t->split,
-                     t->colws, t->lpart, t->hist, t->bpart, t->qbuf, t->hpart};
+                     t->colws, t->lpart, t->hist, t->bpart, t->qbuf, t->hpart, t->wpack};
     for (float* p : bufs)
         if (p) (void)hipFree(p);
     if (t->hx) (void)hipFree(t->hx);
@@ -1813,6 +1879,10 @@ int rdl_set_params(rdl_trainer* t, const float* params) {
     rd::DeviceGuard dg(t->device);
     RD_HIP(hipMemcpyAsync(t->params, params, sizeof(float) * t->np, hipMemcpyDeviceToDevice, t->stream),
            "rdl_set_params");
+    const int64_t n = (int64_t)t->T * HSZ;
+    hipLaunchKernelGGL(pack_heads_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, t->stream,
+                       (const float*)t->params, t->wpack, t->T);
+    RD_HIP(hipGetLastError(), "rdl_set_params: pack_heads_kernel");
     return RD_OK;
 }
 
