@@ -917,6 +917,37 @@ __device__ __forceinline__ void head_dgrad_f(const float (*dout)[LD], float (*di
                                              float* gout, int ldg, int64_t row0, int64_t R, int tid) {
     const int wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
     constexpr int NB = (NI + 15) / 16, IT = (NB + NW - 1) / NW;
+    if constexpr (NW != 16) {   // four waves (mid-size batches: weights streamed per MFMA, 56 VGPRs;
+                                // the fenced form below held 167 and ran slower) and MT (weights in
+                                // registers already): the round-4 chains, clean in the hazard scan
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {   // unrolled: every weight load of the layer in flight at once
+            const int cb = wave + NW * it;
+            if (cb >= NB) break;
+            const int col = 16 * cb + i;
+            const bool cv = col < NI;
+            rdg::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kq = 0; kq < KO / 4; ++kq) {
+                const int k = 4 * kq + gq;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dout[i][k], wf(it, kq, cv, col, k), acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * gq + r;
+                float v = acc[r];
+                if (DT) {
+                    const float a = act[row][col < NI ? col : 0];
+                    v *= fmaf(-a, a, 1.0f);
+                }
+                if (cv) {
+                    if (din) din[row][col] = v;
+                    if (gout && row0 + row < R) gout[(row0 + row) * ldg + col] = v;
+                }
+            }
+        }
+        return;
+    }
     // the chains' operands: dout's (shared by every column block) and this lane's weights, all
     // loads issued before the first MFMA; the chains interleave (one accumulator per block)
     float av[KO / 4], bv[IT][KO / 4];
