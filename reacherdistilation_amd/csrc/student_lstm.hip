@@ -232,7 +232,6 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_kernel(const float* __restri
 constexpr int PR_ROWS = 32, PR_UNITS = 4, PR_GRID = U / PR_UNITS;   // 50 workgroups
 constexpr int PR_COLS = 4 * PR_UNITS;   // 16 gate columns per workgroup: c = 4 y + j
 constexpr int PR_KH = LSTM_KH;          // K split of the forward's gate sums (lstm_rec_fwd_kernel's)
-constexpr int PR_AS = 212;              // h staging row pitch [row][k]: conflict-free A reads (212 = 20 mod 64)
 constexpr int PR_KQ = PR_KH / 4, PR_KQ1 = (U - PR_KH) / 4;   // k steps of the two halves (28, 22: pad k >= U skipped)
 constexpr uint32_t PR_SPIN_LIMIT = 1u << 22;
 static_assert(U % PR_UNITS == 0 && PR_KH % RF_TK == 0 && PR_KQ1 <= PR_KQ, "persistent LSTM tiling");
@@ -301,7 +300,6 @@ __device__ __forceinline__ void fence_end(rdg::f32x4 (&G)[Q]) {
 // Zx_s = X_s Wl[0:43] + bl of the local columns (the Zx GEMM's MFMA k order and epilogue), so
 // G, c and h stay bitwise those of the per-step path.  Zx of step s+1 is formed right after step
 // s publishes h, while the granules travel.
-constexpr int GR_SWEEP = (PR_ROWS * U + 255) / 256;   // h granules per thread per step (at most 25)
 constexpr int PR_XQ = (XI + 3) / 4;                    // Zx k steps (11; k = 43 is the zero column)
 __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ P, const float* __restrict__ ob,
                                                                const float* __restrict__ prev, float* __restrict__ X,
@@ -310,7 +308,6 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
                                                                int T, float keep_prob, uint64_t seed, int64_t row_base,
                                                                const uint32_t* __restrict__ ctl, uint32_t* bar,
                                                                unsigned long long* hx) {
-    __shared__ __attribute__((aligned(16))) float As[PR_ROWS][PR_AS];          // h_s [row][k]; zero past B, U
     __shared__ __attribute__((aligned(16))) float Zp[2][PR_ROWS][PR_COLS + 1];   // the K halves' sums [row][c]
     __shared__ __attribute__((aligned(16))) float Xs[PR_ROWS][XLD];             // X_s rows; zero past B
     __shared__ __attribute__((aligned(16))) float Zx[PR_ROWS][PR_COLS + 1];     // Zx_s of the local columns
@@ -343,7 +340,6 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
 #pragma unroll
     for (int a = 0; a < 4; ++a) wp[a] = P[OFF_WP + a * 32 + dc];
     const float bpc = P[OFF_BP + dc];
-    for (int x = tid; x < PR_ROWS * PR_AS; x += 256) (&As[0][0])[x] = 0.0f;
     for (int x = tid; x < PR_ROWS * XLD; x += 256) (&Xs[0][0])[x] = 0.0f;
     const bool pt = tid < 4 * B;
     const int pr = tid >> 2, pu = u0 + (tid & 3);
@@ -405,29 +401,32 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
             for (int r = 0; r < 4; ++r) Zx[16 * rb + 4 * gq + r][i] = acc[0][r] + bias;
         }
     };
-    __syncthreads();   // As and Xs zeroed before the staging writes
+    __syncthreads();   // Xs zeroed before the staging writes
     inputs(0);
-    const int nb = B * U;
+    const int arow = 16 * rb + i;   // this lane's A-operand row (h_s row), k = 4 (kq0 + q) + gq
+    const bool av_ok = arow < B;
     for (int s = 0; s < T; ++s) {
-        if (s > 0) {   // h_s: every workgroup's granules of step s, re-read until every tag matches
-            const unsigned long long* src = hx + (int64_t)(s & 1) * PR_ROWS * U;
+        // this wave's A operands: h_s[arow][k] over its K half, straight into registers -- each
+        // wave gathers its own quadrant of the other workgroups' granules (re-read until every
+        // tag matches) and starts its chain when they are in, no staging, no workgroup barrier
+        float av[PR_KQ];
+        if (s > 0) {
+            const unsigned long long* src = hx + (int64_t)(s & 1) * PR_ROWS * U + (int64_t)(av_ok ? arow : 0) * U + 4 * kq0 + gq;
             const uint32_t want = gr_tag(gen, (uint32_t)s);
             for (uint32_t spins = 0;;) {
-                unsigned long long v[GR_SWEEP];
+                unsigned long long v[PR_KQ];
 #pragma unroll
-                for (int j = 0; j < GR_SWEEP; ++j)
-                    v[j] = 256 * j < nb ? gr_load(src + min(tid + 256 * j, nb - 1)) : (unsigned long long)want << 32;
+                for (int q = 0; q < PR_KQ1; ++q) v[q] = av_ok ? gr_load(src + 4 * q) : (unsigned long long)want << 32;
+                if (kh == 0) {
+#pragma unroll
+                    for (int q = PR_KQ1; q < PR_KQ; ++q) v[q] = av_ok ? gr_load(src + 4 * q) : (unsigned long long)want << 32;
+                }
                 bool ok = true;
 #pragma unroll
-                for (int j = 0; j < GR_SWEEP; ++j) ok &= (uint32_t)(v[j] >> 32) == want;
-                if (ok) {
+                for (int q = 0; q < PR_KQ; ++q) ok &= (q < PR_KQ1 || kh == 0) ? (uint32_t)(v[q] >> 32) == want : true;
 #pragma unroll
-                    for (int j = 0; j < GR_SWEEP; ++j) {
-                        const int idx = tid + 256 * j;
-                        if (idx < nb) As[idx / U][idx % U] = __uint_as_float((uint32_t)v[j]);
-                    }
-                    break;
-                }
+                for (int q = 0; q < PR_KQ; ++q) av[q] = (q < PR_KQ1 || kh == 0) ? __uint_as_float((uint32_t)v[q]) : 0.0f;
+                if (__all(ok)) break;
                 if (++spins > PR_SPIN_LIMIT) {
                     __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     fail_s = 1;
@@ -435,35 +434,25 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-        } else if (state0) {
-            const float* hs = state0 + (int64_t)B * U;
-            for (int idx = tid; idx < nb; idx += 256) As[idx / U][idx % U] = hs[idx];
+        } else {
+            const float* hs = state0 && av_ok ? state0 + (int64_t)B * U + (int64_t)arow * U + 4 * kq0 + gq : nullptr;
+#pragma unroll
+            for (int q = 0; q < PR_KQ; ++q) av[q] = hs && (q < PR_KQ1 || kh == 0) ? hs[4 * q] : 0.0f;
         }
-        __syncthreads();
-        if (fail_s) break;   // (uniform) a peer's granules never arrived: the timeout flag is raised
         // this wave's K half: one accumulation chain in k order (the per-step kernel's lo / hi)
         rdg::f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
-        {
-            const float* arow = &As[16 * rb + i][4 * kq0 + gq];
-            float av[PR_KQ];
+        fence_begin(acc);
 #pragma unroll
-            for (int q = 0; q < PR_KQ1; ++q) av[q] = arow[4 * q];
-            if (kh == 0) {
+        for (int q = 0; q < PR_KQ1; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[q], acc[0], 0, 0, 0);
+        if (kh == 0) {
 #pragma unroll
-                for (int q = PR_KQ1; q < PR_KQ; ++q) av[q] = arow[4 * q];
-            }
-            fence_begin(acc);
-#pragma unroll
-            for (int q = 0; q < PR_KQ1; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[q], acc[0], 0, 0, 0);
-            if (kh == 0) {
-#pragma unroll
-                for (int q = PR_KQ1; q < PR_KQ; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[q], acc[0], 0, 0, 0);
-            }
-            fence_end(acc);
+            for (int q = PR_KQ1; q < PR_KQ; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[q], acc[0], 0, 0, 0);
         }
+        fence_end(acc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) Zp[kh][16 * rb + 4 * gq + r][i] = acc[0][r];   // C: rows 4 gq + r, column i
         __syncthreads();
+        if (fail_s) break;   // (uniform) a peer's granules never arrived: the timeout flag is raised
         // TF1 LSTMCell (lstm_rec_fwd_kernel's arithmetic) at this thread's point
         if (pt) {
             const int c0 = tid & 3;
