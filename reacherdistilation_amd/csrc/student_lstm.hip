@@ -502,7 +502,6 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
                                                                 float* __restrict__ dbl, const float* __restrict__ prev,
                                                                 float* __restrict__ Q, int B, int T, uint32_t* bar) {
     __shared__ __attribute__((aligned(16))) float Dz[PR_ROWS][PR_COLS + 1];          // dz_s [row][c]; zero past B
-    __shared__ __attribute__((aligned(16))) float Dh[PR_GRID][PR_UNITS][PR_ROWS];    // dh_next partials [w][j][row]
     __shared__ float red[PR_ROWS][PR_UNITS][PB_RED];
     __shared__ int ok_s;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
@@ -571,36 +570,19 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
     load_cell(T - 1);
     load_a(T - 1);
     __syncthreads();   // Dz zeroed
-    const int nrg = (B + 3) >> 2, nl = PR_GRID * PR_UNITS * nrg;   // 16-B partial loads per step (4 rows each)
-    constexpr int NLD = (PR_GRID * PR_UNITS * (PR_ROWS / 4) + 255) / 256;
     uint32_t nsync = 0;
     for (int s = T - 1; s >= 0; --s) {
         float dhn = 0.f;
-        if (s < T - 1) {   // (1) dh_next: the 50 partials of step s+1 for the local units, summed in workgroup order
-            const int64_t pb = (int64_t)((s + 1) & 1) * PR_GRID * PB_PART;
-            rdg::f32x4 v[NLD];
+        if (s < T - 1 && pt) {   // (1) dh_next at the point: the 50 partials of step s+1, summed in workgroup order
+            const int64_t pb = (int64_t)((s + 1) & 1) * PR_GRID * PB_PART + (int64_t)pu * PR_ROWS + pr;
+            float v[PR_GRID];
 #pragma unroll
-            for (int j = 0; j < NLD; ++j) {
-                const int x = min(tid + 256 * j, nl - 1), w = x / (PR_UNITS * nrg), rem = x - w * (PR_UNITS * nrg);
-                const int jj = rem / nrg, rg = rem - jj * nrg;
-                v[j] = 256 * j < nl ? pr_load4(rP, pb + (int64_t)w * PB_PART + (int64_t)(u0 + jj) * PR_ROWS + 4 * rg)
-                                    : rdg::f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+            for (int w = 0; w < PR_GRID; ++w)
+                v[w] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rP, (int)((pb + (int64_t)w * PB_PART) * 4), 0, 16));
+            float acc = v[0];
 #pragma unroll
-            for (int j = 0; j < NLD; ++j) {
-                const int x = tid + 256 * j;
-                if (x < nl) {
-                    const int w = x / (PR_UNITS * nrg), rem = x - w * (PR_UNITS * nrg), jj = rem / nrg, rg = rem - jj * nrg;
-                    *reinterpret_cast<rdg::f32x4*>(&Dh[w][jj][4 * rg]) = v[j];
-                }
-            }
-            __syncthreads();
-            if (pt) {
-                float a = Dh[0][pj][pr];
-#pragma unroll 10
-                for (int w = 1; w < PR_GRID; ++w) a += Dh[w][pj][pr];
-                dhn = a;
-            }
+            for (int w = 1; w < PR_GRID; ++w) acc += v[w];
+            dhn = acc;
         }
         // (2) TF1 LSTMCell backward (cell_bwd_kernel's arithmetic)
         if (pt) {
@@ -666,7 +648,7 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
             }
             ok_s = ok;
         }
-        __syncthreads();   // Dz and Dh are rewritten by the next step
+        __syncthreads();   // Dz is rewritten by the next step
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
         if (!ok_s) return;
     }
