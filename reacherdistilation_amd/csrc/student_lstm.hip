@@ -1408,12 +1408,10 @@ struct AdamArgs {
     int64_t n;   // parameters (params_of(T))
 };
 
-__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t S = a.ctl[4];
-    const float b1p = __uint_as_float(a.ctl[5]), b2p = __uint_as_float(a.ctl[6]);
-    if (p < a.n) {   // TF1 ApplyAdam (lstm_train.py:73-79)
-        const float g = a.grad[p];
+// TF1 ApplyAdam (lstm_train.py:73-79) of parameter p with gradient g; the heads' weights also
+// into their packed copy
+__device__ __forceinline__ void adam_param(const AdamArgs& a, int p, float g, float b1p, float b2p) {
+    {
         const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
         float m = a.m[p], v = a.v[p];
         m += (g - m) * (1.0f - a.b1);
@@ -1427,6 +1425,12 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
             if (x >= 0) a.wpack[(int64_t)ts * HWP + x] = w;
         }
     }
+}
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t S = a.ctl[4];
+    const float b1p = __uint_as_float(a.ctl[5]), b2p = __uint_as_float(a.ctl[6]);
+    if (p < a.n) adam_param(a, p, a.grad[p], b1p, b2p);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctl[0] = S + 1u;
         a.ctl[1] = __float_as_uint(b1p * a.b1);
