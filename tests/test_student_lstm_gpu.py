@@ -285,7 +285,8 @@ def test_driver_restores_and_saves_the_student(tmp_path, name):
     assert torch.equal(st2.params(), saved)
 
 
-@pytest.mark.parametrize("T,B,with_state", [(10, 20, False), (10, 32, True), (1, 7, True), (3, 1, False)])
+@pytest.mark.parametrize("T,B,with_state", [(10, 20, False), (10, 32, True), (1, 7, True), (3, 1, False),
+                                             (16, 24, True), (40, 17, False)])
 def test_persistent_recurrence_matches_per_step_launches(T, B, with_state):
     """B <= 32: the whole forward recurrence and the whole BPTT each run as one persistent
     launch (lstm_fwd_persist_kernel / lstm_bptt_persist_kernel).  Forward: bitwise the per-step
@@ -334,3 +335,23 @@ def test_fused_head_matches_the_layer_gemms(T, B):
     assert np.array_equal(out["1"][1][:w1], out["0"][1][:w1])
     h1, h0 = out["1"][1][w1:], out["0"][1][w1:]
     assert np.abs(h1 - h0).max() <= 1e-5 * np.abs(h0).max()
+
+
+def test_persistent_kernels_many_steps_stay_in_step_with_per_step_path():
+    """500 training steps of the reference's 20 windows through the persistent kernels (50
+    workgroups exchanging h granules / partial dh every unrolled step; the granule generation
+    advances on the device per forward) and through the per-step launches: no hand-off timeout
+    (rdl_get_counter raises on one), the same step count, and parameters that stay within the
+    accumulated f32 reordering of the two paths' gradient sums."""
+    T, B = 10, 20
+    ob, prev, t = _batch(T, B, 77)
+    params = {}
+    for mode in ("1", "0"):
+        tr = _trainer(T, B, "kl", step_recurrence=mode == "0")
+        for _ in range(500):
+            tr.step(_t(ob), _t(prev), _t(t))
+        assert tr.counter() == 500
+        params[mode] = tr.params().cpu().numpy().astype(np.float64)
+        tr.close()
+    d = np.abs(params["1"] - params["0"]).max()
+    assert d <= 1e-4 * np.abs(params["0"]).max(), d
