@@ -1,7 +1,7 @@
 #!/bin/bash
-# r05r: c5 A/B -- the last tile's teacher on the producer (product) vs the round-5 TC kernel (libreacher_c5old.so)
+# r05r: c5 A/B of a distill.hip change (product) vs the previous build (libreacher_c5old.so)
 set -o pipefail
-OUT=gpurun_out/r05r; mkdir -p $OUT
+OUT=gpurun_out/${AB_OUT:-r05r}; mkdir -p $OUT
 for k in 1 2 3; do
   timeout -k 10 120 python scripts/ab_k1.py 2000 c5 >> $OUT/ab.jsonl || exit 1
   RD_LIB=libreacher_c5old.so timeout -k 10 120 python scripts/ab_k1.py 2000 c5 >> $OUT/ab.jsonl || exit 1
