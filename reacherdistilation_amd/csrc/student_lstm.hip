@@ -301,6 +301,11 @@ __device__ __forceinline__ void fence_end(rdg::f32x4 (&G)[Q]) {
 // G, c and h stay bitwise those of the per-step path.  Zx of step s+1 is formed right after step
 // s publishes h, while the granules travel.
 constexpr int PR_XQ = (XI + 3) / 4;                    // Zx k steps (11; k = 43 is the zero column)
+// FU: units per forward workgroup (FNCB column blocks of 16 gate columns each; grid U / FU).
+// Measured at 20 windows (round 5): FU 2 / 4 / 8 (100 / 50 / 25 workgroups) forward 43.7 / 43.0 /
+// 51.7 us -- fewer readers of the h granules do not pay for the longer MFMA chains
+constexpr int FU = 4, FNCB = (FU + 3) / 4, PR_GRID_F = U / FU;
+static_assert(U % FU == 0 && (FU % 4 == 0 || FU < 4) && FU * PR_ROWS <= 256, "forward tiling: a cell point per thread");
 __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ P, const float* __restrict__ ob,
                                                                const float* __restrict__ prev, float* __restrict__ X,
                                                                const float* __restrict__ state0, float* __restrict__ G,
@@ -308,32 +313,37 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
                                                                int T, float keep_prob, uint64_t seed, int64_t row_base,
                                                                const uint32_t* __restrict__ ctl, uint32_t* bar,
                                                                unsigned long long* hx) {
-    __shared__ __attribute__((aligned(16))) float Zp[2][PR_ROWS][PR_COLS + 1];   // the K halves' sums [row][c]
-    __shared__ __attribute__((aligned(16))) float Xs[PR_ROWS][XLD];             // X_s rows; zero past B
-    __shared__ __attribute__((aligned(16))) float Zx[PR_ROWS][PR_COLS + 1];     // Zx_s of the local columns
+    __shared__ __attribute__((aligned(16))) float Zp[2][PR_ROWS][16 * FNCB + 1];   // the K halves' sums [row][c]
+    __shared__ __attribute__((aligned(16))) float Xs[PR_ROWS][XLD];               // X_s rows; zero past B
+    __shared__ __attribute__((aligned(16))) float Zx[PR_ROWS][16 * FNCB + 1];     // Zx_s of the local columns
     __shared__ int fail_s;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, gq = lane >> 4;
-    const int u0 = blockIdx.x * PR_UNITS;
+    const int u0 = blockIdx.x * FU;
     const int rb = wave & 1, kh = wave >> 1;
     const int kq0 = kh ? PR_KQ : 0;
     const uint32_t gen = bar[3], step = ctl[0];
     const float* Wr = P + OFF_WL + XI * G4;
     if (tid == 0) fail_s = 0;
-    // this lane's B operands over the launch: Wr[k][y U + u0 + j] of column i = 4 y + j, and
-    // (waves 0, 1) Wl[k][..] of the input half, k < 43; the lane's bias bl[column i]
-    const int64_t col = (int64_t)(i >> 2) * U + u0 + (i & 3);
-    float bw[PR_KQ], bx[PR_XQ];
+    // this lane's B operands over the launch: Wr[k][y U + u0 + 4 cb + j] of column i = 4 y + j of
+    // block cb, and (block zcb = wave / 2 of the Zx product) Wl[k][..], k < 43, with its bias
+    float bw[FNCB][PR_KQ], bx[PR_XQ];
 #pragma unroll
-    for (int q = 0; q < PR_KQ; ++q) {
-        const int k = 4 * (kq0 + q) + gq;
-        bw[q] = (q < PR_KQ1 || kh == 0) ? Wr[(int64_t)k * G4 + col] : 0.0f;
+    for (int cb = 0; cb < FNCB; ++cb) {
+        const int64_t col = (int64_t)(i >> 2) * U + u0 + 4 * cb + (i & 3);
+#pragma unroll
+        for (int q = 0; q < PR_KQ; ++q) {
+            const int k = 4 * (kq0 + q) + gq;
+            bw[cb][q] = (q < PR_KQ1 || kh == 0) ? Wr[(int64_t)k * G4 + col] : 0.0f;
+        }
     }
+    const int zcb = wave >> 1;   // Zx: waves (rb, zcb) for zcb < FNCB
+    const int64_t zcol = (int64_t)(i >> 2) * U + u0 + 4 * (zcb < FNCB ? zcb : 0) + (i & 3);
 #pragma unroll
     for (int q = 0; q < PR_XQ; ++q) {
         const int k = 4 * q + gq;
-        bx[q] = (kh == 0 && k < XI) ? P[OFF_WL + (int64_t)k * G4 + col] : 0.0f;
+        bx[q] = (zcb < FNCB && k < XI) ? P[OFF_WL + (int64_t)k * G4 + zcol] : 0.0f;
     }
-    const float bias = P[OFF_BL + col];
+    const float bias = P[OFF_BL + zcol];
     // this thread's column of the dense32 part of X (c = 11 + tid % 32 for every row it forms)
     const int dc = tid & 31;
     float wp[4];
@@ -341,8 +351,9 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
     for (int a = 0; a < 4; ++a) wp[a] = P[OFF_WP + a * 32 + dc];
     const float bpc = P[OFF_BP + dc];
     for (int x = tid; x < PR_ROWS * XLD; x += 256) (&Xs[0][0])[x] = 0.0f;
-    const bool pt = tid < 4 * B;
-    const int pr = tid >> 2, pu = u0 + (tid & 3);
+    const bool pt = tid < FU * B;
+    const int pr = tid / FU, pj = tid % FU, pu = u0 + pj;
+    const int pc = 16 * (pj >> 2) + (pj & 3);   // the point's local column of gate 0 (+ 4 y)
     float cst = 0.0f;
     if (pt) {
         const int64_t idx = (int64_t)pr * U + pu;
@@ -388,7 +399,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
         if (blockIdx.x == 0)
             for (int r = tid; r < B; r += 256) X[((int64_t)s * B + r) * XLD + XI] = 0.0f;
         __syncthreads();   // Xs complete; the previous step's cell has read Zx
-        if (kh == 0) {
+        if (zcb < FNCB) {
             float av[PR_XQ];
 #pragma unroll
             for (int q = 0; q < PR_XQ; ++q) av[q] = Xs[16 * rb + i][4 * q + gq];
@@ -398,7 +409,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
             for (int q = 0; q < PR_XQ; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bx[q], acc[0], 0, 0, 0);
             fence_end(acc);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Zx[16 * rb + 4 * gq + r][i] = acc[0][r] + bias;
+            for (int r = 0; r < 4; ++r) Zx[16 * rb + 4 * gq + r][16 * zcb + i] = acc[0][r] + bias;
         }
     };
     __syncthreads();   // Xs zeroed before the staging writes
@@ -439,26 +450,36 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
 #pragma unroll
             for (int q = 0; q < PR_KQ; ++q) av[q] = hs && (q < PR_KQ1 || kh == 0) ? hs[4 * q] : 0.0f;
         }
-        // this wave's K half: one accumulation chain in k order (the per-step kernel's lo / hi)
-        rdg::f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
+        // this wave's K half: one accumulation chain per column block in k order (the per-step
+        // kernel's lo / hi), the blocks' chains interleaved
+        rdg::f32x4 acc[FNCB];
+#pragma unroll
+        for (int cb = 0; cb < FNCB; ++cb) acc[cb] = rdg::f32x4{0.f, 0.f, 0.f, 0.f};
         fence_begin(acc);
 #pragma unroll
-        for (int q = 0; q < PR_KQ1; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[q], acc[0], 0, 0, 0);
+        for (int q = 0; q < PR_KQ1; ++q) {
+#pragma unroll
+            for (int cb = 0; cb < FNCB; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[cb][q], acc[cb], 0, 0, 0);
+        }
         if (kh == 0) {
 #pragma unroll
-            for (int q = PR_KQ1; q < PR_KQ; ++q) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[q], acc[0], 0, 0, 0);
+            for (int q = PR_KQ1; q < PR_KQ; ++q) {
+#pragma unroll
+                for (int cb = 0; cb < FNCB; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bw[cb][q], acc[cb], 0, 0, 0);
+            }
         }
         fence_end(acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Zp[kh][16 * rb + 4 * gq + r][i] = acc[0][r];   // C: rows 4 gq + r, column i
+        for (int cb = 0; cb < FNCB; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Zp[kh][16 * rb + 4 * gq + r][16 * cb + i] = acc[cb][r];   // C: rows 4 gq + r, column i
         __syncthreads();
         if (fail_s) break;   // (uniform) a peer's granules never arrived: the timeout flag is raised
         // TF1 LSTMCell (lstm_rec_fwd_kernel's arithmetic) at this thread's point
         if (pt) {
-            const int c0 = tid & 3;
             float z[4];
 #pragma unroll
-            for (int y = 0; y < 4; ++y) z[y] = ((Zp[0][pr][4 * y + c0] + Zp[1][pr][4 * y + c0]) + 0.0f) + Zx[pr][4 * y + c0];
+            for (int y = 0; y < 4; ++y) z[y] = ((Zp[0][pr][pc + 4 * y] + Zp[1][pr][pc + 4 * y]) + 0.0f) + Zx[pr][pc + 4 * y];
             const float gi = sigm(z[0]), gj = tanhf(z[1]), gf = sigm(z[2] + 1.0f), go = sigm(z[3]);
             const float c = fmaf(gf, cst, gi * gj);
             cst = c;
@@ -1569,7 +1590,7 @@ int run_forward(rdl_trainer* t, const float* ob, const float* prev, const float*
     t->loss_in_head = false;
     const float kp = train ? t->cfg.keep_prob : 1.0f;
     if (persistent(t, B)) {   // X, Zx and all T recurrent steps in one launch (it writes the step-0 state rows)
-        hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID), dim3(256), 0, t->stream, P, ob, prev, t->X, state0,
+        hipLaunchKernelGGL(lstm_fwd_persist_kernel, dim3(PR_GRID_F), dim3(256), 0, t->stream, P, ob, prev, t->X, state0,
                            t->G, t->Cs, t->H, (int)B, T, kp, t->cfg.seed, t->cfg.row_base, (const uint32_t*)t->ctl,
                            t->bar, t->hx);
         RDL_CK(hipGetLastError(), "rdl lstm_fwd_persist_kernel");
