@@ -341,17 +341,18 @@ def test_persistent_kernels_many_steps_stay_in_step_with_per_step_path():
     """500 training steps of the reference's 20 windows through the persistent kernels (50
     workgroups exchanging h granules / partial dh every unrolled step; the granule generation
     advances on the device per forward) and through the per-step launches: no hand-off timeout
-    (rdl_get_counter raises on one), the same step count, and parameters that stay within the
-    accumulated f32 reordering of the two paths' gradient sums."""
+    (rdl_get_counter raises on one), the same step count, two persistent runs bitwise equal, and
+    parameters that stay within the accumulated f32 reordering of the two paths' gradient sums."""
     T, B = 10, 20
     ob, prev, t = _batch(T, B, 77)
     params = {}
-    for mode in ("1", "0"):
+    for mode in ("1", "1b", "0"):   # persistent twice (run to run: bitwise), then per-step
         tr = _trainer(T, B, "kl", step_recurrence=mode == "0")
         for _ in range(500):
             tr.step(_t(ob), _t(prev), _t(t))
         assert tr.counter() == 500
         params[mode] = tr.params().cpu().numpy().astype(np.float64)
         tr.close()
+    assert np.array_equal(params["1"], params["1b"])   # fixed-order sums: deterministic
     d = np.abs(params["1"] - params["0"]).max()
     assert d <= 1e-4 * np.abs(params["0"]).max(), d
