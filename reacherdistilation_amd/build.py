@@ -35,7 +35,7 @@ LDFLAGS = ["-shared", f"--offload-arch={ARCH}", "-ldl"]
 # packed-f32 op queued behind MFMAs can read its operands after such a load landed, and lanes
 # 48-63 of gw3b came out different run to run (DESIGN.md §3 "PKWAR", scripts/isa/hazards.py).
 # The packed tanh / split pairs written explicitly as f32x2 stay.
-SRC_FLAGS = {"distill.hip": ["-fno-slp-vectorize"]}
+SRC_FLAGS = {"distill.hip": ["-fno-slp-vectorize"], "ppo.hip": ["-fno-slp-vectorize"]}
 
 
 def src_flags(path):

@@ -9,10 +9,12 @@
 //    (ob, ac, vpred, rew, new) is written t-major so every later pass is coalesced;
 //  * GAE: one env per lane, backward over its horizon; the advantage moments and the
 //    observation filter's sums are deterministic two-level f64 reductions;
-//  * minibatch step: gather (with the filter applied), the two MLPs' forward and backward
-//    as MFMA GEMMs with fused bias / tanh / tanh' epilogues (rd_gemm.h), the clipped
-//    surrogate + value loss per row, fixed-order column sums for the biases and logstd,
-//    and TF1/MpiAdam over the concatenated [pol | vf] vector.  No atomics: deterministic.
+//  * minibatch step, two launches: minibatch_kernel gathers a 32-row tile (filter applied)
+//    and runs both MLPs forward, the clipped surrogate + value loss per row and both
+//    backward passes with the weights in LDS, each workgroup keeping its weight-gradient
+//    sums in registers over its tiles; reduce_adam_kernel sums the per-workgroup partial rows
+//    in a fixed order and runs TF1/MpiAdam over the concatenated [pol | vf] vector.  No
+//    atomics: deterministic.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,16 +24,13 @@
 
 #include "../../include/reacher_ppo.h"
 #include "rd_common.h"
-#include "rd_gemm.h"
 #include "rd_physics.h"
 
 namespace {
 
 constexpr int OBD = 11, HID = 64, ZLD = 12;
-// Hidden activations are stored [row][HLD] with column HID = 1: a weight-gradient GEMM over
-// HID + 1 rows of A^T then yields dW (rows 0..HID-1) AND the bias gradient db (row HID) in
-// one launch, written straight into the flat [W | b] parameter layout (the input batch Z
-// carries the same 1 in column OBD).
+// LDS row strides of the minibatch tiles: inputs z [row][ZLD] with column OBD = 1 (the bias
+// input of dW1), activations [row][HLD] (16-B rows for the float4 broadcast reads)
 constexpr int HLD = HID + 4;
 // policy (MlpPolicy layout of reacher_distill.h)
 constexpr int PW1 = 0, PB1 = PW1 + OBD * HID, PW2 = PB1 + HID, PB2 = PW2 + HID * HID, PW3 = PB2 + HID,
@@ -336,116 +335,337 @@ __global__ __launch_bounds__(64) void logp_old_kernel(const float* params, const
     lpo[r] = -0.5f * (d0 * d0 + d1 * d1) - (ls0 + ls1) - LOG2PI;
 }
 
-// minibatch rows perm[i] -> Z (filtered obs, 12-wide), A, LPO, ATG, RET.  16 lanes per row,
-// one gathered value each (one lane per row left the random-row loads of a 4,096-row
-// minibatch on 16 workgroups: a chain of load latencies)
-constexpr int GATHER_LANES = 16;
-__global__ __launch_bounds__(256) void gather_kernel(const int* perm, int mb, const float* rms, const float* ob,
-                                                     const float* ac, const float* lpo, const float* atarg,
-                                                     const float* ret, float* Z, float* A, float* LPO, float* ATG,
-                                                     float* RET) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int i = (int)(t / GATHER_LANES), j = (int)(t % GATHER_LANES);
-    if (i >= mb) return;
-    const int64_t r = perm[i];
-    if (j < OBD) Z[i * ZLD + j] = clip5((ob[r * OBD + j] - rms[j]) / rms[OBD + j]);
-    else if (j == OBD) Z[i * ZLD + OBD] = 1.0f;   // the bias input of the layer-1 gradient GEMM
-    else if (j == 12) A[2 * i] = ac[2 * r];
-    else if (j == 13) A[2 * i + 1] = ac[2 * r + 1];
-    else if (j == 14) LPO[i] = lpo[r];
-    else {
-        ATG[i] = atarg[r];
-        RET[i] = ret[r];
+// ---- the minibatch step: two launches --------------------------------------------------
+// minibatch_kernel: workgroup b owns the row tiles b, b + G, b + 2G, ... of MB_R rows: it
+// gathers a tile (filter applied), runs both MLPs forward, the clipped surrogate + value
+// loss per row and both backward passes with the weights in LDS, and keeps its share of the
+// weight-gradient sums in registers across its tiles; at the end it writes one partial
+// gradient row in the flat [pol | vf] layout, plus its loss sums in f64.
+// reduce_adam_kernel: fixed-order column sums of the G partial rows -> grad, then Adam.
+// The old path (gather, 11 grouped GEMMs, loss, loss sums, Adam: 15 dependent launches per
+// minibatch) was latency-bound; one tile's whole chain is ~10 k FMAs per thread.
+constexpr int MB_R = 32;                   // rows per tile
+constexpr int MB_H = MB_R / 2;             // rows per wave in the forward / data-gradient phases
+constexpr int MB_G = 256;                  // at most this many workgroups (= partial rows)
+constexpr int W2LD = HID + 1;              // LDS row stride of W2: the transposed reads are conflict-free
+constexpr int PSTR = (P_ALL + 3) & ~3;     // partial row stride (floats)
+constexpr int NSTAT = 8;                   // f64 per workgroup: pol_surr, vf_loss, clipfrac, dlogstd0, dlogstd1
+constexpr int RA_COLS = 32, RA_SLICES = 8; // reduce_adam: 32 columns x 8 row slices per block
+static_assert(MB_R % 2 == 0 && MB_R <= 64 && HID == 64, "one lane per row in the loss phase");
+
+struct MbArgs {
+    const int* perm;                        // the minibatch's rows of the actor batch
+    int mb;
+    const float *params, *rms, *ob, *ac, *lpo, *atarg, *ret;
+    float clip_eps;
+    float* part;                            // [G][PSTR]
+    double* stat;                           // [G][NSTAT]
+    uint32_t* ctl;
+};
+
+struct MbLds {
+    alignas(16) float w1[2][OBD * HID];
+    alignas(16) float b1[2][HID];
+    alignas(16) float w2[2][HID * W2LD];
+    alignas(16) float b2[2][HID];
+    alignas(16) float w3p[HID * 2];
+    alignas(16) float w3v[HID];
+    float b3[4];                            // policy b3[0..1], value c3, -
+    float ls[2];                            // logstd
+    float rm[2 * OBD];                      // filter mean | std
+    alignas(16) float z[MB_R][ZLD];         // column OBD = 1: the bias input of dW1
+    alignas(16) float h1[2][MB_R][HLD];
+    alignas(16) float h2[2][MB_R][HLD];
+    alignas(16) float d2[2][MB_R][HLD];
+    alignas(16) float d1[2][MB_R][HLD];
+    float dm[MB_R][2];
+    float dv[MB_R];
+    double red[5][64];
+};
+
+// parameter i of the flat [pol | vf] vector -> its LDS slot (W2 rows padded to W2LD)
+__device__ __forceinline__ float* mb_slot(MbLds& L, int i) {
+    if (i < VB) {
+        if (i < PB1) return &L.w1[0][i];
+        if (i < PW2) return &L.b1[0][i - PB1];
+        if (i < PB2) return &L.w2[0][((i - PW2) >> 6) * W2LD + ((i - PW2) & 63)];
+        if (i < PW3) return &L.b2[0][i - PB2];
+        if (i < PB3) return &L.w3p[i - PW3];
+        if (i < PLS) return &L.b3[i - PB3];
+        return &L.ls[i - PLS];
     }
+    const int o = i - VB;
+    if (o < VC1) return &L.w1[1][o];
+    if (o < VW2) return &L.b1[1][o - VC1];
+    if (o < VC2) return &L.w2[1][((o - VW2) >> 6) * W2LD + ((o - VW2) & 63)];
+    if (o < VW3) return &L.b2[1][o - VC2];
+    if (o < VC3) return &L.w3v[o - VW3];
+    return &L.b3[2];
 }
 
-// clipped surrogate + value loss per row: dMEAN, dV, and per-block sums of
-// (pol_surr, vf_loss, clipfrac, dlogstd0, dlogstd1)
-__global__ __launch_bounds__(RB) void ppo_loss_kernel(int mb, const float* params, const float* MEAN, const float* V,
-                                                      const float* A, const float* LPO, const float* ATG,
-                                                      const float* RET, float clip_eps, float* dMEAN, float* dV,
-                                                      double* part) {
-    __shared__ double s[5][RB];
-    const int i = blockIdx.x * RB + threadIdx.x;
-    double ps = 0, vl = 0, cf = 0, g0 = 0, g1 = 0;
-    if (i < mb) {
-        const float ls0 = params[PLS], ls1 = params[PLS + 1];
-        const float sd0 = expf(ls0), sd1 = expf(ls1);
-        const float m0 = MEAN[2 * i], m1 = MEAN[2 * i + 1];
-        const float x0 = (A[2 * i] - m0) / sd0, x1 = (A[2 * i + 1] - m1) / sd1;
-        const float lp = -0.5f * (x0 * x0 + x1 * x1) - (ls0 + ls1) - LOG2PI;
-        const float ratio = expf(lp - LPO[i]);
-        const float at = ATG[i];
-        const float s1 = ratio * at;
-        const float rc = fminf(fmaxf(ratio, 1.0f - clip_eps), 1.0f + clip_eps);
-        const float s2 = rc * at;
-        const bool take1 = s1 <= s2;                       // tf.minimum: ties to the first
-        const bool inside = ratio >= 1.0f - clip_eps && ratio <= 1.0f + clip_eps;
-        const float inv = 1.0f / (float)mb;
-        const float dlp = (take1 || inside) ? -at * inv * ratio : 0.0f;
-        dMEAN[2 * i] = dlp * x0 / sd0;
-        dMEAN[2 * i + 1] = dlp * x1 / sd1;
-        const float dv = V[i] - RET[i];
-        dV[i] = 2.0f * dv * inv;
-        ps = -(double)(take1 ? s1 : s2) * inv;
-        vl = (double)dv * dv * inv;
-        cf = fabsf(ratio - 1.0f) > clip_eps ? (double)inv : 0.0;
-        g0 = (double)dlp * (x0 * x0 - 1.0f);
-        g1 = (double)dlp * (x1 * x1 - 1.0f);
-    }
-    s[0][threadIdx.x] = ps; s[1][threadIdx.x] = vl; s[2][threadIdx.x] = cf; s[3][threadIdx.x] = g0; s[4][threadIdx.x] = g1;
-    __syncthreads();
-    for (int w = RB / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
+__global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
+    __shared__ MbLds L;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int net = w >> 1, half = w & 1, r0 = half * MB_H;
+    {   // all loads in flight before the first LDS store (a load-store loop serialises ~37 L2 round trips)
+        constexpr int NQ = (P_ALL + 255) / 256;
+        float pv[NQ];
 #pragma unroll
-            for (int q = 0; q < 5; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + w];
+        for (int q = 0; q < NQ; ++q) pv[q] = tid + q * 256 < P_ALL ? a.params[tid + q * 256] : 0.0f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            if (tid + q * 256 < P_ALL) *mb_slot(L, tid + q * 256) = pv[q];
+    }
+    if (tid < 2 * OBD) L.rm[tid] = a.rms[tid];
+    if (blockIdx.x == 0 && tid < 4) a.ctl[4 + tid] = a.ctl[tid];   // Adam words for reduce_adam_kernel
+    const float inv = 1.0f / (float)a.mb;
+    float a2[32], a1[6], ab = 0.0f, a3 = 0.0f;   // this thread's weight-gradient sums
+#pragma unroll
+    for (int q = 0; q < 32; ++q) a2[q] = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) a1[q] = 0.0f;
+    double ps = 0, vl = 0, cf = 0, g0 = 0, g1 = 0;
+    const int ntiles = (a.mb + MB_R - 1) / MB_R;
+    __syncthreads();
+    for (int tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+        const int i0 = tl * MB_R;
+        // 1. gather: filtered observations into z; the loss lanes keep their row's scalars
+        constexpr int NZ = (MB_R * ZLD + 255) / 256;
+        float zo[NZ];
+#pragma unroll
+        for (int q = 0; q < NZ; ++q) {
+            const int e = tid + q * 256, r = e / ZLD, k = e % ZLD, i = i0 + r;
+            zo[q] = e < MB_R * ZLD && k < OBD && i < a.mb ? a.ob[(int64_t)a.perm[i] * OBD + k] : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < NZ; ++q) {
+            const int e = tid + q * 256, r = e / ZLD, k = e % ZLD, i = i0 + r;
+            if (e < MB_R * ZLD)
+                L.z[r][k] = k == OBD ? 1.0f : i < a.mb ? clip5((zo[q] - L.rm[k]) / L.rm[OBD + k]) : 0.0f;
+        }
+        const int li = i0 + lane;
+        const bool lrow = w < 2 && lane < MB_R && li < a.mb;
+        float ac0 = 0, ac1 = 0, lpo = 0, atg = 0, ret = 0;
+        if (lrow) {
+            const int64_t p = a.perm[li];
+            if (w == 0) {
+                ac0 = a.ac[2 * p]; ac1 = a.ac[2 * p + 1]; lpo = a.lpo[p]; atg = a.atarg[p];
+            } else {
+                ret = a.ret[p];
+            }
+        }
+        __syncthreads();
+        // 2. layer 1, both nets: wave (net, half) computes rows r0.. r0+MB_H, lane = unit
+        float acc[MB_H];
+#pragma unroll
+        for (int i = 0; i < MB_H; ++i) acc[i] = L.b1[net][lane];
+#pragma unroll
+        for (int k = 0; k < OBD; ++k) {
+            const float wk = L.w1[net][k * HID + lane];
+#pragma unroll
+            for (int i = 0; i < MB_H; ++i) acc[i] = fmaf(L.z[r0 + i][k], wk, acc[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < MB_H; ++i) L.h1[net][r0 + i][lane] = tanhf(acc[i]);
+        __syncthreads();
+        // 3. layer 2
+#pragma unroll
+        for (int i = 0; i < MB_H; ++i) acc[i] = L.b2[net][lane];
+#pragma unroll 4
+        for (int k = 0; k < HID; k += 4) {
+            const float w0 = L.w2[net][k * W2LD + lane], w1 = L.w2[net][(k + 1) * W2LD + lane];
+            const float w2 = L.w2[net][(k + 2) * W2LD + lane], w3 = L.w2[net][(k + 3) * W2LD + lane];
+#pragma unroll
+            for (int i = 0; i < MB_H; ++i) {
+                const float4 h = *(const float4*)&L.h1[net][r0 + i][k];
+                acc[i] = fmaf(h.w, w3, fmaf(h.z, w2, fmaf(h.y, w1, fmaf(h.x, w0, acc[i]))));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < MB_H; ++i) L.h2[net][r0 + i][lane] = tanhf(acc[i]);
+        __syncthreads();
+        // 4. heads and the loss, one lane per row: wave 0 the policy, wave 1 the value net
+        if (w == 0 && lane < MB_R) {
+            float m0 = L.b3[0], m1 = L.b3[1];
+#pragma unroll 4
+            for (int k = 0; k < HID; k += 4) {
+                const float4 h = *(const float4*)&L.h2[0][lane][k];
+                m0 = fmaf(h.x, L.w3p[2 * k], m0);         m1 = fmaf(h.x, L.w3p[2 * k + 1], m1);
+                m0 = fmaf(h.y, L.w3p[2 * k + 2], m0);     m1 = fmaf(h.y, L.w3p[2 * k + 3], m1);
+                m0 = fmaf(h.z, L.w3p[2 * k + 4], m0);     m1 = fmaf(h.z, L.w3p[2 * k + 5], m1);
+                m0 = fmaf(h.w, L.w3p[2 * k + 6], m0);     m1 = fmaf(h.w, L.w3p[2 * k + 7], m1);
+            }
+            float dm0 = 0.0f, dm1 = 0.0f;
+            if (lrow) {
+                // TF's min / clip gradient conventions (see oracle/ppo_np.py loss_and_grads)
+                const float ls0 = L.ls[0], ls1 = L.ls[1];
+                const float sd0 = expf(ls0), sd1 = expf(ls1);
+                const float x0 = (ac0 - m0) / sd0, x1 = (ac1 - m1) / sd1;
+                const float lp = -0.5f * (x0 * x0 + x1 * x1) - (ls0 + ls1) - LOG2PI;
+                const float ratio = expf(lp - lpo);
+                const float s1 = ratio * atg;
+                const float rc = fminf(fmaxf(ratio, 1.0f - a.clip_eps), 1.0f + a.clip_eps);
+                const float s2 = rc * atg;
+                const bool take1 = s1 <= s2;                       // tf.minimum: ties to the first
+                const bool inside = ratio >= 1.0f - a.clip_eps && ratio <= 1.0f + a.clip_eps;
+                const float dlp = (take1 || inside) ? -atg * inv * ratio : 0.0f;
+                dm0 = dlp * x0 / sd0;
+                dm1 = dlp * x1 / sd1;
+                ps += -(double)(take1 ? s1 : s2) * inv;
+                cf += fabsf(ratio - 1.0f) > a.clip_eps ? (double)inv : 0.0;
+                g0 += (double)dlp * (x0 * x0 - 1.0f);
+                g1 += (double)dlp * (x1 * x1 - 1.0f);
+            }
+            L.dm[lane][0] = dm0;
+            L.dm[lane][1] = dm1;
+        } else if (w == 1 && lane < MB_R) {
+            float v = L.b3[2];
+#pragma unroll 4
+            for (int k = 0; k < HID; k += 4) {
+                const float4 h = *(const float4*)&L.h2[1][lane][k];
+                v = fmaf(h.w, L.w3v[k + 3], fmaf(h.z, L.w3v[k + 2], fmaf(h.y, L.w3v[k + 1], fmaf(h.x, L.w3v[k], v))));
+            }
+            float dvr = 0.0f;
+            if (lrow) {
+                const float d = v - ret;
+                dvr = 2.0f * d * inv;
+                vl += (double)d * d * inv;
+            }
+            L.dv[lane] = dvr;
+        }
+        __syncthreads();
+        // 5. head backward: D2 = (dY W3^T) * tanh'; the head weight / bias gradients
+#pragma unroll
+        for (int i = 0; i < MB_H; ++i) {
+            const int r = r0 + i;
+            const float h = L.h2[net][r][lane];
+            const float gy = net == 0 ? fmaf(L.dm[r][1], L.w3p[2 * lane + 1], L.dm[r][0] * L.w3p[2 * lane])
+                                      : L.dv[r] * L.w3v[lane];
+            L.d2[net][r][lane] = gy * (1.0f - h * h);
+        }
+        if (w < 3) {
+#pragma unroll 8
+            for (int r = 0; r < MB_R; ++r)
+                a3 = fmaf(L.h2[net][r][lane], w == 2 ? L.dv[r] : L.dm[r][w], a3);
+        } else if (lane < 3) {
+#pragma unroll 8
+            for (int r = 0; r < MB_R; ++r) a3 += lane < 2 ? L.dm[r][lane] : L.dv[r];
+        }
+        __syncthreads();
+        // 6. layer 2 backward: D1 = (D2 W2^T) * tanh' (rows r0..), and dW2 / db2 (k = half 32..)
+#pragma unroll
+        for (int i = 0; i < MB_H; ++i) acc[i] = 0.0f;
+#pragma unroll 4
+        for (int j = 0; j < HID; j += 4) {
+            const float w0 = L.w2[net][lane * W2LD + j], w1 = L.w2[net][lane * W2LD + j + 1];
+            const float w2 = L.w2[net][lane * W2LD + j + 2], w3 = L.w2[net][lane * W2LD + j + 3];
+#pragma unroll
+            for (int i = 0; i < MB_H; ++i) {
+                const float4 d = *(const float4*)&L.d2[net][r0 + i][j];
+                acc[i] = fmaf(d.w, w3, fmaf(d.z, w2, fmaf(d.y, w1, fmaf(d.x, w0, acc[i]))));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < MB_H; ++i) {
+            const float h = L.h1[net][r0 + i][lane];
+            L.d1[net][r0 + i][lane] = acc[i] * (1.0f - h * h);
+        }
+#pragma unroll 2
+        for (int r = 0; r < MB_R; ++r) {
+            const float d = L.d2[net][r][lane];
+            if (half == 0) ab += d;
+#pragma unroll
+            for (int q = 0; q < 32; q += 4) {
+                const float4 h = *(const float4*)&L.h1[net][r][half * 32 + q];
+                a2[q] = fmaf(h.x, d, a2[q]);
+                a2[q + 1] = fmaf(h.y, d, a2[q + 1]);
+                a2[q + 2] = fmaf(h.z, d, a2[q + 2]);
+                a2[q + 3] = fmaf(h.w, d, a2[q + 3]);
+            }
+        }
+        __syncthreads();
+        // 7. dW1 / db1: inputs k = half 6 .. half 6 + 5 (k = OBD: the ones column)
+#pragma unroll 4
+        for (int r = 0; r < MB_R; ++r) {
+            const float d = L.d1[net][r][lane];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) a1[q] = fmaf(L.z[r][half * 6 + q], d, a1[q]);
+        }
         __syncthreads();
     }
-    if (threadIdx.x < 5) part[blockIdx.x * 5 + threadIdx.x] = s[threadIdx.x][0];
-}
-
-// sum the loss partials: dlogstd into the gradient, losses into the epoch accumulators
-// (acc: pol_surr, vf_loss, clipfrac, minibatches); snapshot of the Adam words
-__global__ void loss_final_kernel(const double* part, int nblk, float* grad, double* acc, int accumulate,
-                                  uint32_t* ctl) {
-    if (threadIdx.x != 0) return;
-    double q[5] = {0, 0, 0, 0, 0};
-    for (int b = 0; b < nblk; ++b)
-        for (int k = 0; k < 5; ++k) q[k] += part[b * 5 + k];
-    grad[PLS] = (float)q[3];
-    grad[PLS + 1] = (float)q[4];
-    if (accumulate) {
-        acc[0] += q[0];
-        acc[1] += q[1];
-        acc[2] += q[2];
-        acc[3] += 1.0;
+    // partial gradient row of this workgroup (every slot written by exactly one thread)
+    float* pr = a.part + (int64_t)blockIdx.x * PSTR;
+    const int nb = net ? VB : 0;
+    const int ow2 = nb + (net ? VW2 : PW2), ow1 = nb + (net ? VW1 : PW1), ob1 = nb + (net ? VC1 : PB1);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) pr[ow2 + (half * 32 + q) * HID + lane] = a2[q];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const int k = half * 6 + q;
+        pr[k < OBD ? ow1 + k * HID + lane : ob1 + lane] = a1[q];
     }
-    for (int k = 0; k < 4; ++k) ctl[4 + k] = ctl[k];
+    if (half == 0) pr[nb + (net ? VC2 : PB2) + lane] = ab;
+    if (w == 0) pr[PW3 + 2 * lane] = a3;
+    else if (w == 1) pr[PW3 + 2 * lane + 1] = a3;
+    else if (w == 2) pr[VB + VW3 + lane] = a3;
+    else if (lane < 2) pr[PB3 + lane] = a3;
+    else if (lane == 2) pr[VB + VC3] = a3;
+    if (w == 0) {
+        L.red[0][lane] = ps; L.red[2][lane] = cf; L.red[3][lane] = g0; L.red[4][lane] = g1;
+    } else if (w == 1) {
+        L.red[1][lane] = vl;
+    }
+    __syncthreads();
+    if (tid < 5) {
+        double s = 0.0;
+        for (int l = 0; l < 64; ++l) s += L.red[tid][l];
+        a.stat[(int64_t)blockIdx.x * NSTAT + tid] = s;
+    }
 }
 
-// column HID of a [rows][HLD] activation buffer = 1 (the bias input of the next layer's
-// weight-gradient GEMM); the forward GEMMs write columns 0..HID-1 only
-__global__ __launch_bounds__(256) void ones_column_kernel(float* H, int64_t rows) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r < rows) H[r * HLD + HID] = 1.0f;
-}
-
-struct AdamArgs {
-    const float* grad;
+struct RaArgs {
+    const float* part;
+    const double* stat;
+    int G;
+    float* grad;
     float* params;
     float* m;
     float* v;
     uint32_t* ctl;
+    double* acc;
+    int accumulate;
     float lr, b1, b2, eps;
 };
 
-// MpiAdam.update (= TF1 form) over [pol | vf]; t counts minibatch steps
-__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
-    const int p = blockIdx.x * 256 + threadIdx.x;
+// grad[p] = fixed-order sum of the G partial rows (logstd: of the f64 sums), then MpiAdam.update
+// (= TF1 form) over [pol | vf]; t counts minibatch steps.  Block 0 also folds the loss sums into
+// the epoch accumulators (acc: pol_surr, vf_loss, clipfrac, minibatches).
+__global__ __launch_bounds__(256) void reduce_adam_kernel(RaArgs a) {
+    __shared__ float rs[RA_SLICES][RA_COLS];
+    __shared__ double rq[RA_SLICES][RA_COLS];
+    const int c = threadIdx.x % RA_COLS, s = threadIdx.x / RA_COLS, p = blockIdx.x * RA_COLS + c;
+    const bool lsc = p == PLS || p == PLS + 1;
+    float sum = 0.0f;
+    double q = 0.0;
+    if (p < P_ALL && !lsc) {
+#pragma unroll 8
+        for (int b = s; b < a.G; b += RA_SLICES) sum += a.part[(int64_t)b * PSTR + p];
+    } else if (lsc) {
+        for (int b = s; b < a.G; b += RA_SLICES) q += a.stat[(int64_t)b * NSTAT + 3 + (p - PLS)];
+    }
+    if (blockIdx.x == 0 && c < 3)
+        for (int b = s; b < a.G; b += RA_SLICES) q += a.stat[(int64_t)b * NSTAT + c];
+    rs[s][c] = sum;
+    rq[s][c] = q;
+    __syncthreads();
+    if (s != 0) return;
+    const float g0 = ((rs[0][c] + rs[1][c]) + (rs[2][c] + rs[3][c])) + ((rs[4][c] + rs[5][c]) + (rs[6][c] + rs[7][c]));
+    const double d0 = ((rq[0][c] + rq[1][c]) + (rq[2][c] + rq[3][c])) + ((rq[4][c] + rq[5][c]) + (rq[6][c] + rq[7][c]));
     const uint32_t S = a.ctl[4];
     const float b1p = __uint_as_float(a.ctl[5]), b2p = __uint_as_float(a.ctl[6]);
     if (p < P_ALL) {
-        const float g = a.grad[p];
+        const float g = lsc ? (float)d0 : g0;
+        a.grad[p] = g;
         const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
         float m = a.m[p], v = a.v[p];
         m += (g - m) * (1.0f - a.b1);
@@ -454,10 +674,14 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
         a.v[p] = v;
         a.params[p] -= (m * alpha) / (sqrtf(v) + a.eps);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        a.ctl[0] = S + 1u;
-        a.ctl[1] = __float_as_uint(b1p * a.b1);
-        a.ctl[2] = __float_as_uint(b2p * a.b2);
+    if (blockIdx.x == 0) {
+        if (a.accumulate && c < 3) a.acc[c] += d0;
+        if (a.accumulate && c == 3) a.acc[3] += 1.0;
+        if (c == 0) {
+            a.ctl[0] = S + 1u;
+            a.ctl[1] = __float_as_uint(b1p * a.b1);
+            a.ctl[2] = __float_as_uint(b2p * a.b2);
+        }
     }
 }
 
@@ -522,49 +746,15 @@ struct rdp_trainer {
     float* rms = nullptr;
     int* perm = nullptr;
     std::vector<int> host_perm;
-    // minibatch buffers
-    float *Z = nullptr, *A = nullptr, *LPO = nullptr, *ATG = nullptr, *RET = nullptr;
-    float *H1 = nullptr, *H2 = nullptr, *MEAN = nullptr, *G1 = nullptr, *G2 = nullptr, *V = nullptr;
-    float *dMEAN = nullptr, *dV = nullptr, *D2 = nullptr, *D1 = nullptr, *E2 = nullptr, *E1 = nullptr;
-    float* split = nullptr;
+    // minibatch step: per-workgroup partial gradient rows and loss sums
+    float* mbpart = nullptr;
+    double* mbstat = nullptr;
     float* hist = nullptr;
     uint32_t* ctl = nullptr;
     int64_t part_doubles = 0;
 };
 
 namespace {
-
-constexpr int64_t SPLIT_FLOATS = 4 << 20;
-
-hipError_t mm(rdp_trainer* t, int M, int N, int K, const float* A, int64_t lda, int ta, const float* B, int64_t ldb,
-              int tb, float* C, int64_t ldc, const float* bias = nullptr, int epi = rdg::EPI_NONE,
-              const float* aux = nullptr, int64_t ldaux = 0) {
-    rdg::GemmArgs g{};
-    g.M = M; g.N = N; g.K = K;
-    g.A = A; g.lda = lda; g.ta = ta;
-    g.B = B; g.ldb = ldb; g.tb = tb;
-    g.C = C; g.ldc = ldc;
-    g.bias = bias; g.epi = epi; g.aux = aux; g.ldaux = ldaux;
-    return rdg::gemm(t->stream, g, t->split, SPLIT_FLOATS, t->cus);
-}
-
-rdg::GemmArgs gm(int M, int N, int K, const float* A, int64_t lda, int ta, const float* B, int64_t ldb, int tb,
-                 float* C, int64_t ldc, const float* bias = nullptr, int epi = rdg::EPI_NONE,
-                 const float* aux = nullptr, int64_t ldaux = 0) {
-    rdg::GemmArgs g{};
-    g.M = M; g.N = N; g.K = K;
-    g.A = A; g.lda = lda; g.ta = ta;
-    g.B = B; g.ldb = ldb; g.tb = tb;
-    g.C = C; g.ldc = ldc;
-    g.bias = bias; g.epi = epi; g.aux = aux; g.ldaux = ldaux;
-    return g;
-}
-
-// the policy's and the value net's GEMM of one layer as one grouped launch (rdg::gemm2)
-hipError_t mm2(rdp_trainer* t, const rdg::GemmArgs& pol, const rdg::GemmArgs& vf) {
-    return rdg::gemm2(t->stream, pol, vf, t->split, SPLIT_FLOATS, t->cus);
-}
-
 
 #define RDP_CK(call, what) RD_HIP((call), what)
 
@@ -601,53 +791,16 @@ int run_rollout(rdp_trainer* t) {
 
 int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
     const int mb = t->mb;
-    const float* P = t->params;
-    float* g = t->grad;
-    const float* Pv = P + VB;
-    float* gv = g + VB;
-    const float eps = t->cfg.clip_param * t->lrmult;
-    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(((int64_t)mb * GATHER_LANES + 255) / 256)), dim3(256), 0,
-                       t->stream, perm, mb,
-                       (const float*)t->rms, (const float*)t->ob, (const float*)t->ac, (const float*)t->lpo,
-                       (const float*)t->atarg, (const float*)t->ret, t->Z, t->A, t->LPO, t->ATG, t->RET);
-    RDP_CK(hipGetLastError(), "rdp gather");
-    // forward: layer k of the policy and of the value net in one launch
-    RDP_CK(mm2(t, gm(mb, HID, OBD, t->Z, ZLD, 0, P + PW1, HID, 0, t->H1, HLD, P + PB1, rdg::EPI_TANH),
-               gm(mb, HID, OBD, t->Z, ZLD, 0, Pv + VW1, HID, 0, t->G1, HLD, Pv + VC1, rdg::EPI_TANH)),
-           "rdp pol1 vf1");
-    RDP_CK(mm2(t, gm(mb, HID, HID, t->H1, HLD, 0, P + PW2, HID, 0, t->H2, HLD, P + PB2, rdg::EPI_TANH),
-               gm(mb, HID, HID, t->G1, HLD, 0, Pv + VW2, HID, 0, t->G2, HLD, Pv + VC2, rdg::EPI_TANH)),
-           "rdp pol2 vf2");
-    RDP_CK(mm2(t, gm(mb, 2, HID, t->H2, HLD, 0, P + PW3, 2, 0, t->MEAN, 2, P + PB3),
-               gm(mb, 1, HID, t->G2, HLD, 0, Pv + VW3, 1, 0, t->V, 1, Pv + VC3)),
-           "rdp pol3 vf3");
-    const int lblk = (mb + RB - 1) / RB;
-    hipLaunchKernelGGL(ppo_loss_kernel, dim3(lblk), dim3(RB), 0, t->stream, mb, P, (const float*)t->MEAN,
-                       (const float*)t->V, (const float*)t->A, (const float*)t->LPO, (const float*)t->ATG,
-                       (const float*)t->RET, eps, t->dMEAN, t->dV, t->part);
-    hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, t->stream, (const double*)t->part, lblk, g, t->acc,
-                       last_epoch ? 1 : 0, t->ctl);
-    RDP_CK(hipGetLastError(), "rdp loss");
-    // backward, policy and value side by side: [dW; db] of a layer in one GEMM (the ones
-    // column of its input), then the data gradient with tanh' fused
-    RDP_CK(mm2(t, gm(HID + 1, 2, mb, t->H2, HLD, 1, t->dMEAN, 2, 0, g + PW3, 2),
-               gm(HID + 1, 1, mb, t->G2, HLD, 1, t->dV, 1, 0, gv + VW3, 1)),
-           "rdp gW3 gV3");
-    RDP_CK(mm2(t, gm(mb, HID, 2, t->dMEAN, 2, 0, P + PW3, 2, 1, t->D2, HID, nullptr, rdg::EPI_DTANH, t->H2, HLD),
-               gm(mb, HID, 1, t->dV, 1, 0, Pv + VW3, 1, 1, t->E2, HID, nullptr, rdg::EPI_DTANH, t->G2, HLD)),
-           "rdp d2 e2");
-    RDP_CK(mm2(t, gm(HID + 1, HID, mb, t->H1, HLD, 1, t->D2, HID, 0, g + PW2, HID),
-               gm(HID + 1, HID, mb, t->G1, HLD, 1, t->E2, HID, 0, gv + VW2, HID)),
-           "rdp gW2 gV2");
-    RDP_CK(mm2(t, gm(mb, HID, HID, t->D2, HID, 0, P + PW2, HID, 1, t->D1, HID, nullptr, rdg::EPI_DTANH, t->H1, HLD),
-               gm(mb, HID, HID, t->E2, HID, 0, Pv + VW2, HID, 1, t->E1, HID, nullptr, rdg::EPI_DTANH, t->G1, HLD)),
-           "rdp d1 e1");
-    RDP_CK(mm2(t, gm(OBD + 1, HID, mb, t->Z, ZLD, 1, t->D1, HID, 0, g + PW1, HID),
-               gm(OBD + 1, HID, mb, t->Z, ZLD, 1, t->E1, HID, 0, gv + VW1, HID)),
-           "rdp gW1 gV1");
-    AdamArgs aa{t->grad, t->params, t->m, t->v, t->ctl, t->cfg.optim_stepsize * t->lrmult, 0.9f, 0.999f, 1e-8f};
-    hipLaunchKernelGGL(adam_kernel, dim3((P_ALL + 255) / 256), dim3(256), 0, t->stream, aa);
-    RDP_CK(hipGetLastError(), "rdp adam");
+    const int ntiles = (mb + MB_R - 1) / MB_R, G = ntiles < MB_G ? ntiles : MB_G;
+    MbArgs a{perm, mb, t->params, t->rms, t->ob, t->ac, t->lpo, t->atarg, t->ret,
+             t->cfg.clip_param * t->lrmult, t->mbpart, t->mbstat, t->ctl};
+    hipLaunchKernelGGL(minibatch_kernel, dim3((unsigned)G), dim3(256), 0, t->stream, a);
+    RDP_CK(hipGetLastError(), "rdp minibatch_kernel");
+    RaArgs r{t->mbpart, t->mbstat, G, t->grad, t->params, t->m, t->v, t->ctl, t->acc, last_epoch ? 1 : 0,
+             t->cfg.optim_stepsize * t->lrmult, 0.9f, 0.999f, 1e-8f};
+    hipLaunchKernelGGL(reduce_adam_kernel, dim3((P_ALL + RA_COLS - 1) / RA_COLS), dim3(RA_SLICES * RA_COLS), 0,
+                       t->stream, r);
+    RDP_CK(hipGetLastError(), "rdp reduce_adam_kernel");
     return RD_OK;
 }
 
@@ -716,7 +869,7 @@ int rdp_create(rdp_trainer** out, const rdp_config* cfg, int device, void* hip_s
     t->S = S;
     t->mb = cfg->optim_batchsize > 0 ? cfg->optim_batchsize : (int)S;
     t->host_perm.resize((size_t)cfg->optim_epochs * S);
-    const int64_t n = t->n, mb = t->mb;
+    const int64_t n = t->n;
     hipError_t e = hipSuccess;
     auto af = [&](float** p, int64_t cnt) {
         if (e == hipSuccess) e = hipMalloc((void**)p, sizeof(float) * (size_t)(cnt > 0 ? cnt : 1));
@@ -742,23 +895,13 @@ int rdp_create(rdp_trainer** out, const rdp_config* cfg, int device, void* hip_s
     ad(&t->acc, 4);
     af(&t->rms, 2 * OBD);
     ai(&t->perm, (int64_t)cfg->optim_epochs * S);
-    af(&t->Z, mb * ZLD); af(&t->A, 2 * mb); af(&t->LPO, mb); af(&t->ATG, mb); af(&t->RET, mb);
-    af(&t->H1, mb * HLD); af(&t->H2, mb * HLD); af(&t->MEAN, 2 * mb); af(&t->G1, mb * HLD); af(&t->G2, mb * HLD);
-    af(&t->V, mb); af(&t->dMEAN, 2 * mb); af(&t->dV, mb); af(&t->D2, mb * HID); af(&t->D1, mb * HID);
-    af(&t->E2, mb * HID); af(&t->E1, mb * HID);
-    af(&t->split, SPLIT_FLOATS);
+    af(&t->mbpart, (int64_t)MB_G * PSTR);
+    ad(&t->mbstat, (int64_t)MB_G * NSTAT);
     af(&t->hist, (int64_t)t->cfg.metrics_len * N_MET);
     if (e == hipSuccess) e = hipMalloc((void**)&t->ctl, sizeof(uint32_t) * 8);
     if (e != hipSuccess) {
         rdp_destroy(t);
         return rd::hip_fail(e, "rdp_create: allocation");
-    }
-    for (float* h : {t->H1, t->H2, t->G1, t->G2})
-        hipLaunchKernelGGL(ones_column_kernel, dim3((unsigned)((mb + 255) / 256)), dim3(256), 0, t->stream, h,
-                           (int64_t)mb);
-    if ((e = hipGetLastError()) != hipSuccess) {
-        rdp_destroy(t);
-        return rd::hip_fail(e, "rdp_create: ones columns");
     }
     if (int rc = rdp_reset(t)) {
         rdp_destroy(t);
@@ -773,9 +916,8 @@ int rdp_destroy(rdp_trainer* t) {
     rd::DeviceGuard dg(t->device);
     void* bufs[] = {t->params, t->m, t->v, t->own_grad, t->state, t->ep_ret, t->new_next, t->it_ret, t->it_eps,
                     t->ep_step, t->ep_idx, t->ob, t->ac, t->vpred, t->rew, t->newf, t->nextv, t->adv, t->ret,
-                    t->atarg, t->lpo, t->rms_sums, t->part, t->stats, t->acc, t->rms, t->perm, t->Z, t->A, t->LPO,
-                    t->ATG, t->RET, t->H1, t->H2, t->MEAN, t->G1, t->G2, t->V, t->dMEAN, t->dV, t->D2, t->D1,
-                    t->E2, t->E1, t->split, t->hist, t->ctl};
+                    t->atarg, t->lpo, t->rms_sums, t->part, t->stats, t->acc, t->rms, t->perm, t->mbpart,
+                    t->mbstat, t->hist, t->ctl};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     delete t;

@@ -60,6 +60,10 @@ def cpu_baseline(n=64, T=50, mb=64, seconds=4.0):
 
 def main():
     n, T, mb, iters = 4096, 50, 4096, 40
+    if "--mb" in sys.argv:                                 # e.g. --mb 64: the reference's minibatch
+        mb = int(sys.argv[sys.argv.index("--mb") + 1])
+    if "--iters" in sys.argv:
+        iters = int(sys.argv[sys.argv.index("--iters") + 1])
     tr = PPOTrainer(PPOConfig(n_envs=n, horizon=T, optim_batchsize=mb, max_timesteps=n * T * iters), device="cuda:0")
     tr.iterate()
     torch.cuda.synchronize()

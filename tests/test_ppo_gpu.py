@@ -69,8 +69,12 @@ def test_actor_batch_matches_oracle():
     np.testing.assert_allclose(std, rms.std, rtol=1e-4, atol=1e-6)
 
 
-def test_full_batch_gradient_matches_oracle():
-    tr = _trainer(optim_epochs=1, optim_batchsize=0)
+@pytest.mark.parametrize("n,T", [(256, 64), (255, 63), (1, 50), (3, 7)])
+def test_full_batch_gradient_matches_oracle(n, T):
+    """One minibatch over the whole actor batch: 512 / 503 32-row tiles (more than the 256
+    workgroups of minibatch_kernel, so workgroups carry sums over several tiles; 255 x 63 ends
+    in a ragged tile), and 2 / 1 tiles (50 and 21 rows: padded rows must add nothing)."""
+    tr = _trainer(n_envs=n, horizon=T, optim_epochs=1, optim_batchsize=0)
     tr.iterate()                                         # one update: the policy moves off the rollout policy
     pol, vf = tr.policy().cpu().numpy(), tr.value().cpu().numpy()
     mean0, std0 = (x.cpu().numpy().astype(np.float64) for x in tr.obfilter())
