@@ -28,9 +28,9 @@
 
 namespace {
 
-constexpr int OBD = 11, HID = 64, ZLD = 12;
+constexpr int OBD = 11, HID = 64, ZLD = 16;
 // LDS row strides of the minibatch tiles: inputs z [row][ZLD] with column OBD = 1 (the bias
-// input of dW1), activations [row][HLD] (16-B rows for the float4 broadcast reads)
+// input of dW1) and columns 12-15 = 0 (the MFMA's 16-row dW1 block), activations [row][HLD]
 constexpr int HLD = HID + 4;
 // policy (MlpPolicy layout of reacher_distill.h)
 constexpr int PW1 = 0, PB1 = PW1 + OBD * HID, PW2 = PB1 + HID, PB2 = PW2 + HID * HID, PW3 = PB2 + HID,
@@ -343,15 +343,28 @@ __global__ __launch_bounds__(64) void logp_old_kernel(const float* params, const
 // gradient row in the flat [pol | vf] layout, plus its loss sums in f64.
 // reduce_adam_kernel: fixed-order column sums of the G partial rows -> grad, then Adam.
 // The old path (gather, 11 grouped GEMMs, loss, loss sums, Adam: 15 dependent launches per
-// minibatch) was latency-bound; one tile's whole chain is ~10 k FMAs per thread.
+// minibatch) was latency-bound.  The GEMM-shaped parts of a tile (layers 1-2 forward, the
+// layer-2 data gradient, dW2, dW1) run on v_mfma_f32_16x16x4_f32 (exact f32 products; a
+// VALU form with broadcast LDS operands measured 10 + 13 us per tile for layer 2 alone).
 constexpr int MB_R = 32;                   // rows per tile
 constexpr int MB_H = MB_R / 2;             // rows per wave in the forward / data-gradient phases
 constexpr int MB_G = 256;                  // at most this many workgroups (= partial rows)
-constexpr int W2LD = HID + 1;              // LDS row stride of W2: the transposed reads are conflict-free
+constexpr int W2LD = HID + 4;              // LDS row stride of W2 (B operands read both ways)
 constexpr int PSTR = (P_ALL + 3) & ~3;     // partial row stride (floats)
 constexpr int NSTAT = 8;                   // f64 per workgroup: pol_surr, vf_loss, clipfrac, dlogstd0, dlogstd1
 constexpr int RA_COLS = 32, RA_SLICES = 8; // reduce_adam: 32 columns x 8 row slices per block
-static_assert(MB_R % 2 == 0 && MB_R <= 64 && HID == 64, "one lane per row in the loss phase");
+static_assert(MB_R == 32 && HID == 64 && PB1 == OBD * HID && VC1 == OBD * HID,
+              "two 16-row MFMA blocks per tile; b1 follows W1");
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// tanh as 1 - 2 / (e^{2|x|} + 1) with the sign of x: v_exp + v_rcp (|error| < 3e-7)
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float t = 1.0f - __fdividef(2.0f, __expf(2.0f * fabsf(x)) + 1.0f);
+    return copysignf(t, x);
+}
 
 struct MbArgs {
     const int* perm;                        // the minibatch's rows of the actor batch
@@ -364,8 +377,7 @@ struct MbArgs {
 };
 
 struct MbLds {
-    alignas(16) float w1[2][OBD * HID];
-    alignas(16) float b1[2][HID];
+    alignas(16) float w1[2][(OBD + 1) * HID];   // W1 rows, then b1 as row OBD (the ones column of z)
     alignas(16) float w2[2][HID * W2LD];
     alignas(16) float b2[2][HID];
     alignas(16) float w3p[HID * 2];
@@ -386,8 +398,7 @@ struct MbLds {
 // parameter i of the flat [pol | vf] vector -> its LDS slot (W2 rows padded to W2LD)
 __device__ __forceinline__ float* mb_slot(MbLds& L, int i) {
     if (i < VB) {
-        if (i < PB1) return &L.w1[0][i];
-        if (i < PW2) return &L.b1[0][i - PB1];
+        if (i < PW2) return &L.w1[0][i];        // W1 | b1 (PB1 = 11 x 64)
         if (i < PB2) return &L.w2[0][((i - PW2) >> 6) * W2LD + ((i - PW2) & 63)];
         if (i < PW3) return &L.b2[0][i - PB2];
         if (i < PB3) return &L.w3p[i - PW3];
@@ -395,8 +406,7 @@ __device__ __forceinline__ float* mb_slot(MbLds& L, int i) {
         return &L.ls[i - PLS];
     }
     const int o = i - VB;
-    if (o < VC1) return &L.w1[1][o];
-    if (o < VW2) return &L.b1[1][o - VC1];
+    if (o < VW2) return &L.w1[1][o];
     if (o < VC2) return &L.w2[1][((o - VW2) >> 6) * W2LD + ((o - VW2) & 63)];
     if (o < VW3) return &L.b2[1][o - VC2];
     if (o < VC3) return &L.w3v[o - VW3];
@@ -419,11 +429,17 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
     if (tid < 2 * OBD) L.rm[tid] = a.rms[tid];
     if (blockIdx.x == 0 && tid < 4) a.ctl[4 + tid] = a.ctl[tid];   // Adam words for reduce_adam_kernel
     const float inv = 1.0f / (float)a.mb;
-    float a2[32], a1[6], ab = 0.0f, a3 = 0.0f;   // this thread's weight-gradient sums
+    // this wave's weight-gradient blocks: dW2 rows 32 half + 16 kb.., columns 16 jb..; dW1 | db1
+    // columns 32 half + 16 jj..; plus db2 (half 0) and one head-gradient slot
+    const int lr = lane & 15, lk = lane >> 4;
+    f32x4 a2[2][4], a1[2];
+    float ab = 0.0f, a3 = 0.0f;
 #pragma unroll
-    for (int q = 0; q < 32; ++q) a2[q] = 0.0f;
+    for (int kb = 0; kb < 2; ++kb) {
+        a1[kb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int q = 0; q < 6; ++q) a1[q] = 0.0f;
+        for (int jb = 0; jb < 4; ++jb) a2[kb][jb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
     double ps = 0, vl = 0, cf = 0, g0 = 0, g1 = 0;
     const int ntiles = (a.mb + MB_R - 1) / MB_R;
     __syncthreads();
@@ -441,7 +457,7 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
         for (int q = 0; q < NZ; ++q) {
             const int e = tid + q * 256, r = e / ZLD, k = e % ZLD, i = i0 + r;
             if (e < MB_R * ZLD)
-                L.z[r][k] = k == OBD ? 1.0f : i < a.mb ? clip5((zo[q] - L.rm[k]) / L.rm[OBD + k]) : 0.0f;
+                L.z[r][k] = k == OBD ? 1.0f : k > OBD ? 0.0f : i < a.mb ? clip5((zo[q] - L.rm[k]) / L.rm[OBD + k]) : 0.0f;
         }
         const int li = i0 + lane;
         const bool lrow = w < 2 && lane < MB_R && li < a.mb;
@@ -455,34 +471,37 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
             }
         }
         __syncthreads();
-        // 2. layer 1, both nets: wave (net, half) computes rows r0.. r0+MB_H, lane = unit
-        float acc[MB_H];
+        // 2. layer 1, both nets: wave (net, half) computes rows r0 .. r0 + 15 as four 16 x 16
+        //    MFMA blocks over k = 0..11 (b1 rides in as row 11 of W1 against z's ones column)
+        f32x4 c[4];
 #pragma unroll
-        for (int i = 0; i < MB_H; ++i) acc[i] = L.b1[net][lane];
+        for (int cb = 0; cb < 4; ++cb) {
+            c[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int k = 0; k < OBD; ++k) {
-            const float wk = L.w1[net][k * HID + lane];
-#pragma unroll
-            for (int i = 0; i < MB_H; ++i) acc[i] = fmaf(L.z[r0 + i][k], wk, acc[i]);
+            for (int s = 0; s < 3; ++s)
+                c[cb] = mfma4(L.z[r0 + lr][4 * s + lk], L.w1[net][(4 * s + lk) * HID + 16 * cb + lr], c[cb]);
         }
 #pragma unroll
-        for (int i = 0; i < MB_H; ++i) L.h1[net][r0 + i][lane] = tanhf(acc[i]);
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) L.h1[net][r0 + 4 * lk + i][16 * cb + lr] = tanh_fast(c[cb][i]);
         __syncthreads();
-        // 3. layer 2
+        // 3. layer 2: C starts at b2, k = 0..63
 #pragma unroll
-        for (int i = 0; i < MB_H; ++i) acc[i] = L.b2[net][lane];
-#pragma unroll 4
-        for (int k = 0; k < HID; k += 4) {
-            const float w0 = L.w2[net][k * W2LD + lane], w1 = L.w2[net][(k + 1) * W2LD + lane];
-            const float w2 = L.w2[net][(k + 2) * W2LD + lane], w3 = L.w2[net][(k + 3) * W2LD + lane];
-#pragma unroll
-            for (int i = 0; i < MB_H; ++i) {
-                const float4 h = *(const float4*)&L.h1[net][r0 + i][k];
-                acc[i] = fmaf(h.w, w3, fmaf(h.z, w2, fmaf(h.y, w1, fmaf(h.x, w0, acc[i]))));
-            }
+        for (int cb = 0; cb < 4; ++cb) {
+            const float b = L.b2[net][16 * cb + lr];
+            c[cb] = f32x4{b, b, b, b};
         }
 #pragma unroll
-        for (int i = 0; i < MB_H; ++i) L.h2[net][r0 + i][lane] = tanhf(acc[i]);
+        for (int s = 0; s < HID / 4; ++s) {
+            const float av = L.h1[net][r0 + lr][4 * s + lk];
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) c[cb] = mfma4(av, L.w2[net][(4 * s + lk) * W2LD + 16 * cb + lr], c[cb]);
+        }
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) L.h2[net][r0 + 4 * lk + i][16 * cb + lr] = tanh_fast(c[cb][i]);
         __syncthreads();
         // 4. heads and the loss, one lane per row: wave 0 the policy, wave 1 the value net
         if (w == 0 && lane < MB_R) {
@@ -552,58 +571,63 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
             for (int r = 0; r < MB_R; ++r) a3 += lane < 2 ? L.dm[r][lane] : L.dv[r];
         }
         __syncthreads();
-        // 6. layer 2 backward: D1 = (D2 W2^T) * tanh' (rows r0..), and dW2 / db2 (k = half 32..)
+        // 6. layer 2 backward: D1 = (D2 W2^T) * tanh' for rows r0.. (B = W2 read transposed),
+        //    then dW2 += H1^T D2 over the tile's 32 rows (k = 32 half ..), and db2 (half 0)
 #pragma unroll
-        for (int i = 0; i < MB_H; ++i) acc[i] = 0.0f;
-#pragma unroll 4
-        for (int j = 0; j < HID; j += 4) {
-            const float w0 = L.w2[net][lane * W2LD + j], w1 = L.w2[net][lane * W2LD + j + 1];
-            const float w2 = L.w2[net][lane * W2LD + j + 2], w3 = L.w2[net][lane * W2LD + j + 3];
+        for (int cb = 0; cb < 4; ++cb) c[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-            for (int i = 0; i < MB_H; ++i) {
-                const float4 d = *(const float4*)&L.d2[net][r0 + i][j];
-                acc[i] = fmaf(d.w, w3, fmaf(d.z, w2, fmaf(d.y, w1, fmaf(d.x, w0, acc[i]))));
-            }
+        for (int s = 0; s < HID / 4; ++s) {
+            const float av = L.d2[net][r0 + lr][4 * s + lk];
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) c[cb] = mfma4(av, L.w2[net][(16 * cb + lr) * W2LD + 4 * s + lk], c[cb]);
         }
 #pragma unroll
-        for (int i = 0; i < MB_H; ++i) {
-            const float h = L.h1[net][r0 + i][lane];
-            L.d1[net][r0 + i][lane] = acc[i] * (1.0f - h * h);
-        }
-#pragma unroll 2
-        for (int r = 0; r < MB_R; ++r) {
-            const float d = L.d2[net][r][lane];
-            if (half == 0) ab += d;
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-            for (int q = 0; q < 32; q += 4) {
-                const float4 h = *(const float4*)&L.h1[net][r][half * 32 + q];
-                a2[q] = fmaf(h.x, d, a2[q]);
-                a2[q + 1] = fmaf(h.y, d, a2[q + 1]);
-                a2[q + 2] = fmaf(h.z, d, a2[q + 2]);
-                a2[q + 3] = fmaf(h.w, d, a2[q + 3]);
+            for (int i = 0; i < 4; ++i) {
+                const int r = r0 + 4 * lk + i;
+                const float h = L.h1[net][r][16 * cb + lr];
+                L.d1[net][r][16 * cb + lr] = c[cb][i] * (1.0f - h * h);
             }
+#pragma unroll
+        for (int s = 0; s < MB_R / 4; ++s) {
+            const float h0 = L.h1[net][4 * s + lk][32 * half + lr], h1 = L.h1[net][4 * s + lk][32 * half + 16 + lr];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) {
+                const float d = L.d2[net][4 * s + lk][16 * jb + lr];
+                a2[0][jb] = mfma4(h0, d, a2[0][jb]);
+                a2[1][jb] = mfma4(h1, d, a2[1][jb]);
+            }
+        }
+        if (half == 0) {
+#pragma unroll 8
+            for (int r = 0; r < MB_R; ++r) ab += L.d2[net][r][lane];
         }
         __syncthreads();
-        // 7. dW1 / db1: inputs k = half 6 .. half 6 + 5 (k = OBD: the ones column)
-#pragma unroll 4
-        for (int r = 0; r < MB_R; ++r) {
-            const float d = L.d1[net][r][lane];
+        // 7. dW1 | db1 += z^T D1: one 16-row block (k = 0..11 used, 12-15 zero), columns 32 half ..
 #pragma unroll
-            for (int q = 0; q < 6; ++q) a1[q] = fmaf(L.z[r][half * 6 + q], d, a1[q]);
+        for (int s = 0; s < MB_R / 4; ++s) {
+            const float zv = L.z[4 * s + lk][lr];
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) a1[jj] = mfma4(zv, L.d1[net][4 * s + lk][32 * half + 16 * jj + lr], a1[jj]);
         }
         __syncthreads();
     }
     // partial gradient row of this workgroup (every slot written by exactly one thread)
     float* pr = a.part + (int64_t)blockIdx.x * PSTR;
     const int nb = net ? VB : 0;
-    const int ow2 = nb + (net ? VW2 : PW2), ow1 = nb + (net ? VW1 : PW1), ob1 = nb + (net ? VC1 : PB1);
+    const int ow2 = nb + (net ? VW2 : PW2), ow1 = nb + (net ? VW1 : PW1);
 #pragma unroll
-    for (int q = 0; q < 32; ++q) pr[ow2 + (half * 32 + q) * HID + lane] = a2[q];
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-        const int k = half * 6 + q;
-        pr[k < OBD ? ow1 + k * HID + lane : ob1 + lane] = a1[q];
-    }
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pr[ow2 + (32 * half + 16 * kb + 4 * lk + i) * HID + 16 * jb + lr] = a2[kb][jb][i];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (4 * lk + i <= OBD) pr[ow1 + (4 * lk + i) * HID + 32 * half + 16 * jj + lr] = a1[jj][i];   // row OBD = db1
     if (half == 0) pr[nb + (net ? VC2 : PB2) + lane] = ab;
     if (w == 0) pr[PW3 + 2 * lane] = a3;
     else if (w == 1) pr[PW3 + 2 * lane + 1] = a3;
