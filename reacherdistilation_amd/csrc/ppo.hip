@@ -3,10 +3,11 @@
 // parallel envs.
 //
 // MI355X mapping:
-//  * rollout: one env per lane for the whole horizon; the policy and value MLPs (2 x 64
-//    tanh each) run per lane as unrolled f32 FMA chains over weights broadcast from LDS
-//    (40 KB), the env step is the shared Reacher physics (rd_physics.h); the actor batch
-//    (ob, ac, vpred, rew, new) is written t-major so every later pass is coalesced;
+//  * rollout: 32 envs per workgroup for the whole horizon, one per lane of wave 0 (the
+//    shared Reacher physics of rd_physics.h, noise, episode clocks); the 32 envs' policy and
+//    value MLPs (2 x 64 tanh each) run on f32 MFMA by all four waves with the weights in LDS;
+//    the actor batch (ob, ac, vpred, rew, new) is written t-major so every later pass is
+//    coalesced;
 //  * GAE: one env per lane, backward over its horizon; the advantage moments and the
 //    observation filter's sums are deterministic two-level f64 reductions;
 //  * minibatch step, two launches: minibatch_kernel gathers a 32-row tile (filter applied)
@@ -18,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <new>
 #include <random>
 #include <vector>
@@ -49,62 +51,6 @@ constexpr float LOG2PI = 1.8378770664093453f;
 
 __device__ __forceinline__ float clip5(float x) { return fminf(fmaxf(x, -5.0f), 5.0f); }
 
-// 2 x 64 tanh hidden stack of one lane: weights broadcast from LDS (L = W1 | b1 | W2 | b2),
-// the lane's input z and first hidden layer in per-lane LDS columns (zs [11][64], h1s
-// [64][64], lane-contiguous) so the k loops stay rolled and only the 64 accumulators of
-// the current layer live in registers.
-__device__ __forceinline__ void hidden(const float* L, const float* zs, float* h1s, int lane, float (&h2)[HID]) {
-    float acc[HID];
-#pragma unroll
-    for (int j = 0; j < HID; ++j) acc[j] = L[PB1 + j];
-#pragma unroll 1
-    for (int k = 0; k < OBD; ++k) {
-        const float zk = zs[k * 64 + lane];
-#pragma unroll
-        for (int j = 0; j < HID; ++j) acc[j] = fmaf(zk, L[PW1 + k * HID + j], acc[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < HID; ++j) h1s[j * 64 + lane] = tanhf(acc[j]);
-#pragma unroll
-    for (int j = 0; j < HID; ++j) h2[j] = L[PB2 + j];
-#pragma unroll 2
-    for (int k = 0; k < HID; ++k) {
-        const float hk = h1s[k * 64 + lane];
-#pragma unroll
-        for (int j = 0; j < HID; ++j) h2[j] = fmaf(hk, L[PW2 + k * HID + j], h2[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < HID; ++j) h2[j] = tanhf(h2[j]);
-}
-
-__device__ __forceinline__ void policy_mean(const float* L, const float* zs, float* h1s, int lane, float& m0,
-                                            float& m1) {
-    float h2[HID];
-    hidden(L, zs, h1s, lane, h2);
-    m0 = L[PB3];
-    m1 = L[PB3 + 1];
-#pragma unroll
-    for (int k = 0; k < HID; ++k) {
-        m0 = fmaf(h2[k], L[PW3 + 2 * k], m0);
-        m1 = fmaf(h2[k], L[PW3 + 2 * k + 1], m1);
-    }
-}
-
-__device__ __forceinline__ float value(const float* V, const float* zs, float* h1s, int lane) {
-    float h2[HID];
-    hidden(V, zs, h1s, lane, h2);   // the value net has the same W1 b1 W2 b2 offsets
-    float v = V[VC3];
-#pragma unroll
-    for (int k = 0; k < HID; ++k) v = fmaf(h2[k], V[VW3 + k], v);
-    return v;
-}
-
-// z = clip((ob - mean) / std, -5, 5) into the lane's LDS column
-__device__ __forceinline__ void normalize(const float* ob, const float* rms, float* zs, int lane) {
-#pragma unroll
-    for (int k = 0; k < OBD; ++k) zs[k * 64 + lane] = clip5((ob[k] - rms[k]) / rms[OBD + k]);
-}
-
 // filter statistics as the policy graph uses them (mpi_running_mean_std: float32 mean/std)
 __global__ void rms_finalize_kernel(const double* s, float* rms) {
     const int k = threadIdx.x;
@@ -132,80 +78,6 @@ struct RolloutArgs {
     float* it_eps;         // [n]
     float *ob, *ac, *vpred, *rew, *newf, *nextv;
 };
-
-__global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
-    __shared__ float L[P_ALL + 2 * OBD];
-    __shared__ float zs[OBD * 64], h1s[HID * 64];
-    const int lane = threadIdx.x;
-    for (int i = threadIdx.x; i < P_ALL; i += 64) L[i] = a.params[i];
-    if (threadIdx.x < 2 * OBD) L[P_ALL + threadIdx.x] = a.rms[threadIdx.x];
-    __syncthreads();
-    const int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (e >= a.n) return;
-    const float* Lp = L;
-    const float* Lv = L + VB;
-    const float* rms = L + P_ALL;
-    const int64_t n = a.n;
-    rd::State st;
-    st.q0 = a.state[e]; st.q1 = a.state[n + e]; st.v0 = a.state[2 * n + e]; st.v1 = a.state[3 * n + e];
-    st.tx = a.state[4 * n + e]; st.ty = a.state[5 * n + e]; st.dx = a.state[6 * n + e]; st.dy = a.state[7 * n + e];
-    int step = a.ep_step[e], epi = a.ep_idx[e];
-    float ret = a.ep_ret[e], newf = a.new_next[e], it_ret = 0.f, it_eps = 0.f;
-    const float s0 = expf(Lp[PLS]), s1 = expf(Lp[PLS + 1]);
-    const uint64_t gid = (uint64_t)(a.env_base + e);
-    const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32) ^ 0xA5A5A5A5u;
-    for (int t = 0; t < a.T; ++t) {
-        const int64_t r = (int64_t)t * n + e;
-        float ob[OBD];
-        rd::observe(st, ob);
-        normalize(ob, rms, zs, lane);
-        float m0, m1;
-        policy_mean(Lp, zs, h1s, lane, m0, m1);
-        const float v = value(Lv, zs, h1s, lane);
-        uint32_t w[4];
-        rd::philox((uint32_t)gid, (uint32_t)(gid >> 32), a.iter, (uint32_t)t, k0, k1, w);
-        const float u1 = (float)((w[0] >> 8) + 1u) * (1.0f / 16777216.0f);   // (0, 1]
-        const float u2 = (float)(w[1] >> 8) * (1.0f / 16777216.0f);
-        const float rad = sqrtf(-2.0f * logf(u1));
-        const float ang = 6.283185307179586f * u2;
-        const float a0 = fmaf(s0, rad * cosf(ang), m0), a1 = fmaf(s1, rad * sinf(ang), m1);
-#pragma unroll
-        for (int k = 0; k < OBD; ++k) a.ob[r * OBD + k] = ob[k];
-        a.ac[2 * r] = a0;
-        a.ac[2 * r + 1] = a1;
-        a.vpred[r] = v;
-        a.newf[r] = newf;
-        const float rw = rd::env_step(st, a0, a1);
-        a.rew[r] = rw;
-        ret += rw;
-        newf = 0.0f;
-        if (++step == rd::kEpisodeSteps) {   // TimeLimit(50): episode ends, env resets
-            it_ret += ret;
-            it_eps += 1.0f;
-            ret = 0.0f;
-            step = 0;
-            ++epi;
-            float d[6];
-            rd::philox_draw(a.seed, gid, (uint32_t)epi, d);
-            rd::env_reset(st, d);
-            newf = 1.0f;
-        }
-    }
-    {   // bootstrap value of the observation after the segment (0 if it starts an episode)
-        float ob[OBD];
-        rd::observe(st, ob);
-        normalize(ob, rms, zs, lane);
-        a.nextv[e] = newf > 0.5f ? 0.0f : value(Lv, zs, h1s, lane);
-    }
-    a.state[e] = st.q0; a.state[n + e] = st.q1; a.state[2 * n + e] = st.v0; a.state[3 * n + e] = st.v1;
-    a.state[4 * n + e] = st.tx; a.state[5 * n + e] = st.ty; a.state[6 * n + e] = st.dx; a.state[7 * n + e] = st.dy;
-    a.ep_step[e] = step;
-    a.ep_idx[e] = epi;
-    a.ep_ret[e] = ret;
-    a.new_next[e] = newf;
-    a.it_ret[e] = it_ret;
-    a.it_eps[e] = it_eps;
-}
 
 // block sums of up to 4 per-thread f64 values into part[blockIdx][4] (fixed-order tree)
 __device__ __forceinline__ void block_sum4(double v0, double v1, double v2, double v3, double* part) {
@@ -317,23 +189,6 @@ __global__ void rms_update_kernel(const double* part, int nblk, int64_t S, doubl
 }
 
 // old policy's log-probabilities (pi frozen, filter already updated: pposgd_simple order)
-__global__ __launch_bounds__(64) void logp_old_kernel(const float* params, const float* rms, const float* ob,
-                                                      const float* ac, int64_t S, float* lpo) {
-    __shared__ float L[P_POL + 2 * OBD];
-    __shared__ float zs[OBD * 64], h1s[HID * 64];
-    const int lane = threadIdx.x;
-    for (int i = threadIdx.x; i < P_POL; i += 64) L[i] = params[i];
-    if (threadIdx.x < 2 * OBD) L[P_POL + threadIdx.x] = rms[threadIdx.x];
-    __syncthreads();
-    const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (r >= S) return;
-    float m0, m1;
-    normalize(ob + r * OBD, L + P_POL, zs, lane);
-    policy_mean(L, zs, h1s, lane, m0, m1);
-    const float ls0 = L[PLS], ls1 = L[PLS + 1];
-    const float d0 = (ac[2 * r] - m0) / expf(ls0), d1 = (ac[2 * r + 1] - m1) / expf(ls1);
-    lpo[r] = -0.5f * (d0 * d0 + d1 * d1) - (ls0 + ls1) - LOG2PI;
-}
 
 // ---- the minibatch step: two launches --------------------------------------------------
 // minibatch_kernel: workgroup b owns the row tiles b, b + G, b + 2G, ... of MB_R rows: it
@@ -392,6 +247,7 @@ struct MbLds {
     alignas(16) float d1[2][MB_R][HLD];
     float dm[MB_R][2];
     float dv[MB_R];
+    float v[MB_R];                          // rollout: the value head's output
     double red[5][64];
 };
 
@@ -413,20 +269,208 @@ __device__ __forceinline__ float* mb_slot(MbLds& L, int i) {
     return &L.b3[2];
 }
 
+// all parameters into LDS, all loads in flight before the first LDS store (a load-store loop
+// serialises ~37 L2 round trips); the filter statistics
+__device__ __forceinline__ void mb_load_params(MbLds& L, const float* params, const float* rms, int tid) {
+    constexpr int NQ = (P_ALL + 255) / 256;
+    float pv[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) pv[q] = tid + q * 256 < P_ALL ? params[tid + q * 256] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+        if (tid + q * 256 < P_ALL) *mb_slot(L, tid + q * 256) = pv[q];
+    if (tid < 2 * OBD) L.rm[tid] = rms[tid];
+}
+
+// layers 1-2 of both nets over the 32 rows of L.z: wave (net, half) computes rows r0 .. r0 + 15
+// as four 16 x 16 MFMA blocks (layer 1 over k = 0..11: b1 rides in as row 11 of W1 against z's
+// ones column; layer 2 starts C at b2); h1 then h2 written, one barrier in between
+__device__ __forceinline__ void mb_forward(MbLds& L, int net, int r0, int lr, int lk) {
+    f32x4 c[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+        c[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+            c[cb] = mfma4(L.z[r0 + lr][4 * s + lk], L.w1[net][(4 * s + lk) * HID + 16 * cb + lr], c[cb]);
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) L.h1[net][r0 + 4 * lk + i][16 * cb + lr] = tanh_fast(c[cb][i]);
+    __syncthreads();
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+        const float b = L.b2[net][16 * cb + lr];
+        c[cb] = f32x4{b, b, b, b};
+    }
+#pragma unroll
+    for (int s = 0; s < HID / 4; ++s) {
+        const float av = L.h1[net][r0 + lr][4 * s + lk];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) c[cb] = mfma4(av, L.w2[net][(4 * s + lk) * W2LD + 16 * cb + lr], c[cb]);
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) L.h2[net][r0 + 4 * lk + i][16 * cb + lr] = tanh_fast(c[cb][i]);
+}
+
+// the heads of row r (after the barrier that follows mb_forward)
+__device__ __forceinline__ void policy_head(const MbLds& L, int r, float& m0, float& m1) {
+    m0 = L.b3[0];
+    m1 = L.b3[1];
+#pragma unroll 4
+    for (int k = 0; k < HID; k += 4) {
+        const float4 h = *(const float4*)&L.h2[0][r][k];
+        m0 = fmaf(h.x, L.w3p[2 * k], m0);         m1 = fmaf(h.x, L.w3p[2 * k + 1], m1);
+        m0 = fmaf(h.y, L.w3p[2 * k + 2], m0);     m1 = fmaf(h.y, L.w3p[2 * k + 3], m1);
+        m0 = fmaf(h.z, L.w3p[2 * k + 4], m0);     m1 = fmaf(h.z, L.w3p[2 * k + 5], m1);
+        m0 = fmaf(h.w, L.w3p[2 * k + 6], m0);     m1 = fmaf(h.w, L.w3p[2 * k + 7], m1);
+    }
+}
+
+__device__ __forceinline__ float value_head(const MbLds& L, int r) {
+    float v = L.b3[2];
+#pragma unroll 4
+    for (int k = 0; k < HID; k += 4) {
+        const float4 h = *(const float4*)&L.h2[1][r][k];
+        v = fmaf(h.w, L.w3v[k + 3], fmaf(h.z, L.w3v[k + 2], fmaf(h.y, L.w3v[k + 1], fmaf(h.x, L.w3v[k], v))));
+    }
+    return v;
+}
+
+// z row r of an observation (filter applied; 0 for a padded row), the ones column, zero pad
+__device__ __forceinline__ float z_entry(const MbLds& L, float ob, int k, bool valid) {
+    return k == OBD ? 1.0f : k > OBD ? 0.0f : valid ? clip5((ob - L.rm[k]) / L.rm[OBD + k]) : 0.0f;
+}
+
+// rollout (traj_segment_generator): 32 envs per workgroup, one per lane of wave 0 (physics,
+// noise, episode clocks, records); the policy and value MLPs of the 32 envs run as the
+// minibatch tile's forward (MFMA layers 1-2 by all four waves, heads by waves 0 / 1); one more
+// value forward after the segment bootstraps nextvpred
+constexpr int RO_E = MB_R;
+__global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
+    __shared__ MbLds L;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int net = w >> 1, r0 = (w & 1) * 16, lr = lane & 15, lk = lane >> 4;
+    mb_load_params(L, a.params, a.rms, tid);
+    const int64_t n = a.n, e = (int64_t)blockIdx.x * RO_E + lane;
+    const bool envl = w == 0 && lane < RO_E && e < n;
+    rd::State st{};
+    int step = 0, epi = 0;
+    float ret = 0.f, newf = 0.f, it_ret = 0.f, it_eps = 0.f;
+    if (envl) {
+        st.q0 = a.state[e]; st.q1 = a.state[n + e]; st.v0 = a.state[2 * n + e]; st.v1 = a.state[3 * n + e];
+        st.tx = a.state[4 * n + e]; st.ty = a.state[5 * n + e]; st.dx = a.state[6 * n + e]; st.dy = a.state[7 * n + e];
+        step = a.ep_step[e]; epi = a.ep_idx[e]; ret = a.ep_ret[e]; newf = a.new_next[e];
+    }
+    const uint64_t gid = (uint64_t)(a.env_base + e);
+    const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32) ^ 0xA5A5A5A5u;
+    __syncthreads();
+    const float s0 = expf(L.ls[0]), s1 = expf(L.ls[1]);
+    for (int t = 0;; ++t) {
+        float ob[OBD];
+        if (w == 0 && lane < RO_E) {
+            rd::observe(st, ob);
+#pragma unroll
+            for (int k = 0; k < ZLD; ++k) L.z[lane][k] = z_entry(L, k < OBD ? ob[k] : 0.0f, k, envl);
+        }
+        __syncthreads();
+        mb_forward(L, net, r0, lr, lk);
+        __syncthreads();
+        float m0 = 0.f, m1 = 0.f;
+        if (w == 1 && lane < RO_E) L.v[lane] = value_head(L, lane);
+        else if (w == 0 && lane < RO_E && t < a.T) policy_head(L, lane, m0, m1);
+        __syncthreads();
+        if (t == a.T) {   // bootstrap value of the observation after the segment (0 if it starts an episode)
+            if (envl) a.nextv[e] = newf > 0.5f ? 0.0f : L.v[lane];
+            break;
+        }
+        if (envl) {
+            const int64_t r = (int64_t)t * n + e;
+            uint32_t wd[4];
+            rd::philox((uint32_t)gid, (uint32_t)(gid >> 32), a.iter, (uint32_t)t, k0, k1, wd);
+            const float u1 = (float)((wd[0] >> 8) + 1u) * (1.0f / 16777216.0f);   // (0, 1]
+            const float u2 = (float)(wd[1] >> 8) * (1.0f / 16777216.0f);
+            const float rad = sqrtf(-2.0f * logf(u1));
+            const float ang = 6.283185307179586f * u2;
+            const float a0 = fmaf(s0, rad * cosf(ang), m0), a1 = fmaf(s1, rad * sinf(ang), m1);
+#pragma unroll
+            for (int k = 0; k < OBD; ++k) a.ob[r * OBD + k] = ob[k];
+            a.ac[2 * r] = a0;
+            a.ac[2 * r + 1] = a1;
+            a.vpred[r] = L.v[lane];
+            a.newf[r] = newf;
+            const float rw = rd::env_step(st, a0, a1);
+            a.rew[r] = rw;
+            ret += rw;
+            newf = 0.0f;
+            if (++step == rd::kEpisodeSteps) {   // TimeLimit(50): episode ends, env resets
+                it_ret += ret;
+                it_eps += 1.0f;
+                ret = 0.0f;
+                step = 0;
+                ++epi;
+                float d[6];
+                rd::philox_draw(a.seed, gid, (uint32_t)epi, d);
+                rd::env_reset(st, d);
+                newf = 1.0f;
+            }
+        }
+    }
+    if (envl) {
+        a.state[e] = st.q0; a.state[n + e] = st.q1; a.state[2 * n + e] = st.v0; a.state[3 * n + e] = st.v1;
+        a.state[4 * n + e] = st.tx; a.state[5 * n + e] = st.ty; a.state[6 * n + e] = st.dx; a.state[7 * n + e] = st.dy;
+        a.ep_step[e] = step;
+        a.ep_idx[e] = epi;
+        a.ep_ret[e] = ret;
+        a.new_next[e] = newf;
+        a.it_ret[e] = it_ret;
+        a.it_eps[e] = it_eps;
+    }
+}
+
+// oldpi's log-probs of the whole actor batch under the updated filter: minibatch_kernel's tile
+// forward (same products in the same order), so the first minibatch of an epoch sees ratio 1
+constexpr int LP_GRID = 1024;
+__global__ __launch_bounds__(256) void logp_old_kernel(const float* params, const float* rms, const float* ob,
+                                                       const float* ac, int64_t S, float* lpo) {
+    __shared__ MbLds L;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int net = w >> 1, r0 = (w & 1) * 16, lr = lane & 15, lk = lane >> 4;
+    mb_load_params(L, params, rms, tid);
+    __syncthreads();
+    const float ls0 = L.ls[0], ls1 = L.ls[1], sd0 = expf(ls0), sd1 = expf(ls1);
+    const int64_t ntiles = (S + MB_R - 1) / MB_R;
+    for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+        const int64_t i0 = tl * MB_R;
+        constexpr int NZ = (MB_R * ZLD + 255) / 256;
+#pragma unroll
+        for (int q = 0; q < NZ; ++q) {
+            const int e = tid + q * 256, r = e / ZLD, k = e % ZLD;
+            const int64_t i = i0 + r;
+            if (e < MB_R * ZLD) L.z[r][k] = z_entry(L, k < OBD && i < S ? ob[i * OBD + k] : 0.0f, k, i < S);
+        }
+        __syncthreads();
+        mb_forward(L, net, r0, lr, lk);
+        __syncthreads();
+        const int64_t i = i0 + lane;
+        if (w == 0 && lane < MB_R && i < S) {
+            float m0, m1;
+            policy_head(L, lane, m0, m1);
+            const float x0 = (ac[2 * i] - m0) / sd0, x1 = (ac[2 * i + 1] - m1) / sd1;
+            lpo[i] = -0.5f * (x0 * x0 + x1 * x1) - (ls0 + ls1) - LOG2PI;
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
     __shared__ MbLds L;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int net = w >> 1, half = w & 1, r0 = half * MB_H;
-    {   // all loads in flight before the first LDS store (a load-store loop serialises ~37 L2 round trips)
-        constexpr int NQ = (P_ALL + 255) / 256;
-        float pv[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) pv[q] = tid + q * 256 < P_ALL ? a.params[tid + q * 256] : 0.0f;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-            if (tid + q * 256 < P_ALL) *mb_slot(L, tid + q * 256) = pv[q];
-    }
-    if (tid < 2 * OBD) L.rm[tid] = a.rms[tid];
+    mb_load_params(L, a.params, a.rms, tid);
     if (blockIdx.x == 0 && tid < 4) a.ctl[4 + tid] = a.ctl[tid];   // Adam words for reduce_adam_kernel
     const float inv = 1.0f / (float)a.mb;
     // this wave's weight-gradient blocks: dW2 rows 32 half + 16 kb.., columns 16 jb..; dW1 | db1
@@ -456,8 +500,7 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
 #pragma unroll
         for (int q = 0; q < NZ; ++q) {
             const int e = tid + q * 256, r = e / ZLD, k = e % ZLD, i = i0 + r;
-            if (e < MB_R * ZLD)
-                L.z[r][k] = k == OBD ? 1.0f : k > OBD ? 0.0f : i < a.mb ? clip5((zo[q] - L.rm[k]) / L.rm[OBD + k]) : 0.0f;
+            if (e < MB_R * ZLD) L.z[r][k] = z_entry(L, zo[q], k, i < a.mb);
         }
         const int li = i0 + lane;
         const bool lrow = w < 2 && lane < MB_R && li < a.mb;
@@ -471,49 +514,13 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
             }
         }
         __syncthreads();
-        // 2. layer 1, both nets: wave (net, half) computes rows r0 .. r0 + 15 as four 16 x 16
-        //    MFMA blocks over k = 0..11 (b1 rides in as row 11 of W1 against z's ones column)
-        f32x4 c[4];
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-            c[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int s = 0; s < 3; ++s)
-                c[cb] = mfma4(L.z[r0 + lr][4 * s + lk], L.w1[net][(4 * s + lk) * HID + 16 * cb + lr], c[cb]);
-        }
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) L.h1[net][r0 + 4 * lk + i][16 * cb + lr] = tanh_fast(c[cb][i]);
-        __syncthreads();
-        // 3. layer 2: C starts at b2, k = 0..63
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-            const float b = L.b2[net][16 * cb + lr];
-            c[cb] = f32x4{b, b, b, b};
-        }
-#pragma unroll
-        for (int s = 0; s < HID / 4; ++s) {
-            const float av = L.h1[net][r0 + lr][4 * s + lk];
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb) c[cb] = mfma4(av, L.w2[net][(4 * s + lk) * W2LD + 16 * cb + lr], c[cb]);
-        }
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) L.h2[net][r0 + 4 * lk + i][16 * cb + lr] = tanh_fast(c[cb][i]);
+        // 2-3. layers 1-2 of both nets
+        mb_forward(L, net, r0, lr, lk);
         __syncthreads();
         // 4. heads and the loss, one lane per row: wave 0 the policy, wave 1 the value net
         if (w == 0 && lane < MB_R) {
-            float m0 = L.b3[0], m1 = L.b3[1];
-#pragma unroll 4
-            for (int k = 0; k < HID; k += 4) {
-                const float4 h = *(const float4*)&L.h2[0][lane][k];
-                m0 = fmaf(h.x, L.w3p[2 * k], m0);         m1 = fmaf(h.x, L.w3p[2 * k + 1], m1);
-                m0 = fmaf(h.y, L.w3p[2 * k + 2], m0);     m1 = fmaf(h.y, L.w3p[2 * k + 3], m1);
-                m0 = fmaf(h.z, L.w3p[2 * k + 4], m0);     m1 = fmaf(h.z, L.w3p[2 * k + 5], m1);
-                m0 = fmaf(h.w, L.w3p[2 * k + 6], m0);     m1 = fmaf(h.w, L.w3p[2 * k + 7], m1);
-            }
+            float m0, m1;
+            policy_head(L, lane, m0, m1);
             float dm0 = 0.0f, dm1 = 0.0f;
             if (lrow) {
                 // TF's min / clip gradient conventions (see oracle/ppo_np.py loss_and_grads)
@@ -538,12 +545,7 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
             L.dm[lane][0] = dm0;
             L.dm[lane][1] = dm1;
         } else if (w == 1 && lane < MB_R) {
-            float v = L.b3[2];
-#pragma unroll 4
-            for (int k = 0; k < HID; k += 4) {
-                const float4 h = *(const float4*)&L.h2[1][lane][k];
-                v = fmaf(h.w, L.w3v[k + 3], fmaf(h.z, L.w3v[k + 2], fmaf(h.y, L.w3v[k + 1], fmaf(h.x, L.w3v[k], v))));
-            }
+            const float v = value_head(L, lane);
             float dvr = 0.0f;
             if (lrow) {
                 const float d = v - ret;
@@ -573,6 +575,7 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
         __syncthreads();
         // 6. layer 2 backward: D1 = (D2 W2^T) * tanh' for rows r0.. (B = W2 read transposed),
         //    then dW2 += H1^T D2 over the tile's 32 rows (k = 32 half ..), and db2 (half 0)
+        f32x4 c[4];
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) c[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -669,6 +672,9 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(RaArgs a) {
     __shared__ double rq[RA_SLICES][RA_COLS];
     const int c = threadIdx.x % RA_COLS, s = threadIdx.x / RA_COLS, p = blockIdx.x * RA_COLS + c;
     const bool lsc = p == PLS || p == PLS + 1;
+    // Adam's operands in flight before the column sums
+    const bool own = s == 0 && p < P_ALL;
+    const float m0 = own ? a.m[p] : 0.0f, v0 = own ? a.v[p] : 0.0f, x0 = own ? a.params[p] : 0.0f;
     float sum = 0.0f;
     double q = 0.0;
     if (p < P_ALL && !lsc) {
@@ -691,12 +697,12 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(RaArgs a) {
         const float g = lsc ? (float)d0 : g0;
         a.grad[p] = g;
         const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-        float m = a.m[p], v = a.v[p];
+        float m = m0, v = v0;
         m += (g - m) * (1.0f - a.b1);
         v += (g * g - v) * (1.0f - a.b2);
         a.m[p] = m;
         a.v[p] = v;
-        a.params[p] -= (m * alpha) / (sqrtf(v) + a.eps);
+        a.params[p] = x0 - (m * alpha) / (sqrtf(v) + a.eps);
     }
     if (blockIdx.x == 0) {
         if (a.accumulate && c < 3) a.acc[c] += d0;
@@ -769,7 +775,9 @@ struct rdp_trainer {
     double *rms_sums = nullptr, *part = nullptr, *stats = nullptr, *acc = nullptr;
     float* rms = nullptr;
     int* perm = nullptr;
-    std::vector<int> host_perm;
+    std::vector<int> host_perm[2];   // double-buffered: the next iteration's shuffles are drawn
+    int perm_buf = 0;                 //   while the GPU runs this iteration's minibatches
+    uint32_t perm_for = UINT32_MAX;   // iteration whose shuffles host_perm[perm_buf] holds
     // minibatch step: per-workgroup partial gradient rows and loss sums
     float* mbpart = nullptr;
     double* mbstat = nullptr;
@@ -791,7 +799,7 @@ int run_rollout(rdp_trainer* t) {
     a.params = t->params; a.rms = t->rms; a.state = t->state; a.ep_step = t->ep_step; a.ep_idx = t->ep_idx;
     a.ep_ret = t->ep_ret; a.new_next = t->new_next; a.it_ret = t->it_ret; a.it_eps = t->it_eps;
     a.ob = t->ob; a.ac = t->ac; a.vpred = t->vpred; a.rew = t->rew; a.newf = t->newf; a.nextv = t->nextv;
-    hipLaunchKernelGGL(rollout_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, t->stream, a);
+    hipLaunchKernelGGL(rollout_kernel, dim3((unsigned)((n + RO_E - 1) / RO_E)), dim3(256), 0, t->stream, a);
     RDP_CK(hipGetLastError(), "rdp rollout_kernel");
     const int gblk = (int)((n + RB - 1) / RB);
     hipLaunchKernelGGL(gae_kernel, dim3(gblk), dim3(RB), 0, t->stream, n, T, t->cfg.gamma, t->cfg.lam,
@@ -806,7 +814,8 @@ int run_rollout(rdp_trainer* t) {
     hipLaunchKernelGGL(rms_update_kernel, dim3(1), dim3(64), 0, t->stream, (const double*)t->part, oblk, S,
                        t->rms_sums);
     hipLaunchKernelGGL(rms_finalize_kernel, dim3(1), dim3(64), 0, t->stream, (const double*)t->rms_sums, t->rms);
-    hipLaunchKernelGGL(logp_old_kernel, dim3((unsigned)((S + 63) / 64)), dim3(64), 0, t->stream,
+    hipLaunchKernelGGL(logp_old_kernel, dim3((unsigned)std::min<int64_t>((S + MB_R - 1) / MB_R, LP_GRID)), dim3(256), 0,
+                       t->stream,
                        (const float*)t->params, (const float*)t->rms, (const float*)t->ob, (const float*)t->ac, S,
                        t->lpo);
     RDP_CK(hipGetLastError(), "rdp filter / logp_old");
@@ -828,13 +837,12 @@ int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
     return RD_OK;
 }
 
-int run_optimize(rdp_trainer* t) {
+// the optim_epochs shuffles of iteration `iter` (host Fisher-Yates, seeded by seed and iter)
+void draw_perms(const rdp_trainer* t, uint32_t iter, int* out) {
     const int64_t S = t->S;
-    const int E = t->cfg.optim_epochs;
-    const int nmb = (int)(S / t->mb);   // baselines iterate_once: full minibatches only
-    std::mt19937_64 rng(t->cfg.seed * 0x9E3779B97F4A7C15ull + t->iter + 1);
-    for (int e = 0; e < E; ++e) {
-        int* p = t->host_perm.data() + (int64_t)e * S;
+    std::mt19937_64 rng(t->cfg.seed * 0x9E3779B97F4A7C15ull + iter + 1);
+    for (int e = 0; e < t->cfg.optim_epochs; ++e) {
+        int* p = out + (int64_t)e * S;
         for (int64_t i = 0; i < S; ++i) p[i] = (int)i;
         for (int64_t i = S - 1; i > 0; --i) {   // Fisher-Yates
             const int64_t j = (int64_t)(rng() % (uint64_t)(i + 1));
@@ -843,7 +851,16 @@ int run_optimize(rdp_trainer* t) {
             p[j] = tmp;
         }
     }
-    RDP_CK(hipMemcpyAsync(t->perm, t->host_perm.data(), sizeof(int) * (size_t)E * S, hipMemcpyHostToDevice, t->stream),
+}
+
+int run_optimize(rdp_trainer* t) {
+    const int64_t S = t->S;
+    const int E = t->cfg.optim_epochs;
+    const int nmb = (int)(S / t->mb);   // baselines iterate_once: full minibatches only
+    const int cur = t->perm_buf;
+    if (t->perm_for != t->iter) draw_perms(t, t->iter, t->host_perm[cur].data());
+    RDP_CK(hipMemcpyAsync(t->perm, t->host_perm[cur].data(), sizeof(int) * (size_t)E * S, hipMemcpyHostToDevice,
+                          t->stream),
            "rdp perm");
     RDP_CK(hipMemsetAsync(t->acc, 0, sizeof(double) * 4, t->stream), "rdp acc");
     for (int e = 0; e < E; ++e)
@@ -854,7 +871,10 @@ int run_optimize(rdp_trainer* t) {
                        (const double*)t->acc, (const float*)t->params, t->lrmult, t->timesteps,
                        t->hist + (int64_t)(t->iter % (uint32_t)t->cfg.metrics_len) * N_MET);
     RDP_CK(hipGetLastError(), "rdp metrics");
-    RDP_CK(hipStreamSynchronize(t->stream), "rdp optimize");   // host_perm is reused next iteration
+    draw_perms(t, t->iter + 1, t->host_perm[cur ^ 1].data());   // overlaps the minibatches on the GPU
+    t->perm_buf = cur ^ 1;
+    t->perm_for = t->iter + 1;
+    RDP_CK(hipStreamSynchronize(t->stream), "rdp optimize");
     ++t->iter;
     t->lrmult = t->cfg.schedule_linear
                     ? (float)fmax(1.0 - t->timesteps / (double)t->cfg.max_timesteps, 0.0)
@@ -892,7 +912,7 @@ int rdp_create(rdp_trainer** out, const rdp_config* cfg, int device, void* hip_s
     t->n = cfg->n_envs;
     t->S = S;
     t->mb = cfg->optim_batchsize > 0 ? cfg->optim_batchsize : (int)S;
-    t->host_perm.resize((size_t)cfg->optim_epochs * S);
+    for (auto& h : t->host_perm) h.resize((size_t)cfg->optim_epochs * S);
     const int64_t n = t->n;
     hipError_t e = hipSuccess;
     auto af = [&](float** p, int64_t cnt) {
@@ -993,6 +1013,7 @@ int rdp_reset(rdp_trainer* t) {
     RD_HIP(hipMemsetAsync(t->v, 0, sizeof(float) * P_ALL, t->stream), "rdp_reset");
     RD_HIP(hipGetLastError(), "rdp_reset");
     t->iter = 0;
+    t->perm_for = UINT32_MAX;
     t->timesteps = 0.0;
     t->lrmult = 1.0f;
     return RD_OK;

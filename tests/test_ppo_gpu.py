@@ -151,3 +151,17 @@ def test_trained_teacher_plugs_into_distillation():
     d = DistillTrainer(DistillConfig(n_envs=1024), device=DEV, teacher=tr.teacher())
     d.step()
     assert np.isfinite(d.metrics(1)).all()
+
+
+def test_two_trainers_are_bitwise_equal():
+    """Same config and seed: the actor batch, the parameters after two iterations (ragged
+    minibatch tiles: 1,000 rows) and the metrics are bitwise equal (fixed-order sums only)."""
+    runs = []
+    for _ in range(2):
+        tr = _trainer(n_envs=500, horizon=50, optim_batchsize=1000, optim_epochs=2)
+        for _ in range(2):
+            tr.iterate()
+        runs.append((tr.policy().cpu(), tr.value().cpu(), tr.batch()["vpred"].cpu(), tr.metrics(2)))
+    (p0, v0, b0, m0), (p1, v1, b1, m1) = runs
+    assert torch.equal(p0, p1) and torch.equal(v0, v1) and torch.equal(b0, b1)
+    np.testing.assert_array_equal(m0, m1)
