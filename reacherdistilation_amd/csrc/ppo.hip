@@ -564,18 +564,13 @@ __global__ __launch_bounds__(256) void minibatch_kernel(MbArgs a) {
                                       : L.dv[r] * L.w3v[lane];
             L.d2[net][r][lane] = gy * (1.0f - h * h);
         }
-        {   // four independent chains over the tile's rows (a 32-deep chain of LDS-fed FMAs was
-            // latency-bound)
-            float q[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (w < 3) {
-#pragma unroll
-                for (int r = 0; r < MB_R; ++r)
-                    q[r & 3] = fmaf(L.h2[net][r][lane], w == 2 ? L.dv[r] : L.dm[r][w], q[r & 3]);
-            } else if (lane < 3) {
-#pragma unroll
-                for (int r = 0; r < MB_R; ++r) q[r & 3] += lane < 2 ? L.dm[r][lane] : L.dv[r];
-            }
-            a3 += (q[0] + q[1]) + (q[2] + q[3]);
+        if (w < 3) {
+#pragma unroll 8
+            for (int r = 0; r < MB_R; ++r)
+                a3 = fmaf(L.h2[net][r][lane], w == 2 ? L.dv[r] : L.dm[r][w], a3);
+        } else if (lane < 3) {
+#pragma unroll 8
+            for (int r = 0; r < MB_R; ++r) a3 += lane < 2 ? L.dm[r][lane] : L.dv[r];
         }
         __syncthreads();
         // 6. layer 2 backward: D1 = (D2 W2^T) * tanh' for rows r0.. (B = W2 read transposed),
