@@ -607,6 +607,25 @@ def fitted_teacher(dev):
     return p, info
 
 
+def teacher_ppo(dev, n=4096, T=50, mb=4096, iters=5):
+    """The teacher's PPO iteration (csrc/ppo.hip): n envs x T steps of rollout, GAE,
+    the filter update and 10 epochs of mb-row minibatch steps (two launches each), timed over
+    iters - 1 whole iterations after one warm-up; the longer run is scripts/bench_ppo.py."""
+    import torch
+
+    from reacherdistilation_amd.ppo import PPOConfig, PPOTrainer
+    tr = PPOTrainer(PPOConfig(n_envs=n, horizon=T, optim_batchsize=mb, max_timesteps=n * T * 40), device=dev)
+    tr.iterate()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(iters - 1):
+        tr.iterate()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / (iters - 1)
+    return {"n_envs": n, "horizon": T, "minibatch": mb, "epochs": 10, "iter_ms": dt * 1e3,
+            "env_steps_per_s": n * T / dt, "ep_ret_mean_last": float(tr.metrics(1)[0][0])}
+
+
 def cpu_baseline(workload, seconds, threads, n):
     """Time the oracle's C f32 rollout+distill step (OpenMP) at the workload's own env count
     (the same per-GPU batch as the timed GPU step), for a bounded number of steps."""
@@ -1005,6 +1024,8 @@ def main():
                                                          accum=max(1, args.accum))
         if world == 1 and args.fixture_steps > 0:
             out["convergence_fixture"] = convergence_fixture(dev, args.lr, args.fixture_steps, args.fixture_ref_steps)
+        if world == 1 and args.fixture_steps > 0:
+            out["teacher_ppo"] = teacher_ppo(dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads, n)
             out["cpu_baseline"]["ref_loop"] = cpu_ref_loop(min(4.0, args.cpu_seconds))
