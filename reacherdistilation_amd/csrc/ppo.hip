@@ -207,7 +207,8 @@ constexpr int MB_G = 256;                  // at most this many workgroups (= pa
 constexpr int W2LD = HID + 4;              // LDS row stride of W2 (B operands read both ways)
 constexpr int PSTR = (P_ALL + 3) & ~3;     // partial row stride (floats)
 constexpr int NSTAT = 8;                   // f64 per workgroup: pol_surr, vf_loss, clipfrac, dlogstd0, dlogstd1
-constexpr int RA_COLS = 32, RA_SLICES = 8; // reduce_adam: 32 columns x 8 row slices per block
+constexpr int RA_COLS = 16, RA_SLICES = 16;   // reduce_adam: 16 columns x 16 row slices per block (32 x 8: +4 %, 64 x 4: +19 %)
+static_assert(RA_COLS * RA_SLICES == 256 && (RA_SLICES & (RA_SLICES - 1)) == 0, "256 threads, power-of-two slices");
 static_assert(MB_R == 32 && HID == 64 && PB1 == OBD * HID && VC1 == OBD * HID,
               "two 16-row MFMA blocks per tile; b1 follows W1");
 
@@ -689,8 +690,22 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(RaArgs a) {
     rq[s][c] = q;
     __syncthreads();
     if (s != 0) return;
-    const float g0 = ((rs[0][c] + rs[1][c]) + (rs[2][c] + rs[3][c])) + ((rs[4][c] + rs[5][c]) + (rs[6][c] + rs[7][c]));
-    const double d0 = ((rq[0][c] + rq[1][c]) + (rq[2][c] + rq[3][c])) + ((rq[4][c] + rq[5][c]) + (rq[6][c] + rq[7][c]));
+    float fs[RA_SLICES];   // adjacent-pair tree over the slices: ((0 + 1) + (2 + 3)) + ...
+    double ds[RA_SLICES];
+#pragma unroll
+    for (int q = 0; q < RA_SLICES; ++q) {
+        fs[q] = rs[q][c];
+        ds[q] = rq[q][c];
+    }
+#pragma unroll
+    for (int w = RA_SLICES / 2; w >= 1; w /= 2)
+#pragma unroll
+        for (int q = 0; q < w; ++q) {
+            fs[q] = fs[2 * q] + fs[2 * q + 1];
+            ds[q] = ds[2 * q] + ds[2 * q + 1];
+        }
+    const float g0 = fs[0];
+    const double d0 = ds[0];
     const uint32_t S = a.ctl[4];
     const float b1p = __uint_as_float(a.ctl[5]), b2p = __uint_as_float(a.ctl[6]);
     if (p < P_ALL) {
