@@ -103,6 +103,8 @@ def parse():
                          "0-19 (the reference's budget: 5000 episodes x 50 steps); 0 = skip")
     ap.add_argument("--fixture-ref-steps", type=int, default=25_000,
                     help="the same leg's steps for the reference graph student (student_nn.py:51-57)")
+    ap.add_argument("--no-workloads", action="store_true",
+                    help="at N = 1 skip the `workloads` object (configs 2, 3 and the config-5 shard at K = 1 and 50)")
     ap.add_argument("--no-strong-projection", action="store_true",
                     help="at N = 1 skip timing c4's 2/4/8-GPU strong shards (strong_projection)")
     ap.add_argument("--teacher", default="synthetic", choices=["synthetic", "fitted"],
@@ -338,6 +340,67 @@ def time_leg(wl, n, sdt, split, dev, lr, steps, warmup, npass=100, settle_ms=0.0
     return {"f32_mode": "split" if split else "exact", "value": n * steps / el, "ms_per_step": el * 1e3 / steps,
             "launch_us": kern_ms * 1e3, "achieved_tflops": achieved, "peak_tflops": peak, "frac": achieved / peak,
             "frac_of_f32_mfma_peak": achieved / PEAK_F32_TFLOPS}
+
+
+def workload_leg(name, dev, lr, steps, warmup, settle_ms, K=1, split=True, npass=50):
+    """one BASELINE config at world size 1, timed like the headline (settle,
+    warm-up, then exactly `steps` env steps between synchronizes, no events), plus an
+    event-timed pass over the rollout launches for the mixed-peak fraction.  K = 1: rdd_step per
+    env step; K > 1: rdd_step_accum (one K-env-step launch + reduce + Adam per optimiser step,
+    SURVEY §8d's K = 50 reading), its launch timed with the reduce (rdd_rollout_accum)."""
+    import torch
+
+    from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
+    wl = WORKLOADS[name]
+    n, sdt = wl["envs"], wl.get("student_dtype", "f32")
+    tr = DistillTrainer(DistillConfig(n_envs=n, seed=0, loss=wl["loss"], act_with=wl["act_with"], lr=lr,
+                                      student_dtype=sdt, f32_split=split, accum_steps=K), device=dev)
+    fn = tr.step if K == 1 else tr.step_accum
+    calls = steps if K == 1 else max(4, steps // K)
+    settle(fn, dev, settle_ms)
+    for _ in range(max(1, warmup // K)):
+        fn()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        fn()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    npass = npass if K == 1 else max(4, npass // 10)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(npass)]
+    for a, b in evs:
+        a.record()
+        if K == 1:
+            tr.launch(tr.STAGE_ROLLOUT)
+        else:
+            tr.rollout_accum()
+        b.record()
+        tr.launch(tr.STAGE_REDUCE_APPLY if K == 1 else tr.STAGE_APPLY)
+    torch.cuda.synchronize(dev)
+    launch_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    tr.close()
+    env_steps = calls * K
+    achieved = FLOP_PER_ENV_STEP * n * K / (launch_ms * 1e-3) / 1e12
+    peak = mixed_peak(sdt, split)
+    return {"workload": name, "envs": n, "accum_steps": K, "env_steps": env_steps,
+            "us_per_env_step": el * 1e6 / env_steps, "env_steps_per_s": n * env_steps / el,
+            "launch_us": launch_ms * 1e3, "launch_us_per_env_step": launch_ms * 1e3 / K,
+            "launch": "rollout_kernel" if K == 1 else f"rollout_kernel, {K} env steps per launch, + its reduce",
+            "achieved_tflops": achieved, "mixed_peak_tflops": peak, "frac": achieved / peak,
+            "f32_mode": "split" if split else "exact", "student_dtype": sdt, "loss": wl["loss"],
+            "act_with": wl["act_with"]}
+
+
+def workloads(dev, lr, steps, warmup, settle_ms, accum=50, names=("c2", "c3", "c5")):
+    """Every BASELINE config besides the headline's in the driver-run line: K = 1 and K = accum."""
+    out = {"timing": "per leg: settle, warm-up, then `env_steps` env steps between synchronizes (the "
+                     "headline's method); launch_us from HIP events around the rollout launches in a pass after",
+           "flop_per_env_step": FLOP_PER_ENV_STEP}
+    for name in names:
+        out[name] = {"description": WORKLOADS[name]["desc"], "k1": workload_leg(name, dev, lr, steps, warmup, settle_ms)}
+        if accum > 1:
+            out[name][f"k{accum}"] = workload_leg(name, dev, lr, max(steps, 8 * accum), warmup, settle_ms, K=accum)
+    return out
 
 
 def exchange_latency(comm, dev, n=5060, iters=200, warmup=20):
@@ -1022,6 +1085,10 @@ def main():
         if world == 1 and args.workload == "c4" and not args.no_strong_projection and not args.envs_per_gpu:
             out["strong_projection"] = strong_projection(wl, sdt, split, dev, args.lr, 200, min(args.settle_ms, 100.0),
                                                          accum=max(1, args.accum))
+        if world == 1 and not args.no_workloads and not args.envs_per_gpu:
+            out["workloads"] = workloads(dev, args.lr, max(args.steps, 200), args.warmup, min(args.settle_ms, 100.0),
+                                         accum=max(1, args.accum),
+                                         names=tuple(k for k in ("c2", "c3", "c5") if k != args.workload))
         if world == 1 and args.fixture_steps > 0:
             out["convergence_fixture"] = convergence_fixture(dev, args.lr, args.fixture_steps, args.fixture_ref_steps)
         if world == 1 and args.fixture_steps > 0:

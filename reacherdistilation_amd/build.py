@@ -34,8 +34,14 @@ LDFLAGS = ["-shared", f"--offload-arch={ARCH}", "-ldl"]
 # tile loop's latch, whose operands the next tile's first LDS loads overwrite; on gfx950 a
 # packed-f32 op queued behind MFMAs can read its operands after such a load landed, and lanes
 # 48-63 of gw3b came out different run to run (DESIGN.md §3 "PKWAR", scripts/isa/hazards.py).
-# The packed tanh / split pairs written explicitly as f32x2 stay.
-SRC_FLAGS = {"distill.hip": ["-fno-slp-vectorize"], "ppo.hip": ["-fno-slp-vectorize"]}
+# Round 6 also unpacked the explicit f32x2 tanh / split pairs, so no rollout kernel contains a
+# packed-f32 op at all.  ppo.hip: its minibatch kernel keeps 38 gradient sums per thread across
+# tiles, and its SLP build had loads 14-46 instructions behind unread packed accumulators.
+# student_mlp.hip / student_lstm.hip: their SLP builds had the same pattern (PKWAR hits in the
+# reference student's kernel and reduce+Adam, the LSTM's BPTT, head and reduce kernels); every
+# product source is now scanned for it (tests/test_product_hygiene.py).
+NO_SLP = ["-fno-slp-vectorize"]
+SRC_FLAGS = {"distill.hip": NO_SLP, "ppo.hip": NO_SLP, "student_mlp.hip": NO_SLP, "student_lstm.hip": NO_SLP}
 
 
 def src_flags(path):

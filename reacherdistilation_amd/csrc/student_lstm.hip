@@ -254,7 +254,7 @@ __device__ __forceinline__ rdg::f32x4 pr_load4(__amdgpu_buffer_rsrc_t r, int64_t
 // "allgather"): each exchanged f32 travels as ONE naturally aligned 8-byte word {tag, value},
 // written by one agent-scope (sc1) store and read by agent-scope loads; a consumer re-reads
 // its granules until every tag is the one it waits for.  No payload drain, no arrival counter,
-// no barrier poll per step: the data is the flag.  Tags = (generation << 8) | phase, the
+// no barrier poll per step: the data is the flag.  Tags = (generation << 12) | phase, the
 // generation advanced on the device once per forward call (the forward's last workgroup, bar[3];
 // a replayed graph advances it too), so a granule left by an earlier call never matches.  Two buffers by
 // step parity: a workgroup overwrites parity p only after it read every other workgroup's
@@ -267,7 +267,12 @@ __device__ __forceinline__ void gr_store(unsigned long long* p, uint32_t tag, fl
 __device__ __forceinline__ unsigned long long gr_load(const unsigned long long* p) {
     return __hip_atomic_load((const gu64_t*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t gr_tag(uint32_t gen, uint32_t phase) { return (gen << 8) | phase; }
+// phase = the unrolled step s + 1 <= T - 1 in its own 12 bits (persistent() admits T < PR_MAX_T),
+// the generation in the 20 above: with an 8-bit phase, T >= 258 let step 257 of call g - 1 carry
+// step 1's tag of call g
+constexpr int PR_PHASE_BITS = 12;
+constexpr int PR_MAX_T = 1 << PR_PHASE_BITS;
+__device__ __forceinline__ uint32_t gr_tag(uint32_t gen, uint32_t phase) { return (gen << PR_PHASE_BITS) | phase; }
 
 // SrcC fence around MFMA chains (student_mlp.hip's fence_begin / fence_end): every operand is
 // in registers before the chains start, the accumulators pass through an empty asm
@@ -541,7 +546,13 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
             for (int rq = 0; rq < PR_ROWS / 4; ++rq) {
                 const int r = 4 * rq + gq;
                 const int64_t row = (int64_t)s * B + r;
-                xa[q][rq] = (r >= B || k >= XI + U) ? 0.0f : k < XI ? X[row * XLD + k] : Hp[row * U + (k - XI)];
+                // branch-free: every lane loads (a lane without an entry from X[0]) and selects, so
+                // the 32 loads stay in flight together (as branches, the no-SLP build waited
+                // vmcnt(0) between them: BPTT 45 -> 56 us at 20 windows, profiles/r06e_*)
+                const bool in = r < B && k < XI + U;
+                const float* src = !in ? X : k < XI ? X + row * XLD + k : Hp + row * U + (k - XI);
+                const float v = *src;
+                xa[q][rq] = in ? v : 0.0f;
             }
         }
     };
@@ -578,15 +589,17 @@ __global__ __launch_bounds__(256) void lstm_bptt_persist_kernel(const float* __r
     float qsum[4][4] = {};                    // Q = prev^T dz: [prev component][gate]
     float cg[4], cct, ccp, cdh, cpv[4];
     auto load_cell = [&](int s) {   // gates, c_t, c_{t-1}, dh from the head: written before the launch
+        // branch-free as load_a: a lane without a point loads row (s, 0) of its unit (valid) and
+        // its values are never used (every use is under pt)
         const int64_t rs = (int64_t)s * B + (pt ? pr : 0);
         const float* g = G + rs * G4 + pu;
 #pragma unroll
-        for (int y = 0; y < 4; ++y) cg[y] = pt ? g[y * U] : 0.0f;
-        cct = pt ? Cs[(rs + B) * U + pu] : 0.0f;
-        ccp = pt ? Cs[rs * U + pu] : 0.0f;
-        cdh = pt ? dHh[rs * U + pu] : 0.0f;
+        for (int y = 0; y < 4; ++y) cg[y] = g[y * U];
+        cct = Cs[(rs + B) * U + pu];
+        ccp = Cs[rs * U + pu];
+        cdh = dHh[rs * U + pu];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) cpv[a] = pt ? prev[rs * 4 + a] : 0.0f;
+        for (int a = 0; a < 4; ++a) cpv[a] = prev[rs * 4 + a];
     };
     load_cell(T - 1);
     load_a(T - 1);
@@ -1573,8 +1586,8 @@ bool fused_head(const rdl_trainer* t, int64_t R) {
     return !(t->cfg.kernels & RDL_KERNELS_LAYER_HEAD) && t->hpart && R <= HF_MAX_ROWS;
 }
 
-bool persistent(const rdl_trainer* t, int64_t B) {
-    return !(t->cfg.kernels & RDL_KERNELS_STEP_RECURRENCE) && B <= PR_ROWS;
+bool persistent(const rdl_trainer* t, int64_t B) {   // (T < PR_MAX_T: every phase fits its tag field)
+    return !(t->cfg.kernels & RDL_KERNELS_STEP_RECURRENCE) && B <= PR_ROWS && t->T < PR_MAX_T;
 }
 
 // forward over all T steps of B windows.  out_pdflat: where the head's output goes (the

@@ -254,6 +254,7 @@ class DistillTrainer:
             self.allreduce_grad()
             nat.check(self._lib.rdd_apply(self._h), "rdd_apply")
         self._keep = (obs, tp)
+        self.steps += 1   # one optimiser step, as step() (fit_records' eager tail)
 
     def rollout_rows(self, obs: torch.Tensor, t_pdflat: torch.Tensor, n_global: int | None = None):
         obs, tp = self._obs_arg(obs), self._tflat_arg(t_pdflat, obs.shape[0])

@@ -308,6 +308,59 @@ def scan_pkwar(code, window=64):
     return sorted(out.values(), key=lambda h: (h[3], h[5]))
 
 
+def scan_ldsrc(code, window=64):
+    """LDSRC hits under the interlock rule [(kind, wait states, horizon, line, op, line2,
+    instruction2)] of one function (every hit is a violation): a DS / VMEM load whose destination
+    overlaps the SrcC (outside the destination) of an earlier exact-f32 MFMA (the 8/16-pass forms,
+    which ROCm 7.2's hazard recognizer does not protect against loads), reached on some control-flow
+    path within NP + 6 wait states (4 beyond completion, the scan_code horizon) with nothing in
+    between that completes the MFMA first: a VALU / DS / VMEM read of its destination or an MFMA
+    reading it as SrcA/SrcB (both wait for the result), or a VALU write of the SrcC registers
+    (interlocked behind the MFMA's read).  Stricter than scan_code's LDSRC, which accepts a load
+    at NP + 2 wait states by the pass count alone: here completion must be forced by an
+    instruction, or the load lies beyond the horizon."""
+    insts, succ = _cfg(code)
+    parsed = [(ln, l, *classify(l)) for ln, l in insts]
+    out = {}
+    for idx, (ln, l, op, w, r, sd) in enumerate(parsed):
+        if not op.startswith("v_mfma") or xdl(op):
+            continue
+        o = operands(l)
+        dst, a, b, c = (regs(x) for x in (o + ["", "", "", ""])[:4])
+        srcc = vset(c) - vset(dst)
+        if not srcc:
+            continue
+        horizon = PASSES.get(op, 8) + 6
+        seen = {}
+        stack = [(k, 0, 1) for k in succ[idx]]
+        while stack:
+            k2, ws, steps = stack.pop()
+            if k2 >= len(parsed) or steps > window or ws >= horizon or seen.get(k2, 1 << 30) <= ws:
+                continue
+            seen[k2] = ws
+            ln2, l2, op2, w2, r2, sd2 = parsed[k2]
+            if op2 == "s_nop":
+                stack.extend((k3, ws + int(l2.split()[1], 0) + 1, steps + 1) for k3 in succ[k2])
+                continue
+            m2 = op2.startswith(("v_mfma", "v_smfmac"))
+            if m2:
+                o2 = operands(l2)
+                a2, b2 = regs((o2 + ["", "", ""])[1]), regs((o2 + ["", "", ""])[2])
+                if (a2 | b2) & dst:   # MRAW: waits for the result
+                    continue
+            elif not op2.startswith("s_") and vset(r2) & vset(dst):   # RAW read: the MFMA completed
+                continue
+            ld2 = op2.startswith(LOAD) or (op2.startswith(VMEM) and "atomic" in op2) or "_rtn" in op2
+            if ld2 and vset(w2) & srcc:
+                if (idx, k2) not in out or ws < out[(idx, k2)][1]:
+                    out[(idx, k2)] = ("LDSRC", ws, horizon, ln, op, ln2, l2)
+                continue
+            if op2.startswith("v_") and not m2 and vset(w2) & srcc:   # WARc: interlocked VALU write
+                continue
+            stack.extend((k3, ws + 1, steps + 1) for k3 in succ[k2])
+    return sorted(out.values(), key=lambda h: (h[3], h[5]))
+
+
 def scan(path, sym, window=24):
     """Hits of the first function whose name contains `sym` (round-3 interface), and its code."""
     fns = functions(path)

@@ -9,10 +9,10 @@ byte for byte, and the bench's headline mode is the library's default mode.
 - The consumer-side env step is instantiated only for the bf16 student (rollout_kernel<true, *,
   true>), whose f32 MFMAs (the exact teacher's) are SrcC-fenced.
 - Statically, in the product's ISA no LDS / global load is issued into a register that an
-  in-flight f32 MFMA (8 passes) still reads as SrcC: every such load comes >= 10 wait states
-  after the MFMA, i.e. after it completed -- the pattern that made the unfenced consumer-side
-  step lose loaded values in lanes 48-63 (scripts/isa/hazards.py, profiles/r03_srcc_probe_*.txt).
-  The split kernels (the default mode) have no f32 MFMA followed by such a load at all.
+  in-flight f32 MFMA (8 passes) still reads as SrcC unless an instruction in between forced the
+  MFMA to complete -- the pattern that made the unfenced consumer-side step lose loaded values in
+  lanes 48-63 (scripts/isa/hazards.py scan_ldsrc, profiles/r03_srcc_probe_*.txt); and no load
+  overwrites a source of an unread packed-f32 op (scan_pkwar), the rollout having none at all.
 """
 import ctypes
 import os
@@ -85,22 +85,23 @@ def product_isa():
 
 
 def test_no_load_into_an_inflight_f32_mfma_srcc(product_isa):
-    """The product's rollout kernels: every LDS / global load whose destination is the SrcC of an
-    earlier v_mfma_f32_16x16x4_f32 issues >= 10 wait states after it, i.e. after the MFMA
-    completed (the compiler's RAW wait for an 8-pass result, NumPasses + 2; ROCm 7.2 itself only
-    keeps 3-5 for this WAR).  In the split kernels no load follows an f32 MFMA into its SrcC
-    within the scan at all (their f32 MFMAs are dW1 only)."""
+    """VERDICT r5 item 1 (LDSRC by interlock, no distance exemption): in every function of every
+    product source, no LDS / global load writes a SrcC register of an exact-f32 MFMA
+    (v_mfma_f32_16x16x4_f32, 8 passes) within its NP + 6 wait-state horizon unless an instruction
+    in between forces that MFMA to complete (a VALU / memory read of its result, an MFMA reading it
+    as SrcA/B, an interlocked VALU write of the SrcC registers) -- hazards.py scan_ldsrc.  The
+    exact pair forward's per-site fences (distill.hip kPairFence) are what makes the exact-f32
+    rollout instances pass; the split (default) and bf16 instances pass unfenced."""
     hz = _hz()
-    out = product_isa["distill.hip"]
-    for sym, split in (("rollout_kernelILb0ELb0ELb0ELi0ELb0E", False), ("rollout_kernelILb0ELb1ELb0ELi0ELb0E", True),
-                       ("rollout_kernelILb1ELb0ELb1ELi0ELb0E", False), ("rollout_kernelILb1ELb1ELb1ELi0ELb0E", True),
-                       ("rollout_kernelILb0ELb0ELb0ELi2ELb0E", False), ("rollout_kernelILb0ELb1ELb0ELi2ELb0E", True),
-                       ("rollout_kernelILb0ELb0ELb0ELi0ELb1E", False), ("rollout_kernelILb0ELb1ELb0ELi0ELb1E", True),
-                       ("rollout_kernelILb1ELb0ELb0ELi0ELb1E", False), ("rollout_kernelILb1ELb1ELb0ELi0ELb1E", True)):
-        hits = [h for h in hz.scan(out, sym, 40)[0] if h[0] == "LDSRC" and "16x16x4" in h[4]]
-        assert all(h[1] >= 10 for h in hits), (sym, [h[:6] for h in hits if h[1] < 10][:5])
-        if split:
-            assert not hits, (sym, [h[:6] for h in hits][:5])
+    bad, nf32 = {}, 0
+    for src, path in product_isa.items():
+        for name, code in hz.functions(path).items():
+            nf32 += sum(1 for _, l in code if l.startswith("v_mfma_f32_16x16x4"))
+            hits = hz.scan_ldsrc(code)
+            if hits:
+                bad[f"{src}:{name}"] = [h[:6] for h in hits[:3]]
+    assert nf32 > 1000, nf32   # the scan saw the exact-f32 MFMAs (rollout, PPO, LSTM, reference student)
+    assert not bad, bad
 
 
 ROLLOUT_SYMS = ("rollout_kernelILb0ELb0ELb0ELi0ELb0E", "rollout_kernelILb0ELb1ELb0ELi0ELb0E",
@@ -112,24 +113,26 @@ ROLLOUT_SYMS = ("rollout_kernelILb0ELb0ELb0ELi0ELb0E", "rollout_kernelILb0ELb1EL
                 "rollout_kernelILb1ELb0ELb0ELi0ELb1E", "rollout_kernelILb1ELb1ELb0ELi0ELb1E")
 
 
-def test_no_packed_f32_accumulator_overwritten_by_a_load(product_isa):
-    """PKWAR (scripts/isa/hazards.py): in every rollout kernel no LDS / global load
-    overwrites a source of a packed-f32 op (v_pk_fma/mul/add_f32) that nothing has read yet, more
-    than 5 instructions after it.  The violating pattern was the SLP-packed dW3 accumulation at the
-    tile loop's latch (gw3b lanes 48-63 different run to run); distill.hip is built without SLP
-    (build.SRC_FLAGS) and the explicit f32x2 pairs (tanh, the operand splits) are consumed within a
-    few instructions (>= 200 repeated rollouts bitwise identical, tests/test_determinism_gpu.py)."""
+def test_no_packed_f32_op_in_the_rollout_and_no_pkwar_anywhere(product_isa):
+    """PKWAR (scripts/isa/hazards.py), closed by construction:
+    - the rollout kernels contain no packed-f32 instruction (v_pk_fma/mul/add_f32) at all: distill.hip
+      is built without SLP and its tanh / operand splits / partial-row sums are scalar code;
+    - in every function of every product source no LDS / global load overwrites a source of a
+      packed-f32 op that nothing has read yet (scan_pkwar, no distance exemption): ppo.hip,
+      student_mlp.hip and student_lstm.hip are built without SLP too (build.SRC_FLAGS)."""
     hz = _hz()
     fns = hz.functions(product_isa["distill.hip"])
     for sym in ROLLOUT_SYMS:
         name = next(n for n in fns if sym in n)
-        far = [h[:6] for h in hz.scan_pkwar(fns[name]) if h[1] > 5]
-        assert not far, (sym, far[:5])
-    # the PPO minibatch kernel keeps 38 gradient sums per thread across its tiles: built without
-    # SLP too (its SLP build had loads 14-46 instructions behind unread packed accumulators)
-    for name, code in hz.functions(product_isa["ppo.hip"]).items():
-        far = [h[:6] for h in hz.scan_pkwar(code) if h[1] > 5]
-        assert not far, (name, far[:5])
+        pk = [(ln, l) for ln, l in fns[name] if l.startswith(hz.PK_F32)]
+        assert not pk, (sym, pk[:5])
+    bad = {}
+    for src, path in product_isa.items():
+        for name, code in hz.functions(path).items():
+            hits = hz.scan_pkwar(code)
+            if hits:
+                bad[f"{src}:{name}"] = [h[:6] for h in hits[:3]]
+    assert not bad, bad
 
 
 def test_no_hazard_below_its_requirement_in_any_kernel(product_isa):
@@ -234,3 +237,18 @@ def test_bench_headline_mode_is_the_library_default(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     args = bench.parse()
     assert (args.f32_mode == "split") == DistillConfig().f32_split
+
+
+def test_interlock_scanners_positive_controls():
+    """scan_ldsrc / scan_pkwar report a load into an in-flight exact-f32 MFMA's SrcC (even at
+    NP + 3 wait states, which the pass-count rule accepts) and a load over an unread packed-f32
+    source; an instruction reading the producer's result in between (the interlock) clears both."""
+    hz = _hz()
+    mf = "v_mfma_f32_16x16x4_f32 v[0:3], v4, v5, v[8:11]"
+    late = [(1, mf), (2, "s_nop 10"), (3, "ds_read_b128 v[8:11], v6")]
+    assert [h[0] for h in hz.scan_ldsrc(late)] == ["LDSRC"]
+    assert not hz.scan_ldsrc([(1, mf), (2, "v_add_f32_e32 v7, v0, v7"), (3, "ds_read_b128 v[8:11], v6")])
+    assert not hz.scan_ldsrc([(1, mf), (2, "s_nop 15"), (3, "s_nop 15"), (4, "ds_read_b128 v[8:11], v6")])
+    pk = "v_pk_fma_f32 v[0:1], v[2:3], v[4:5], v[0:1]"
+    assert [h[0] for h in hz.scan_pkwar([(1, pk), (2, "s_nop 7"), (3, "ds_read_b64 v[2:3], v6")])] == ["PKWAR"]
+    assert not hz.scan_pkwar([(1, pk), (2, "v_mov_b32_e32 v7, v0"), (3, "ds_read_b64 v[2:3], v6")])

@@ -356,3 +356,28 @@ def test_persistent_kernels_many_steps_stay_in_step_with_per_step_path():
     assert np.array_equal(params["1"], params["1b"])   # fixed-order sums: deterministic
     d = np.abs(params["1"] - params["0"]).max()
     assert d <= 1e-4 * np.abs(params["0"]).max(), d
+
+
+def test_persistent_forward_past_256_steps_two_calls():
+    """the persistent forward's granule tags carry the unrolled step in their own
+    12-bit field (the old 8-bit phase let step 257 of one call pass for step 1 of the next).  At
+    T = 258 with 8 windows (persistent: B <= 32, T < 4,096) a trainer's second forward equals a
+    fresh trainer's first forward on the same inputs bitwise -- nothing of the first call is taken
+    for the second's -- and both agree with the per-step launches to f32 rounding (at 2,064 rows
+    the per-step input product tiles its k sum differently)."""
+    T, B = 258, 8
+    ob, prev, _ = _batch(T, B, 91)
+    ob2 = np.ascontiguousarray(ob[::-1])
+    tr = _trainer(T, B, "kl")
+    tr.forward(_t(ob), _t(prev))
+    y2, fin2 = tr.forward(_t(ob2), _t(prev))
+    y2, h2 = y2.cpu().numpy(), fin2[1].cpu().numpy()
+    tr.close()
+    tr = _trainer(T, B, "kl")
+    y1, fin1 = tr.forward(_t(ob2), _t(prev))
+    assert np.array_equal(y2, y1.cpu().numpy()) and np.array_equal(h2, fin1[1].cpu().numpy())
+    tr.close()
+    tr = _trainer(T, B, "kl", step_recurrence=True)
+    y0, _ = tr.forward(_t(ob2), _t(prev))
+    tr.close()
+    assert np.abs(y2 - y0.cpu().numpy()).max() <= 1e-5 * max(1.0, np.abs(y2).max())
