@@ -1,6 +1,8 @@
-"""The xGMI push exchange (include/reacher_comm.h rd_xcomm_*, csrc/rd_xgmi.hip) with two
-ranks: one per device where two are visible, else both on cuda:0 (IPC within one device;
-the same kernel, the peer's buffer mapped through hipIpcOpenMemHandle).  Checks: the SUM of
+"""The xGMI push exchange (include/reacher_comm.h rd_xcomm_*, csrc/rd_xgmi.hip) with 2, 4 and 8
+ranks (the N = 8 path rehearsed before an 8-GPU node runs it): one per device
+where enough are visible, else round-robin on the visible devices -- on a one-GPU box all on
+cuda:0 (IPC within one device; the same kernel, the peers' buffers mapped through
+hipIpcOpenMemHandle).  Checks: the SUM of
 known patterns (exact in f32: small integers), repeated across both buffer parities and a
 ragged length; the error word stays clear; and a DistillTrainer with the exchange bound
 reproduces the single-rank run over the whole batch (student within 1e-5 after 5 Adam steps:
@@ -75,22 +77,27 @@ def _rank(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_xgmi_exchange_two_ranks():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_xgmi_exchange(world):
+    """Exact sums over both epoch parities and ragged / unaligned lengths, a 3,000-exchange chain
+    whose replicas stay bitwise identical, and a trainer bound to the exchange that reproduces the
+    single-rank run over the whole batch (the shards' states concatenate to it)."""
     from reacherdistilation_amd.distill import DistillConfig, DistillTrainer
     out = mp.get_context("spawn").Manager().dict()
-    mp.start_processes(_rank, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
-    r0, r1 = out[0], out[1]
-    if r0[0] == "skip" or r1[0] == "skip":
-        pytest.skip(f"xGMI exchange unavailable here: {r0[1] if r0[0] == 'skip' else r1[1]}")
-    (_, s0, p0, st0, m0, same0), (_, s1, p1, st1, m1, same1) = r0, r1
-    assert all(s0) and all(s1), (s0, s1)
-    assert same0 and same1 and np.array_equal(p0, p1)
+    mp.start_processes(_rank, args=(world, _port(), out), nprocs=world, join=True, start_method="spawn")
+    rs = [out[r] for r in range(world)]
+    skip = [r for r in rs if r[0] == "skip"]
+    if skip:
+        pytest.skip(f"xGMI exchange unavailable here: {skip[0][1]}")
+    for r in rs:
+        assert all(r[1]), r[1]
+        assert r[5] and np.array_equal(r[2], rs[0][2])
     ref = DistillTrainer(DistillConfig(n_envs=N_GLOBAL, seed=7, lr=1e-3), device="cuda:0")
     for _ in range(STEPS):
         ref.step()
-    np.testing.assert_allclose(p0, ref.student_params().cpu().numpy(), atol=1e-5)
-    np.testing.assert_allclose(np.concatenate([st0, st1], axis=1), ref.env_state().cpu().numpy(), atol=1e-4)
-    np.testing.assert_allclose(m0[:, 3] + m1[:, 3], ref.metrics(STEPS)[:, 3])
+    np.testing.assert_allclose(rs[0][2], ref.student_params().cpu().numpy(), atol=1e-5)
+    np.testing.assert_allclose(np.concatenate([r[3] for r in rs], axis=1), ref.env_state().cpu().numpy(), atol=1e-4)
+    np.testing.assert_allclose(sum(r[4][:, 3] for r in rs), ref.metrics(STEPS)[:, 3])
     ref.close()
 
 
@@ -98,9 +105,9 @@ TIMEOUT_S, LATE_S = 2.0, 6.0
 
 
 def _late_rank(rank, world, port, out):
-    """Rank 1 reaches its third step LATE_S seconds after rank 0 (host skew past the
-    exchange's TIMEOUT_S deadline): rank 0's exchange times out and poisons both buffers, rank
-    1's then fails on the poison; neither applies Adam, and both raise on their next step."""
+    """The last rank reaches its third step LATE_S seconds after the others (host skew past the
+    exchange's TIMEOUT_S deadline): the others' exchanges time out and poison every buffer, the
+    late rank's then fails on the poison; no rank applies Adam, and all raise on their next step."""
     import time
 
     import torch.distributed as dist
@@ -125,7 +132,7 @@ def _late_rank(rank, world, port, out):
     torch.cuda.synchronize(dev)
     before = tr.student_params().cpu().numpy()
     dist.barrier()
-    if rank == 1:
+    if rank == world - 1:
         time.sleep(LATE_S)
     t0 = time.perf_counter()
     tr.step()            # rank 0: times out after TIMEOUT_S; rank 1: fails on the poison
@@ -146,16 +153,18 @@ def _late_rank(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_xgmi_exchange_late_peer_fails_both_ranks_and_skips_adam():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_xgmi_exchange_late_peer_fails_every_rank_and_skips_adam(world):
     out = mp.get_context("spawn").Manager().dict()
-    mp.start_processes(_late_rank, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
-    r0, r1 = out[0], out[1]
-    if r0[0] == "skip" or r1[0] == "skip":
-        pytest.skip(f"xGMI exchange unavailable here: {r0[1] if r0[0] == 'skip' else r1[1]}")
-    for r in (r0, r1):
+    mp.start_processes(_late_rank, args=(world, _port(), out), nprocs=world, join=True, start_method="spawn")
+    rs = [out[r] for r in range(world)]
+    skip = [r for r in rs if r[0] == "skip"]
+    if skip:
+        pytest.skip(f"xGMI exchange unavailable here: {skip[0][1]}")
+    for r in rs:
         _, before, after, errs, _ = r
         assert np.array_equal(before, after)          # Adam skipped: parameters unchanged
         assert all(e is not None for e in errs), errs  # rdd_step, rd_comm_check, the counters
-    assert np.array_equal(r0[1], r1[1])
-    assert TIMEOUT_S * 0.8 <= r0[4] < LATE_S + TIMEOUT_S   # rank 0 waited for its deadline
-    assert r1[4] < TIMEOUT_S                               # rank 1 failed at once on the poison
+        assert np.array_equal(before, rs[0][1])
+    assert TIMEOUT_S * 0.8 <= rs[0][4] < LATE_S + TIMEOUT_S   # an early rank waited for its deadline
+    assert rs[-1][4] < TIMEOUT_S                              # the late rank failed at once on the poison
