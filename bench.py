@@ -107,10 +107,12 @@ def parse():
                     help="at N = 1 skip the `workloads` object (configs 2, 3 and the config-5 shard at K = 1 and 50)")
     ap.add_argument("--no-strong-projection", action="store_true",
                     help="at N = 1 skip timing c4's 2/4/8-GPU strong shards (strong_projection)")
-    ap.add_argument("--teacher", default="synthetic", choices=["synthetic", "fitted"],
-                    help="fixed teacher of the run and its convergence legs: the seeded synthetic MlpPolicy, or the "
+    ap.add_argument("--teacher", default="synthetic", choices=["synthetic", "fitted", "ppo"],
+                    help="fixed teacher of the run and its convergence legs: the seeded synthetic MlpPolicy, the "
                          "reference teacher's structure fitted to the fixture's 1,050 teacher records "
-                         "(teacher.fit_teacher); the line carries a fitted-teacher convergence block either way")
+                         "(teacher.fit_teacher), or the teacher PPO-trained here with the reference's hyperparameters "
+                         "(teacher.ppo_teacher, teachers/ppo_teacher.ckpt); the line carries fitted- and PPO-teacher "
+                         "convergence blocks either way")
     return ap.parse_args()
 
 
@@ -670,6 +672,26 @@ def fitted_teacher(dev):
     return p, info
 
 
+def ppo_teacher_info(dev, episodes=1024):
+    """The committed PPO-trained teacher (teacher.ppo_teacher): its training record
+    (profiles/r06_ppo_teacher.json, scripts/train_ppo_teacher.py) and its mean-action 50-step return
+    measured in this run on fresh gym-seeded episodes, beside the reference teacher's -7.53."""
+    from reacherdistilation_amd.teacher import PPO_TEACHER, episode_returns, ppo_teacher
+    p = ppo_teacher()
+    r = episode_returns(p, episodes, seed=777, device=dev)
+    info = {"checkpoint": os.path.relpath(PPO_TEACHER, ROOT), "format": "TF1 V2 bundle, scope 'pi' (tf_checkpoint)",
+            "return_mean_this_run": float(r.mean()), "return_std_this_run": float(r.std()), "episodes": episodes,
+            "reference_teacher_return": -7.53}
+    rec = os.path.join(ROOT, "profiles", "r06_ppo_teacher.json")
+    if os.path.exists(rec):
+        with open(rec) as fh:
+            d = json.load(fh)
+        info["training"] = {"config": d["config"], "train_seconds": d["train_seconds"],
+                            "env_steps_per_s": d["env_steps_per_s_training"], "final": d["final"],
+                            "record": os.path.relpath(rec, ROOT)}
+    return p, info
+
+
 def teacher_ppo(dev, n=4096, T=50, mb=4096, iters=5):
     """The teacher's PPO iteration (csrc/ppo.hip): n envs x T steps of rollout, GAE,
     the filter update and 10 epochs of mb-row minibatch steps (two launches each), timed over
@@ -736,7 +758,7 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
                                       student_dtype=sdt, f32_split=split), device=dev, rank=rank, world_size=world,
                         comm=comm, teacher=teacher)
     t0 = time.perf_counter()
-    steps, mse, hit = 0, float("nan"), None
+    steps, mse, hit, first = 0, float("nan"), None, None
     if chunk is None:   # small batches: checked every 10 steps, as scripts/conv_sweep.py measures them
         chunk = 10 if n * world <= 256 else 100
     while steps < max_steps:
@@ -748,6 +770,8 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
         if world > 1:
             dist.all_reduce(mt)
         mse = float(mt[2] / (2 * mt[3]))
+        if first is None:   # the untrained student's MSE (the first check): how far the leg had to go
+            first = mse
         if mse < target:
             hit = steps
             break
@@ -763,7 +787,7 @@ def convergence(wl, n, sdt, dev, rank, world, lr, max_steps, target=1e-3, chunk=
             "reference_budget_opt_steps": budget, "reference_budget_env_steps": budget,
             "within_opt_step_budget": hit is not None and hit <= budget,
             "within_env_step_budget": env_steps is not None and env_steps <= budget,
-            "student_mse_final": mse, "opt_steps_run": steps, "seconds": el}
+            "student_mse_first_check": first, "student_mse_final": mse, "opt_steps_run": steps, "seconds": el}
 
 
 def convergence_driver(dev, lr, max_episodes=5000, target=1e-3, teacher=None):
@@ -784,6 +808,7 @@ def convergence_driver(dev, lr, max_episodes=5000, target=1e-3, teacher=None):
             "episodes": ds.num_episodes(), "env_steps_to_target": env_steps if hit else None,
             "opt_steps_to_target": 50 * len(losses) if hit else None, "reference_budget_env_steps": budget,
             "within_env_step_budget": hit and env_steps <= budget,
+            "student_mse_first_episode": losses[0] / 50 if losses else None,
             "student_mse_final": losses[-1] / 50 if losses else None, "seconds": el}
 
 
@@ -861,7 +886,9 @@ def main():
         else (None, None)
     if args.teacher == "fitted" and fitted is None:
         raise SystemExit("--teacher fitted needs tests/golden/reacher_fixture.npz")
-    teacher = fitted if args.teacher == "fitted" else None
+    ppo_t, ppo_info = ppo_teacher_info(dev) if ((args.conv_steps > 0 and world == 1) or args.teacher == "ppo") \
+        else (None, None)
+    teacher = fitted if args.teacher == "fitted" else ppo_t if args.teacher == "ppo" else None
     if args.conv_steps > 0:
         conv = convergence(wl, n, sdt, dev, rank, world, args.lr, args.conv_steps, comm=comm, split=split,
                            teacher=teacher)
@@ -1073,6 +1100,19 @@ def main():
                                                             args.conv_steps, split=split, teacher=fitted)
                 ft["convergence_reference_driver"] = convergence_driver(dev, args.lr, teacher=fitted)
             out["convergence_fitted_teacher"] = ft
+        if ppo_info is not None and world == 1 and args.conv_steps > 0:
+            # the north star's student action-MSE against the teacher PPO-trained here
+            pt = {"teacher": ppo_info}
+            if args.teacher == "ppo":
+                pt["convergence"], pt["convergence_small_batch"] = conv, conv_small
+                pt["convergence_reference_driver"] = out["convergence_reference_driver"]
+            else:
+                pt["convergence"] = convergence(wl, n, sdt, dev, 0, 1, args.lr, args.conv_steps, split=split,
+                                                teacher=ppo_t)
+                pt["convergence_small_batch"] = convergence(wl, args.conv_small_envs, sdt, dev, 0, 1, args.lr,
+                                                            args.conv_steps, split=split, teacher=ppo_t)
+                pt["convergence_reference_driver"] = convergence_driver(dev, args.lr, teacher=ppo_t)
+            out["convergence_ppo_teacher"] = pt
         out["roofline_env"] = env_roofline(dev)
         ceil = copy_ceiling()
         if ceil is not None:   # the float4 copy measured in this run

@@ -14,7 +14,8 @@ baselines (commit 3900f2a, not in /root/reference; restated from its published a
     1 + e) A)), e = clip_param * lrmult; vf_loss = mean((V - ret)^2); A standardized over
     the actor batch; entcoeff 0.  TF gradient conventions: min() passes to its first
     argument on ties; clip passes inside the closed interval.
-  * MpiAdam: the TF1 form (a = lr sqrt(1 - b2^t) / (1 - b1^t), eps outside the sqrt) on the
+  * MpiAdam (epsilon 1e-5, learn()'s adam_epsilon default): the TF1 form (a = lr sqrt(1 -
+    b2^t) / (1 - b1^t), eps outside the sqrt) on the
     concatenated trainable vector [pol | vf] with stepsize optim_stepsize * lrmult,
     lrmult = max(1 - timesteps_so_far / max_timesteps, 0).
 Parameter vectors here: pol = the 5,060-float MlpPolicy layout of policy_np (W1 b1 W2 b2

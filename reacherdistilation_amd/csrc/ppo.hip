@@ -837,6 +837,10 @@ int run_rollout(rdp_trainer* t) {
     return RD_OK;
 }
 
+// MpiAdam's epsilon: pposgd_simple.learn(..., adam_epsilon=1e-5) (baselines ppo1; the reference's
+// teacher.py:30-36 call leaves it at that default), not tf.train.AdamOptimizer's 1e-8
+constexpr float kAdamEps = 1e-5f;
+
 int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
     const int mb = t->mb;
     const int ntiles = (mb + MB_R - 1) / MB_R, G = ntiles < MB_G ? ntiles : MB_G;
@@ -845,7 +849,7 @@ int minibatch(rdp_trainer* t, const int* perm, bool last_epoch) {
     hipLaunchKernelGGL(minibatch_kernel, dim3((unsigned)G), dim3(256), 0, t->stream, a);
     RDP_CK(hipGetLastError(), "rdp minibatch_kernel");
     RaArgs r{t->mbpart, t->mbstat, G, t->grad, t->params, t->m, t->v, t->ctl, t->acc, last_epoch ? 1 : 0,
-             t->cfg.optim_stepsize * t->lrmult, 0.9f, 0.999f, 1e-8f};
+             t->cfg.optim_stepsize * t->lrmult, 0.9f, 0.999f, kAdamEps};
     hipLaunchKernelGGL(reduce_adam_kernel, dim3((P_ALL + RA_COLS - 1) / RA_COLS), dim3(RA_SLICES * RA_COLS), 0,
                        t->stream, r);
     RDP_CK(hipGetLastError(), "rdp reduce_adam_kernel");

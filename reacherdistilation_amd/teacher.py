@@ -3,8 +3,10 @@
   TeacherAgent (teacher.py:12-20)  -> policy.TeacherAgent (TF checkpoint or safetensors restore)
   train (:23-37, ppo1 learn)       -> ppo.train
   collect_reward (:39-62)          -> collect_reward below, batched over ``n_envs`` envs
-  (the restored teacher.ckpt)      -> fit_teacher below: the teacher's structure fitted to the
-                                      teacher records the reference ships (its checkpoint does not)
+  (the restored teacher.ckpt)      -> ppo_teacher below: the checkpoint ppo.train writes with the
+                                      reference's hyperparameters (teachers/ppo_teacher.ckpt), or
+                                      fit_teacher: the teacher's structure fitted to the teacher
+                                      records the reference ships (its checkpoint does not)
 
 ``collect_reward`` as committed cannot run (``TeaherAgent``, ``ob_ph``, ``t_pdflat``,
 ``reward`` and ``Dataset`` are undefined there).  Its evident intent -- the teacher's mean
@@ -21,6 +23,8 @@ store attached, full pages of MAX_CAPACITY episodes are written as the drivers d
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -32,7 +36,39 @@ from .pages import PageStore
 from .policy import MlpPolicyParams, TeacherAgent
 from .ppo import train  # noqa: F401  (teacher.train: PPO on the batched env)
 
-__all__ = ["TeacherAgent", "train", "collect_reward", "fit_teacher"]
+__all__ = ["TeacherAgent", "train", "collect_reward", "fit_teacher", "episode_returns", "ppo_teacher", "PPO_TEACHER"]
+
+# The teacher trained by PPO here (scripts/train_ppo_teacher.py): the reference's
+# teacher.train with its own hyperparameters (teacher.py:30-36; one env, 2,048-step actor batches,
+# 1e6 steps, 9.8 s on one MI355X), saved as the reference Saver's scope-'pi' checkpoint; mean
+# 50-step return of its mean action -4.61 over 4,096 fresh episodes against the reference
+# teacher's -7.53 on the fixture (profiles/r06_ppo_teacher.json)
+PPO_TEACHER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "teachers", "ppo_teacher.ckpt")
+
+
+def ppo_teacher(path: str = PPO_TEACHER) -> MlpPolicyParams:
+    """The committed PPO-trained teacher (TeacherAgent(restore=True, path=...).pi)."""
+    return TeacherAgent(restore=True, path=path).pi
+
+
+def episode_returns(teacher: MlpPolicyParams, episodes: int, seed: int = 0, device="cuda:0") -> np.ndarray:
+    """50-step returns (gym's episode reward: the 50 step rewards summed) of ``episodes`` fresh
+    gym-seeded envs (env i seeded seed + i) stepped with ``teacher``'s mean action, as the
+    reference's collect_reward steps the teacher (teacher.py:39-62).  The fixture's -7.53 sums each
+    episode's 50 recorded rewards, whose first is the previous episode's last: the
+    same quantity in expectation."""
+    dev = torch.device(device)
+    env = BatchedReacher(episodes, seed=seed, device=dev, reset="gym")
+    tq = DistillTrainer(DistillConfig(n_envs=64, seed=seed), device=dev, teacher=teacher)
+    ob = env.reset()
+    ret = torch.zeros(episodes, dtype=torch.float64, device=dev)
+    for _ in range(EPISODE_STEPS):
+        t, _ = tq.forward(ob, student=False)
+        ob, rew, _, _ = env.step(t[:, :ACSPACE_SHAPE].contiguous())
+        ret += rew.double()
+    env.close()
+    tq.close()
+    return ret.cpu().numpy()
 
 
 def fit_teacher(ob, t_pdflat, *, phases=((30_000, 1e-3), (20_000, 1e-4)), seed: int = 0, device="cuda:0",

@@ -165,3 +165,17 @@ def test_two_trainers_are_bitwise_equal():
     (p0, v0, b0, m0), (p1, v1, b1, m1) = runs
     assert torch.equal(p0, p1) and torch.equal(v0, v1) and torch.equal(b0, b1)
     np.testing.assert_array_equal(m0, m1)
+
+
+def test_committed_ppo_teacher_reaches_the_reference_teachers_return():
+    """the teacher PPO-trained with the reference's hyperparameters
+    (scripts/train_ppo_teacher.py, profiles/r06_ppo_teacher.json) and committed as the reference
+    Saver's scope-'pi' checkpoint restores through TeacherAgent, and its mean action's 50-step
+    return on 512 fresh gym-seeded episodes is at least the reference teacher's -7.53 (fixture)."""
+    from reacherdistilation_amd.policy import TeacherAgent
+    from reacherdistilation_amd.teacher import PPO_TEACHER, episode_returns, ppo_teacher
+    p = ppo_teacher()
+    q = TeacherAgent(restore=True, path=PPO_TEACHER).pi
+    assert np.array_equal(p.flat, q.flat) and p.flat.shape == (5060,)
+    r = episode_returns(p, 512, seed=31, device=DEV)
+    assert r.mean() >= -7.53, r.mean()
