@@ -7,13 +7,15 @@ set -o pipefail
 OUT=gpurun_out/r06j; mkdir -p $OUT; export TMPDIR=/tmp
 BARGS="--steps 100 --warmup 200 --no-workloads --no-cpu-baseline --no-exact-leg --accum 0 --conv-steps 0 --fixture-steps 0 --no-strong-projection"
 PARGS="--steps 20 --warmup 3 --no-workloads --no-cpu-baseline --no-exact-leg --accum 0 --conv-steps 0 --fixture-steps 0 --no-strong-projection"
-for WL in c2 c3 c5 c4; do
-  mkdir -p $OUT/$WL
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$WL/prof -o run -- python3 bench.py --workload $WL $BARGS > $OUT/$WL/bench.json 2> $OUT/$WL/prof.err || { tail $OUT/$WL/prof.err; exit 1; }
+for W in c2 c3 c5 c4 c4x; do
+  WL=${W%x}; MODE=$([ "$W" = "c4x" ] && echo exact || echo split)
+  mkdir -p $OUT/$W
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$W/prof -o run -- python3 bench.py --workload $WL --f32-mode $MODE $BARGS > $OUT/$W/bench.json 2> $OUT/$W/prof.err || { tail $OUT/$W/prof.err; exit 1; }
   for c in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA"; do
     t=$(echo $c | cut -d' ' -f1)
-    timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $OUT/$WL/pmc_$t -o run -- python3 bench.py --workload $WL $PARGS > $OUT/$WL/pmc_$t.log 2>&1 || { tail $OUT/$WL/pmc_$t.log; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $OUT/$W/pmc_$t -o run -- python3 bench.py --workload $WL --f32-mode $MODE $PARGS > $OUT/$W/pmc_$t.log 2>&1 || { tail $OUT/$W/pmc_$t.log; exit 1; }
   done
+  WL=$W
   python3 scripts/pmc_traffic.py $OUT/$WL/pmc_rollout.json "rollout_kernel" $OUT/$WL/pmc_*/ > /dev/null
   echo "$WL done"
 done
