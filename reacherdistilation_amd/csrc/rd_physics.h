@@ -79,6 +79,28 @@ __device__ __forceinline__ void sincos_acc(float x, float* s, float* c) {
 }
 
 
+// sin and cos of a JOINT-1 angle (q1, the RK4 stage angles, the held kinematics' kq1): the
+// hardware v_sin_f32 / v_cos_f32 (argument in revolutions).  Joint 1 is limited to +-3 rad (a soft
+// constraint: |q1| stays below ~3.2), where |error| <= 3.5e-7 (scripts/micro/trig_acc.hip; 9e-8
+// for sincos_acc): in the dynamics sin/cos(q1) enter M(q1) and the bias only through HC = 2.2e-4
+// beside the armature-dominated diagonal (a < 1e-10 relative change), in the fingertip and the
+// observation 0.11 sin / cos(q0 + q1) and sin / cos(q1) directly (< 4e-8 and 3.5e-7 absolute) --
+// 3 VALU instead of ~23.  Joint 0 is unlimited (|q0| reaches tens of rad within an episode, where
+// the hardware's f32 argument scaling costs ~|q0| 2^-24 rev), so q0 and kq0 keep sincos_acc.
+// kWideRange (the gym-API env, whose states a caller may set): beyond 512 rad sincos_acc (the
+// hardware's argument range is +-256 revolutions).
+template <bool kWideRange = true>
+__device__ __forceinline__ void sincos_q1(float x, float* s, float* c) {
+    FP_SOURCE_ROUNDING();
+    if (kWideRange && __builtin_expect(fabsf(x) > 512.0f, 0)) {
+        sincos_acc<true>(x, s, c);
+        return;
+    }
+    const float r = x * 0.159154943091895336f;   // 1 / (2 pi)
+    *s = __builtin_amdgcn_sinf(r);
+    *c = __builtin_amdgcn_cosf(r);
+}
+
 // One MuJoCo forward pass -> constrained qacc of the two arm dofs; (s, c) = sin, cos q1.
 __device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, float v1, float c0, float c1,
                                         float& a0, float& a1) {
@@ -115,7 +137,7 @@ template <bool kWideRange = true>
 __device__ __forceinline__ void qacc(float q1, float v0, float v1, float c0, float c1, float& a0, float& a1) {
     FP_SOURCE_ROUNDING();
     float s, c;
-    sincos_acc<kWideRange>(q1, &s, &c);
+    sincos_q1<kWideRange>(q1, &s, &c);
     qacc_sc(q1, s, c, v0, v1, c0, c1, a0, a1);
 }
 
@@ -141,7 +163,7 @@ __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
         const float v0d = v0 + h * k3a, v1d = v1 + h * k3b;
         kq0 = q0 + h * v0c;
         kq1 = q1 + h * v1c;
-        sincos_acc<kWideRange>(kq1, &s4, &c4);   // also the held kinematics' q1 after the 2nd substep
+        sincos_q1<kWideRange>(kq1, &s4, &c4);   // also the held kinematics' q1 after the 2nd substep
         qacc_sc(kq1, s4, c4, v0d, v1d, c0, c1, k4a, k4b);
         const float b1 = 1.0f / 6.0f, b2 = 1.0f / 3.0f;
         q0 += h * (v0 * b1 + v0b * b2 + v0c * b2 + v0d * b1);
@@ -176,7 +198,7 @@ __device__ __forceinline__ void observe(const State& st, float* ob) {
     FP_SOURCE_ROUNDING();
     float s0, c0, s1, c1;
     sincos_acc<kWideRange>(st.q0, &s0, &c0);
-    sincos_acc<kWideRange>(st.q1, &s1, &c1);
+    sincos_q1<kWideRange>(st.q1, &s1, &c1);
     ob[0] = c0; ob[1] = c1; ob[2] = s0; ob[3] = s1;
     ob[4] = st.tx; ob[5] = st.ty; ob[6] = st.v0; ob[7] = st.v1;
     ob[8] = st.dx; ob[9] = st.dy; ob[10] = 0.0f;
