@@ -619,51 +619,8 @@ __device__ __forceinline__ void split8(f32x4 lo, f32x4 hi, bf16x8 (&p)[3]) {
     p[2] = __builtin_bit_cast(bf16x8, q2);
 }
 
-// split1 on four values, as bit patterns whose high halves are the pieces (split8's arithmetic)
-__device__ __forceinline__ void split4(const float (&x)[4], uint32_t (&u0)[4], uint32_t (&u1)[4],
-                                       uint32_t (&u2)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) split_bits(x[i], u0[i], u1[i], u2[i]);
-}
 // one bf16 pair (lo = high half of a, hi = high half of b)
 __device__ __forceinline__ uint32_t pair_hi(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
-
-// dW2 += H1^T dZ2 over a tile's 16 envs (K = env) as f32 emulated on v_mfma_f32_16x16x32_bf16
-// (f32_split).  x[b][e] = H1[16b + j][env 4g + e], y[b][e] = dZ2[16b + j][env 4g + e]: lane
-// group g holds envs 4g..4g+3 and a K = 32 step carries two pieces of each of them (slots 2e,
-// 2e + 1 of the lane's eight), so the six products of order >= 2^-16 take three MFMAs per
-// block: x0y2 + x2y0, x0y1 + x1y1, x0y0 + x1y0 (smallest first) -- 48 bf16 MFMAs per tile
-// instead of 64 f32 ones, which on gfx950 hold the SIMD's VALU issue for their whole 32 cycles.
-__device__ __forceinline__ void dw2_split(const float (&x)[4][4], const float (&y)[4][4], f32x4 (&gW2)[4][4]) {
-    u32x4 a02[4], a01[4];
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-        uint32_t u0[4], u1[4], u2[4];
-        split4(x[mb], u0, u1, u2);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            a02[mb][e] = pair_hi(u0[e], u2[e]);
-            a01[mb][e] = pair_hi(u0[e], u1[e]);
-        }
-    }
-    uint32_t v0[4][4], v1[4][4], v2[4][4];
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) split4(y[nb], v0[nb], v1[nb], v2[nb]);
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb) {
-            u32x4 bq;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                bq[e] = q == 0 ? pair_hi(v2[nb][e], v0[nb][e]) : q == 1 ? pair_hi(v1[nb][e], v1[nb][e])
-                                                                       : pair_hi(v0[nb][e], v0[nb][e]);
-            const bf16x8 b = __builtin_bit_cast(bf16x8, bq);
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-                gW2[mb][nb] = mfma_k32(__builtin_bit_cast(bf16x8, q == 0 ? a02[mb] : a01[mb]), b, gW2[mb][nb]);
-        }
-}
 
 // acc += W . X over one K = 32 step from split pieces w[3] (A) and x[3] (B)
 __device__ __forceinline__ f32x4 mfma_split(const bf16x8 (&w)[3], const bf16x8 (&x)[3], f32x4 c) {
@@ -673,6 +630,40 @@ __device__ __forceinline__ f32x4 mfma_split(const bf16x8 (&w)[3], const bf16x8 (
     c = mfma_k32(w[1], x[0], c);
     c = mfma_k32(w[0], x[1], c);
     return mfma_k32(w[0], x[0], c);
+}
+
+// dW2 += H1^T dZ2 over a tile's 16 envs as f32 emulated on v_mfma_f32_32x32x16_bf16 (f32_split, f32
+// student): K = the tile's 16 envs (lane half h = lane >> 5 carries envs 8h .. 8h + 7), the 64 x 64
+// gradient as 2 x 2 blocks of 32 x 32 (C/D: column lane & 31, row (reg & 3) + 8 (reg >> 2) + 4 h).
+// x[mb][e] = H1[32 mb + (lane & 31)][env 8h + e], y[nb][e] = dZ2[32 nb + (lane & 31)][env 8h + e],
+// each split into its three bf16 pieces (split8); per block the six products of order >= 2^-16,
+// smallest first (mfma_split): 24 MFMAs of 32 cycles that hold the SIMD's VALU issue for 8 each,
+// where the round-5 16x16x32 form took 48 of 16 holding it for 8 (c4 75.2 -> 74.3 us per step,
+// c3 28.1 -> 27.8, profiles/r06p_dw2_32x32_ab.jsonl) --
+// half the held issue for the same MFMA time, and 17 % fewer VALU (no piece re-pairing).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mfma_32k16(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void dw2_split32(const float (&x)[2][8], const float (&y)[2][8], f32x16 (&g)[2][2]) {
+    bf16x8 xp[2][3], yp[2][3];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        split8(f32x4{x[b][0], x[b][1], x[b][2], x[b][3]}, f32x4{x[b][4], x[b][5], x[b][6], x[b][7]}, xp[b]);
+        split8(f32x4{y[b][0], y[b][1], y[b][2], y[b][3]}, f32x4{y[b][4], y[b][5], y[b][6], y[b][7]}, yp[b]);
+    }
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            f32x16 c = g[mb][nb];
+            c = mfma_32k16(xp[mb][2], yp[nb][0], c);
+            c = mfma_32k16(xp[mb][1], yp[nb][1], c);
+            c = mfma_32k16(xp[mb][0], yp[nb][2], c);
+            c = mfma_32k16(xp[mb][1], yp[nb][0], c);
+            c = mfma_32k16(xp[mb][0], yp[nb][1], c);
+            g[mb][nb] = mfma_32k16(xp[mb][0], yp[nb][0], c);
+        }
 }
 
 // Split-mode image of a net (offsets in floats): the small vectors first, then the three
@@ -709,7 +700,7 @@ __device__ __forceinline__ void ld_pieces(const float* L, int base, int o, bf16x
     for (int q = 0; q < 3; ++q) w[q] = *reinterpret_cast<const bf16x8*>(h + q * SP_PIECE + o);
 }
 
-// Layer 1 of a split image's net on v_mfma_f32_16x16x32_bf16 (f32 emulated, as dw2_split):
+// Layer 1 of a split image's net on v_mfma_f32_16x16x32_bf16 (f32 emulated by three-piece splits):
 // lane group g's inputs 4s + g (s < 3; input 11 is the bias input 1) as three pieces each, a
 // K = 32 step carrying two pieces of each input (slots 2s, 2s + 1), the six products of order
 // >= 2^-16 in three MFMAs per output block: w0z2 + w2z0, w0z1 + w1z1, w0z0 + w1z0.  12 bf16
@@ -1545,6 +1536,11 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         // partial sums: dW2, dW1 (+db1 in row 11), db2 (envs 4s+g of feature 16x+j), rewards
         f32x4 gW2[4][4], gW1[4];
         float gb2[4];
+        // f32 student, split mode: dW2 in 32 x 32 blocks (dw2_split32) and db2 of features 32 nb + (lane & 31)
+        // over the envs of this lane half
+        constexpr bool D32 = SPL && !BS;
+        f32x16 gW2s[2][2];
+        float gb2s[2] = {0.f, 0.f};
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
 #pragma unroll
@@ -1552,6 +1548,13 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             gW1[x] = f32x4{0.f, 0.f, 0.f, 0.f};
             gb2[x] = 0.0f;
         }
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) gW2s[x][y][r] = 0.0f;
+        const int c32 = lane & 31, h32 = lane >> 5;   // D32: the 32 x 32 operand / accumulator lane map
         // student filter of input j for the dW1 A operand (lane-constant)
         const float smu = j < 12 ? LS[SMU + j] : 0.0f, srs = j < 12 ? LS[SRS + j] : 0.0f;
         float met_r = 0.0f, met_n = 0.0f;   // CP: reward and env count of the envs this wave steps
@@ -1613,22 +1616,28 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                         acc[mb] = mfma_k32(ldbf8(LS + NB_W2B, (((s * 4 + g) * 4 + mb) * 16 + j) * 8), db, acc[mb]);
                 }
             } else {
-                // split: dW2 on split bf16 MFMAs, x[b][e] / y[b][e] over envs 4g+e (dw2_split);
+                // split: dW2 on split bf16 32x32x16 MFMAs, x32[b][e] / y32[b][e] over envs 8h+e (dw2_split32);
                 // exact: f32 MFMAs, x[s][b] / y[s][b] over env 4s+g (k-step s)
                 constexpr bool S2 = SPL;
-                float x[4][4], y[4][4];
+                float x[4][4], y[4][4];     // exact
+                float x32[2][8], y32[2][8];   // split: dw2_split32's operands
+                if constexpr (S2) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+#pragma unroll
+                        for (int b = 0; b < 2; ++b) {
+                            x32[b][e] = h1t[(8 * h32 + e) * SAS + 32 * b + c32];   // H1[32b + c][env 8h+e]
+                            y32[b][e] = dzt[(8 * h32 + e) * SAS + 32 * b + c32];   // dZ2[32b + c][env 8h+e]
+                        }
+                } else {
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
-                        if constexpr (S2) {
-                            x[b][s] = h1t[(4 * g + s) * SAS + 16 * b + j];   // H1[16b + j][env 4g+s]
-                            y[b][s] = dzt[(4 * g + s) * SAS + 16 * b + j];   // dZ2[16b + j][env 4g+s]
-                        } else {
-                            x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
-                            y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
-                        }
+                        x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];   // H1[16b + j][env 4s+g]
+                        y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];   // dZ2[16b + j][env 4s+g]
                     }
+                }
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
                     H1[b] = ld4(h1t + j * SAS + 16 * b + 4 * g);   // accumulator layout
@@ -1645,11 +1654,13 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 if constexpr (S2) {
                     if constexpr (!HLP) {   // HLP: the helper pair's consumer takes dW2 and db2
 #pragma unroll
-                        for (int b = 0; b < 4; ++b) gb2[b] += (y[b][0] + y[b][1]) + (y[b][2] + y[b][3]);
+                        for (int b = 0; b < 2; ++b)
+                            gb2s[b] += ((y32[b][0] + y32[b][1]) + (y32[b][2] + y32[b][3])) +
+                                       ((y32[b][4] + y32[b][5]) + (y32[b][6] + y32[b][7]));
                     }
                     split8(dZ[0], dZ[1], dpre[0]);
                     split8(dZ[2], dZ[3], dpre[1]);
-                    if constexpr (!HLP) dw2_split(x, y, gW2);
+                    if constexpr (!HLP) dw2_split32(x32, y32, gW2s);
                 } else if constexpr (!HLP) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
@@ -1679,7 +1690,7 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                     }
                     __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
 #pragma unroll
-                    for (int i = 0; i < 80; ++i) {
+                    for (int i = 0; i < (HLP ? 48 : 72); ++i) {   // 24 dW2 (32x32x16) + 48 dH1 MFMAs
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
                     }
@@ -1772,24 +1783,29 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 if (ok) {
                     const float* h1t = OP + P_H1T;
                     const float* dzt = OP + P_DZT;
+                    if constexpr (SPL) {   // as the plain layout's consumer (dw2_split32)
+                        float x32[2][8], y32[2][8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+#pragma unroll
+                            for (int b = 0; b < 2; ++b) {
+                                x32[b][e] = h1t[(8 * h32 + e) * SAS + 32 * b + c32];
+                                y32[b][e] = dzt[(8 * h32 + e) * SAS + 32 * b + c32];
+                            }
+#pragma unroll
+                        for (int b = 0; b < 2; ++b)
+                            gb2s[b] += ((y32[b][0] + y32[b][1]) + (y32[b][2] + y32[b][3])) +
+                                       ((y32[b][4] + y32[b][5]) + (y32[b][6] + y32[b][7]));
+                        dw2_split32(x32, y32, gW2s);
+                    } else {
                     float x[4][4], y[4][4];
 #pragma unroll
                     for (int s = 0; s < 4; ++s)
 #pragma unroll
                         for (int b = 0; b < 4; ++b) {
-                            if constexpr (SPL) {
-                                x[b][s] = h1t[(4 * g + s) * SAS + 16 * b + j];
-                                y[b][s] = dzt[(4 * g + s) * SAS + 16 * b + j];
-                            } else {
-                                x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];
-                                y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];
-                            }
+                            x[s][b] = h1t[(4 * s + g) * SAS + 16 * b + j];
+                            y[s][b] = dzt[(4 * s + g) * SAS + 16 * b + j];
                         }
-                    if constexpr (SPL) {
-#pragma unroll
-                        for (int b = 0; b < 4; ++b) gb2[b] += (y[b][0] + y[b][1]) + (y[b][2] + y[b][3]);
-                        dw2_split(x, y, gW2);
-                    } else {
 #pragma unroll
                         for (int s = 0; s < 4; ++s) {
 #pragma unroll
@@ -1846,24 +1862,41 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         // ------------------------------------------------------------ this wave's share
 #pragma unroll
         for (int x = 0; x < 4; ++x) gb2[x] = xsum32(xsum16(gb2[x]));   // over the k-groups g
+#pragma unroll
+        for (int x = 0; x < 2; ++x) gb2s[x] = xsum32(gb2s[x]);          // D32: over the two lane halves
         if constexpr (CP) { met_r = wave_sum(met_r); met_n = wave_sum(met_n); }
         STAMP(6);
         __syncthreads();   // (one of the two barriers every wave meets) weights/scratch are free
         STAMP(9);
         float* R = lds + pair * RPAD;   // rows of RROW floats: W1|b1 rows 0..11, W2 rows 12..75
+        if constexpr (D32) {   // 32 x 32 blocks: column lane & 31, row (reg & 3) + 8 (reg >> 2) + 4 h
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        R[(12 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h32) * RROW + 32 * nb + c32] = gW2s[mb][nb][r];
+        } else {
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) R[(12 + 16 * mb + 4 * g + r) * RROW + 16 * nb + j] = gW2[mb][nb][r];
+        }
         if (g < 3) {   // rows 4g + r < 12: W1 rows 0..10 and b1 as row 11
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) R[(4 * g + r) * RROW + 16 * nb + j] = gW1[nb][r];
         }
-        if (g == 0) {
+        if constexpr (D32) {
+            if (h32 == 0) {
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) R[RSHIFT + P_B2 + 32 * nb + c32] = gb2s[nb];
+            }
+        } else if (g == 0) {
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb) R[RSHIFT + P_B2 + 16 * nb + j] = gb2[nb];
         }
