@@ -1113,6 +1113,24 @@ def main():
                                                             args.conv_steps, split=split, teacher=ppo_t)
                 pt["convergence_reference_driver"] = convergence_driver(dev, args.lr, teacher=ppo_t)
             out["convergence_ppo_teacher"] = pt
+        if conv is not None and world == 1:
+            # every convergence leg at a glance -- which reach the north star's
+            # action-MSE < 1e-3 within the reference's 250,000 env steps, against which teacher
+            legs = {}
+            for tname, blk in (("synthetic", out), ("fitted", out.get("convergence_fitted_teacher")),
+                               ("ppo", out.get("convergence_ppo_teacher"))):
+                if not blk:
+                    continue
+                if tname == "synthetic" and args.teacher != "synthetic":
+                    tname = args.teacher
+                for leg in ("convergence", "convergence_small_batch", "convergence_reference_driver"):
+                    c = blk.get(leg)
+                    if c:
+                        legs[f"{tname}/{leg.replace('convergence_', '').replace('convergence', 'headline_batch')}"] = {
+                            k: c.get(k) for k in ("envs_total", "env_steps_to_target", "within_env_step_budget",
+                                                  "student_mse_first_check", "student_mse_first_episode",
+                                                  "student_mse_final") if c.get(k) is not None}
+            out["student_mse_legs"] = legs
         out["roofline_env"] = env_roofline(dev)
         ceil = copy_ceiling()
         if ceil is not None:   # the float4 copy measured in this run

@@ -1536,9 +1536,9 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
         // partial sums: dW2, dW1 (+db1 in row 11), db2 (envs 4s+g of feature 16x+j), rewards
         f32x4 gW2[4][4], gW1[4];
         float gb2[4];
-        // f32 student, split mode: dW2 in 32 x 32 blocks (dw2_split32) and db2 of features 32 nb + (lane & 31)
-        // over the envs of this lane half
-        constexpr bool D32 = SPL && !BS;
+        // split mode and the bf16 student: dW2 in 32 x 32 blocks (v_mfma_f32_32x32x16_bf16) and db2 of
+        // features 32 nb + (lane & 31) over the envs of this lane half
+        constexpr bool D32 = SPL || BS;
         f32x16 gW2s[2][2];
         float gb2s[2] = {0.f, 0.f};
 #pragma unroll
@@ -1577,18 +1577,20 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
             f32x4 H1[4], dZ[4], acc[4];
             if constexpr (BS) {
                 // dW2 operands over the tile's envs 4g..4g+3 (K = 16 envs), rounded to bf16
-                s16x4 xa[4], yb[4];
+                // dW2 on v_mfma_f32_32x32x16_bf16 (as dw2_split32's layout, one product per block): K =
+                // the tile's 16 envs, lane half h32 carries envs 8h..8h+7, operands rounded to bf16
+                bf16x8 xa8[2], yb8[2];
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    float xv[4], yv[4];
+                for (int b = 0; b < 2; ++b) {
+                    float xv[8], yv[8];
 #pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        xv[jj] = h1t[(4 * g + jj) * SAS + 16 * b + j];   // H1[16b + j][env 4g+jj]
-                        yv[jj] = dzt[(4 * g + jj) * SAS + 16 * b + j];   // dZ2[16b + j][env 4g+jj]
+                    for (int e = 0; e < 8; ++e) {
+                        xv[e] = h1t[(8 * h32 + e) * SAS + 32 * b + c32];   // H1[32b + c][env 8h+e]
+                        yv[e] = dzt[(8 * h32 + e) * SAS + 32 * b + c32];   // dZ2[32b + c][env 8h+e]
                     }
-                    gb2[b] += (yv[0] + yv[1]) + (yv[2] + yv[3]);         // db2 partial (f32)
-                    xa[b] = pack4(xv[0], xv[1], xv[2], xv[3]);
-                    yb[b] = pack4(yv[0], yv[1], yv[2], yv[3]);
+                    gb2s[b] += ((yv[0] + yv[1]) + (yv[2] + yv[3])) + ((yv[4] + yv[5]) + (yv[6] + yv[7]));   // db2 (f32)
+                    xa8[b] = pack8(f32x4{xv[0], xv[1], xv[2], xv[3]}, f32x4{xv[4], xv[5], xv[6], xv[7]});
+                    yb8[b] = pack8(f32x4{yv[0], yv[1], yv[2], yv[3]}, f32x4{yv[4], yv[5], yv[6], yv[7]});
                 }
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
@@ -1602,9 +1604,9 @@ __global__ __launch_bounds__(BLOCK, 2) void rollout_kernel(RolloutArgs a) {
                 publish(flags + 1, ++tiles);
                 STAMP(13);
 #pragma unroll
-                for (int mb = 0; mb < 4; ++mb)
+                for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-                    for (int nb = 0; nb < 4; ++nb) gW2[mb][nb] = mfma_k16(xa[mb], yb[nb], gW2[mb][nb]);
+                    for (int nb = 0; nb < 2; ++nb) gW2s[mb][nb] = mfma_32k16(xa8[mb], yb8[nb], gW2s[mb][nb]);
                 // dH1 = W2 . dZ2: two K = 32 steps, dZ2 in accumulator layout = the B operand
 #pragma unroll
                 for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};

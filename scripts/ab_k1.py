@@ -14,6 +14,8 @@ from reacherdistilation_amd.distill import DistillConfig, DistillTrainer  # noqa
 WL = {"c2": dict(n_envs=4096), "c3": dict(n_envs=65536, loss="kl"), "c4": dict(n_envs=262144),
       "c4x": dict(n_envs=262144, f32_split=False), "c3x": dict(n_envs=65536, loss="kl", f32_split=False),
       "c5": dict(n_envs=131072, act_with="student", student_dtype="bf16"),
+      "c5x": dict(n_envs=131072, act_with="student", student_dtype="bf16", f32_split=False),
+      "k50_c5": dict(n_envs=131072, act_with="student", student_dtype="bf16", accum_steps=50),
       "k50_32768": dict(n_envs=32768, accum_steps=50), "k50_c3": dict(n_envs=65536, loss="kl", accum_steps=50)}
 
 
