@@ -86,7 +86,7 @@ __device__ __forceinline__ void sincos_acc(float x, float* s, float* c) {
 // beside the armature-dominated diagonal (a < 1e-10 relative change), in the fingertip and the
 // observation 0.11 sin / cos(q0 + q1) and sin / cos(q1) directly (< 4e-8 and 3.5e-7 absolute) --
 // 3 VALU instead of ~23.  Joint 0 is unlimited (|q0| reaches tens of rad within an episode, where
-// the hardware's f32 argument scaling costs ~|q0| 2^-24 rev), so q0 and kq0 keep sincos_acc.
+// the hardware's f32 argument scaling alone costs ~|q0| 2^-24 rev): sincos_q0 reduces it first.
 // kWideRange (the gym-API env, whose states a caller may set): beyond 512 rad sincos_acc (the
 // hardware's argument range is +-256 revolutions).
 template <bool kWideRange = true>
@@ -99,6 +99,27 @@ __device__ __forceinline__ void sincos_q1(float x, float* s, float* c) {
     const float r = x * 0.159154943091895336f;   // 1 / (2 pi)
     *s = __builtin_amdgcn_sinf(r);
     *c = __builtin_amdgcn_cosf(r);
+}
+
+// sin and cos of a JOINT-0 angle (the observation's q0, the held kinematics' kq0): joint 0 is
+// unlimited, so the angle is first reduced by 2 pi (Cody-Waite, two constants: k 6.28125 is exact
+// for |k| < 2^16, the second constant's rounding costs |k| 1e-10) to |r| <= pi, then the hardware
+// v_sin_f32 / v_cos_f32 of r in revolutions: |error| <= 3.5e-7 at any |q0| below 8192 rad (the
+// measured bound of sincos_q1's range), 9 VALU instead of ~23 for sincos_acc.  kWideRange: beyond
+// 8192 rad the libm path, as sincos_acc.  (env_reset keeps sincos_acc: once per episode.)
+template <bool kWideRange = true>
+__device__ __forceinline__ void sincos_q0(float x, float* s, float* c) {
+    FP_SOURCE_ROUNDING();
+    if (kWideRange && __builtin_expect(fabsf(x) > 8192.0f, 0)) {
+        sincosf(x, s, c);
+        return;
+    }
+    const float k = rintf(x * 0.159154943091895336f);     // 1 / (2 pi)
+    float r = __fmaf_rn(k, -6.28125f, x);                  // exact product
+    r = __fmaf_rn(k, -1.9353071795864769e-3f, r);          // 2 pi - 6.28125
+    const float u = r * 0.159154943091895336f;             // |u| <= 0.5 revolutions
+    *s = __builtin_amdgcn_sinf(u);
+    *c = __builtin_amdgcn_cosf(u);
 }
 
 // One MuJoCo forward pass -> constrained qacc of the two arm dofs; (s, c) = sin, cos q1.
@@ -172,7 +193,7 @@ __device__ __forceinline__ float env_step(State& st, float a0, float a1) {
         v1 += h * (k1b * b1 + k2b * b2 + k3b * b2 + k4b * b1);
     }
     float s0, c0k;
-    sincos_acc<kWideRange>(kq0, &s0, &c0k);
+    sincos_q0<kWideRange>(kq0, &s0, &c0k);
     const float s01 = __fmaf_rn(s0, c4, c0k * s4);    // sin(kq0 + kq1)
     const float c01 = __fmaf_rn(c0k, c4, -s0 * s4);   // cos(kq0 + kq1)
     st.q0 = q0; st.q1 = q1; st.v0 = v0; st.v1 = v1;
@@ -197,7 +218,7 @@ template <bool kWideRange = true>
 __device__ __forceinline__ void observe(const State& st, float* ob) {
     FP_SOURCE_ROUNDING();
     float s0, c0, s1, c1;
-    sincos_acc<kWideRange>(st.q0, &s0, &c0);
+    sincos_q0<kWideRange>(st.q0, &s0, &c0);
     sincos_q1<kWideRange>(st.q1, &s1, &c1);
     ob[0] = c0; ob[1] = c1; ob[2] = s0; ob[3] = s1;
     ob[4] = st.tx; ob[5] = st.ty; ob[6] = st.v0; ob[7] = st.v1;
