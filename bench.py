@@ -438,7 +438,10 @@ def _make_comm(kind, dev, world):
             c = RcclComm(dev)
         else:
             from reacherdistilation_amd.dist import XgmiComm
-            c = XgmiComm(dev)
+            # a 60-s deadline per wait (the library's default is 600 s): on a node where the IPC-mapped
+            # pushes do not arrive, the self-check fails within the driver's 600-s run instead of
+            # outlasting it, and the run goes on with RCCL (or torch's collective)
+            c = XgmiComm(dev, timeout=60.0)
         ok = c.self_check()
         if not ok:
             why = "self-check sum mismatch"
