@@ -87,13 +87,16 @@ __device__ __forceinline__ void sincos_acc(float x, float* s, float* c) {
 // observation 0.11 sin / cos(q0 + q1) and sin / cos(q1) directly (< 4e-8 and 3.5e-7 absolute) --
 // 3 VALU instead of ~23.  Joint 0 is unlimited (|q0| reaches tens of rad within an episode, where
 // the hardware's f32 argument scaling alone costs ~|q0| 2^-24 rev): sincos_q0 reduces it first.
-// kWideRange (the gym-API env, whose states a caller may set): beyond 512 rad sincos_acc (the
-// hardware's argument range is +-256 revolutions).
+// kWideRange (the gym-API env, whose states a caller may set): beyond |q1| = 4 rad -- past the
+// joint's limit, where that scaling error would grow to ~|q1| 2^-24 2 pi (3e-5 at 512 rad) --
+// sincos_q0's 2-pi reduction (and its libm path beyond 8192 rad).
+template <bool kWideRange = true>
+__device__ __forceinline__ void sincos_q0(float x, float* s, float* c);
 template <bool kWideRange = true>
 __device__ __forceinline__ void sincos_q1(float x, float* s, float* c) {
     FP_SOURCE_ROUNDING();
-    if (kWideRange && __builtin_expect(fabsf(x) > 512.0f, 0)) {
-        sincos_acc<true>(x, s, c);
+    if (kWideRange && __builtin_expect(fabsf(x) > 4.0f, 0)) {
+        sincos_q0<true>(x, s, c);
         return;
     }
     const float r = x * 0.159154943091895336f;   // 1 / (2 pi)
@@ -107,7 +110,7 @@ __device__ __forceinline__ void sincos_q1(float x, float* s, float* c) {
 // v_sin_f32 / v_cos_f32 of r in revolutions: |error| <= 3.5e-7 at any |q0| below 8192 rad (the
 // measured bound of sincos_q1's range), 9 VALU instead of ~23 for sincos_acc.  kWideRange: beyond
 // 8192 rad the libm path, as sincos_acc.  (env_reset keeps sincos_acc: once per episode.)
-template <bool kWideRange = true>
+template <bool kWideRange>
 __device__ __forceinline__ void sincos_q0(float x, float* s, float* c) {
     FP_SOURCE_ROUNDING();
     if (kWideRange && __builtin_expect(fabsf(x) > 8192.0f, 0)) {

@@ -117,6 +117,38 @@ def test_step_matches_oracle_random(oracle_c, n):
                   atol=2e-4, rtol=1e-4)
 
 
+def test_joint_trig_over_wide_angles():
+    """obs[0:4] = cos q0, cos q1, sin q0, sin q1 of the post-step state, for angles far past an
+    episode's range (a caller may set any state): joint 0 -- unlimited -- up to 1e5 rad (the 2-pi
+    reduced hardware path below 8192 rad, libm above) and joint 1 set past its soft limit up to
+    2,000 rad (the hardware path within 4 rad, the joint-0 path beyond; rd_physics.h sincos_q0 /
+    sincos_q1).  Checked against numpy's f64 cos / sin of the f32 state the kernel wrote."""
+    from reacherdistilation_amd.env import BatchedReacher
+    n = 8192
+    rs = np.random.RandomState(17)
+    sgn = lambda: rs.choice([-1.0, 1.0], n)  # noqa: E731
+    q0 = sgn() * rs.choice([0.5, 3, 30, 300, 3000, 8000, 8191, 8300, 9000, 3e4, 1e5], n) * rs.uniform(0.97, 1.0, n)
+    q1 = sgn() * rs.choice([0.5, 2.9, 3.5, 5, 10, 100, 500, 600, 2000], n) * rs.uniform(0.98, 1.0, n)
+    st = np.zeros((8, n), np.float32)
+    st[0], st[1] = q0, q1
+    st[4], st[5] = 0.1, -0.1
+    env = BatchedReacher(n, device=DEV)
+    env.set_state(torch.from_numpy(st), step=3, episode=0)
+    o, r, _, _ = env.step(torch.zeros(n, 2, device=DEV))
+    o = o.cpu().numpy().astype(np.float64)
+    after = env.get_state()[0].cpu().numpy().astype(np.float64)
+    assert np.isfinite(after).all() and np.isfinite(o).all()
+    a0, a1 = np.abs(after[0]), np.abs(after[1])
+    # every path is exercised by the post-step angles
+    assert (a0 < 8192).any() and (a0 > 8192).any() and (a1 <= 4).any() and ((a1 > 4) & (a1 < 512)).any() \
+        and (a1 > 512).any()
+    tol = 1e-6   # hardware sin / cos <= 3.8e-7 after the reduction, whose second constant adds <= 1.3e-7 at 8192 rad
+    np.testing.assert_allclose(o[:, 0], np.cos(after[0]), atol=tol, rtol=0)
+    np.testing.assert_allclose(o[:, 2], np.sin(after[0]), atol=tol, rtol=0)
+    np.testing.assert_allclose(o[:, 1], np.cos(after[1]), atol=tol, rtol=0)
+    np.testing.assert_allclose(o[:, 3], np.sin(after[1]), atol=tol, rtol=0)
+
+
 def test_philox_resets_bit_exact(oracle_c):
     from reacherdistilation_amd.env import BatchedReacher
     n, seed, base = 5000, 1234, 77
