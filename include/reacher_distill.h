@@ -182,6 +182,10 @@ int rdd_forward(rdd_trainer* tr, const float* obs, int64_t n, float* t_pdflat, f
 
 /* Env state hooks (state [8][n_envs] SoA, see reacher.h). */
 int rdd_get_env_state(rdd_trainer* tr, float* state);
+/* rdd_set_env_state checks the caller's joint angles first (host-synchronising): the fused
+ * rollout's trig is exact for |q0| < 8192 and |q1| <= 4 rad (an episode's own states never
+ * leave that range); outside it, or not finite -> RD_EINVAL and the trainer's state is unchanged.
+ * The gym-API env (reacher.h rd_set_state) takes any state. */
 int rdd_set_env_state(rdd_trainer* tr, const float* state);
 
 /* Host-synchronising readers (they also report a timed-out producer/consumer hand-off

@@ -1964,6 +1964,18 @@ __global__ __launch_bounds__(256) void reset_state_kernel(int64_t n, int64_t env
     state[4 * n + i] = st.tx; state[5 * n + i] = st.ty; state[6 * n + i] = st.dx; state[7 * n + i] = st.dy;
 }
 
+// rdd_set_env_state's range check: the fused rollout takes its joint trig on the short paths
+// (rd_physics.h, kWideRange = false: joint 1 on the hardware within its limit, joint 0 reduced by
+// 2 pi below 8192 rad), which an episode's own states never leave; a caller's state outside that
+// range (or not finite) raises flag[0]
+__global__ __launch_bounds__(256) void check_state_kernel(int64_t n, const float* state, uint32_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float q0 = state[i], q1 = state[n + i];
+    if (!(fabsf(q0) < rd::kRolloutMaxQ0) || !(fabsf(q1) <= rd::kRolloutMaxQ1))
+        __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(256) void init_ctl_kernel(uint32_t* ctl, float b1, float b2) {
     if (threadIdx.x < 2) {
         const int o = 4 * threadIdx.x;   // live words and their snapshot
@@ -2462,7 +2474,21 @@ int rdd_get_env_state(rdd_trainer* t, float* state) {
 int rdd_set_env_state(rdd_trainer* t, const float* state) {
     if (!t || !state) return rd::set_error(RD_EINVAL, "rdd_set_env_state: null argument");
     rd::DeviceGuard g(t->device);
-    RD_HIP(hipMemcpyAsync(t->state, state, sizeof(float) * 8 * t->cfg.n_envs, hipMemcpyDeviceToDevice, t->stream),
+    // the caller's angles are checked before they replace the trainer's (ctl[14]: this check's flag)
+    const int64_t n = t->cfg.n_envs;
+    uint32_t bad = 0;
+    RD_HIP(hipMemsetAsync(t->ctl + 14, 0, sizeof(uint32_t), t->stream), "rdd_set_env_state");
+    hipLaunchKernelGGL(check_state_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, t->stream, n, state,
+                       t->ctl + 14);
+    RD_HIP(hipGetLastError(), "rdd_set_env_state: check_state_kernel launch");
+    RD_HIP(hipMemcpyAsync(&bad, t->ctl + 14, sizeof(bad), hipMemcpyDeviceToHost, t->stream), "rdd_set_env_state");
+    RD_HIP(hipStreamSynchronize(t->stream), "rdd_set_env_state");
+    if (bad)
+        return rd::set_error(RD_EINVAL,
+                             "rdd_set_env_state: a joint angle outside the fused rollout's range (|q0| < %g, |q1| <= %g "
+                             "rad, finite); the gym-API env (rd_set_state) takes any state",
+                             (double)rd::kRolloutMaxQ0, (double)rd::kRolloutMaxQ1);
+    RD_HIP(hipMemcpyAsync(t->state, state, sizeof(float) * 8 * n, hipMemcpyDeviceToDevice, t->stream),
            "rdd_set_env_state");
     return RD_OK;
 }

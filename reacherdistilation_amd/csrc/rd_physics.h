@@ -125,6 +125,13 @@ __device__ __forceinline__ void sincos_q0(float x, float* s, float* c) {
     *c = __builtin_amdgcn_cosf(u);
 }
 
+// The joint angles the kWideRange = false paths (the fused rollout) are exact for: joint 1 on the
+// hardware within its limit (+-3, soft: an episode stays within ~3.3), joint 0 reduced by 2 pi
+// below 8192 rad (an episode's 50 steps stay within ~200 rad).  rdd_set_env_state rejects a
+// caller's state outside them.
+constexpr float kRolloutMaxQ0 = 8192.0f;
+constexpr float kRolloutMaxQ1 = 4.0f;
+
 // One MuJoCo forward pass -> constrained qacc of the two arm dofs; (s, c) = sin, cos q1.
 __device__ __forceinline__ void qacc_sc(float q1, float s, float c, float v0, float v1, float c0, float c1,
                                         float& a0, float& a1) {

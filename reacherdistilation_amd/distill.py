@@ -347,6 +347,8 @@ class DistillTrainer:
         return st
 
     def set_env_state(self, st: torch.Tensor):
+        """Replace the envs' state ([8, n] SoA).  Raises NativeError for joint angles outside the
+        fused rollout's range (|q0| < 8192, |q1| <= 4 rad, finite; include/reacher_distill.h)."""
         st = st.to(self.device, torch.float32).contiguous()
         nat.check(self._lib.rdd_set_env_state(self._h, nat.ptr(st)), "rdd_set_env_state")
         torch.cuda.current_stream(self.device).synchronize()

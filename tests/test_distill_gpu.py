@@ -523,3 +523,26 @@ def test_each_env_contribution_isolated_bf16(loss):
         assert r.max() <= 1.0, (e, int(np.argmax(r)), float(r.max()))
     print(f"per-env bf16 {loss}: worst error / bound {worst:.3f}")
     tr.close()
+
+
+def test_set_env_state_rejects_angles_outside_the_rollout_range():
+    """The fused rollout's joint trig is exact for |q0| < 8192 and |q1| <= 4 rad
+    (include/reacher_distill.h): a caller's state outside that range, or not finite, raises and
+    leaves the trainer's state as it was; the edges of the range are taken."""
+    from reacherdistilation_amd import _native as nat
+    n = 300
+    tr = _trainer(n, seed=4)
+    st, _ = _limit_states(n, np.random.RandomState(8))
+    tr.set_env_state(torch.from_numpy(st))
+    before = tr.env_state().cpu().numpy()
+    for row, val in ((1, 4.5), (1, -100.0), (0, 8192.0), (0, -1e5), (1, np.nan), (0, np.inf)):
+        bad = st.copy()
+        bad[row, n - 1] = val
+        with pytest.raises(nat.NativeError, match="outside the fused rollout's range"):
+            tr.set_env_state(torch.from_numpy(bad))
+        assert np.array_equal(tr.env_state().cpu().numpy(), before)
+    edge = st.copy()
+    edge[0, 0], edge[1, 0], edge[0, 1], edge[1, 1] = 8191.0, 4.0, -8191.0, -4.0
+    tr.set_env_state(torch.from_numpy(edge))
+    assert np.array_equal(tr.env_state().cpu().numpy(), edge)
+    tr.close()
